@@ -1,0 +1,204 @@
+"""ORACLE -- TEST INFRASTRUCTURE ONLY.
+
+ctypes front-end to the CPU restatement in this directory (liboracle.so) and, when it
+was built in the survey container, to the genuine vendored iSWIFT (_ref/libiswift_ref.so).
+
+Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may import this
+package, and only as the checker / CPU baseline.  The product library never loads it.
+
+Reference anchors: problem assembly /root/reference/src/MPC_dist.cpp:81-321, closest
+obstacle :371-396, iSWIFT /root/reference/optimization/iSWIFT/src/Prime.c:127-230,
+NLP rows /root/reference/include/dec_vars_constr_cost.h:245-438, Bezier fit
+MPC_dist.cpp:784-855.
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+import subprocess
+from dataclasses import dataclass
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB = os.path.join(_HERE, "liboracle.so")
+_REF = os.path.join(_HERE, "_ref", "libiswift_ref.so")
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+
+class OrcParams(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int), ("C", ctypes.c_int), ("K_obs", ctypes.c_int), ("K_nbr", ctypes.c_int),
+                ("grav", ctypes.c_double), ("hcom", ctypes.c_double), ("Ts", ctypes.c_double), ("mu", ctypes.c_double),
+                ("Qw", ctypes.c_double), ("Pw", ctypes.c_double), ("Rw", ctypes.c_double), ("Sw", ctypes.c_double),
+                ("box", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
+                ("vsat", ctypes.c_double), ("tol", ctypes.c_double),
+                ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int), ("use_nlp", ctypes.c_int)]
+
+
+def build(force: bool = False) -> None:
+    """Compile liboracle.so (always possible) and, if /root/reference exists, _ref."""
+    if force or not os.path.exists(_LIB) or any(
+            os.path.getmtime(os.path.join(_HERE, f)) > os.path.getmtime(_LIB)
+            for f in os.listdir(_HERE) if f.endswith((".c", ".h"))):
+        subprocess.run(["make", "-s", "-C", _HERE, "all"], check=True)
+    if os.path.isdir("/root/reference/optimization/iSWIFT") and (force or not os.path.exists(_REF)):
+        subprocess.run(["make", "-s", "-C", _HERE, "ref"], check=True)
+
+
+_lib = None
+_ref = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB):
+            build()
+        _lib = ctypes.CDLL(_LIB)
+        _lib.orc_params_default.argtypes = [ctypes.POINTER(OrcParams), ctypes.c_int, ctypes.c_int]
+        for f in ("orc_nv", "orc_neq", "orc_mqp", "orc_mnlp"):
+            getattr(_lib, f).argtypes = [ctypes.POINTER(OrcParams)]
+            getattr(_lib, f).restype = ctypes.c_int
+    return _lib
+
+
+def ref_available() -> bool:
+    return os.path.exists(_REF)
+
+
+def ref_lib():
+    global _ref
+    if _ref is None:
+        _ref = ctypes.CDLL(_REF)
+        _ref.iswift_ref_solve.restype = ctypes.c_int
+        _ref.iswift_ref_solve_ccs.restype = ctypes.c_int
+    return _ref
+
+
+def params(N: int = 4, C: int = 4, **kw) -> OrcParams:
+    p = OrcParams()
+    lib().orc_params_default(ctypes.byref(p), N, C)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def sizes(p: OrcParams):
+    L = lib()
+    return (L.orc_nv(ctypes.byref(p)), L.orc_neq(ctypes.byref(p)), L.orc_mqp(ctypes.byref(p)),
+            L.orc_mnlp(ctypes.byref(p)))
+
+
+def _c(a, dtype=np.float64):
+    return np.ascontiguousarray(a, dtype=dtype)
+
+
+def _ptr(a):
+    return a.ctypes.data_as(_dp if a.dtype == np.float64 else _ip)
+
+
+def lip(p: OrcParams):
+    Ad = np.zeros(16); Bd = np.zeros(8)
+    lib().orc_lip(ctypes.byref(p), _ptr(Ad), _ptr(Bd))
+    return Ad.reshape(4, 4), Bd.reshape(4, 2)
+
+
+def build_qp(p: OrcParams, x0, ref, foot):
+    """Dense QP of MPC_dist.cpp:135-321. foot: (N, 2, C). Returns P(diag), c, A, b, G, h."""
+    nv, neq, mq, _ = sizes(p)
+    x0, ref, foot = _c(x0), _c(ref), _c(foot)
+    Pd = np.zeros(nv); c = np.zeros(nv); A = np.zeros((neq, nv)); b = np.zeros(neq)
+    G = np.zeros((mq, nv)); h = np.zeros(mq)
+    lib().orc_build_qp(ctypes.byref(p), _ptr(x0), _ptr(ref), _ptr(foot), _ptr(Pd), _ptr(c), _ptr(A), _ptr(b),
+                       _ptr(G), _ptr(h))
+    return Pd, c, A, b, G, h
+
+
+def qp_solve(Pd, c, A, b, G, h, maxit=25, tol=1e-6):
+    n = Pd.size; m = G.shape[0]; pp = A.shape[0]
+    x = np.zeros(n); q = np.zeros(n); it = ctypes.c_int()
+    arrs = [_c(a) for a in (Pd, c, A, b, G, h)]
+    f = lib().orc_qp_solve(n, m, pp, *[_ptr(a) for a in arrs], maxit, ctypes.c_double(tol), _ptr(x), _ptr(q),
+                           ctypes.byref(it))
+    return x, f, it.value, q
+
+
+def select_obstacles(p: OrcParams, x0, obstacles, nbr_state=None, self_idx=-1):
+    K = p.K_obs + p.K_nbr
+    obs = np.zeros((p.N, max(K, 1), 2)); eps = np.zeros(max(K, 1))
+    ob = _c(obstacles).reshape(-1, 2)
+    nb = _c(nbr_state if nbr_state is not None else np.zeros((0, 4))).reshape(-1, 4)
+    lib().orc_select_obstacles(ctypes.byref(p), _ptr(_c(x0)), _ptr(ob), ob.shape[0], _ptr(nb), nb.shape[0],
+                               self_idx, _ptr(obs), _ptr(eps))
+    return obs[:, :K], eps[:K]
+
+
+def nlp_solve(p: OrcParams, x0, foot, Pd, c, A, b, G, h, obs, eps, x_init):
+    n = Pd.size
+    x = np.zeros(n); it = ctypes.c_int()
+    obs = _c(obs); eps = _c(eps)
+    f = lib().orc_nlp_solve(ctypes.byref(p), _ptr(_c(x0)), _ptr(_c(foot)), *[_ptr(_c(a)) for a in (Pd, c, A, b, G, h)],
+                            _ptr(obs), _ptr(eps), _ptr(_c(x_init)), _ptr(x), ctypes.byref(it))
+    return x, f, it.value
+
+
+def solve_batch(p: OrcParams, x0, ref, foot, obstacles, nbr_state=None, agent_offset=0, nthreads=1):
+    """Whole run_NMPC hot path for a batch (agent-major arrays, see include/srbnmpc.h)."""
+    nv = sizes(p)[0]
+    x0 = _c(x0).reshape(-1, 4); A_ = x0.shape[0]
+    ref = _c(ref).reshape(A_, -1); foot = _c(foot).reshape(A_, -1)
+    ob = _c(obstacles).reshape(-1, 2)
+    nb = _c(nbr_state if nbr_state is not None else np.zeros((0, 4))).reshape(-1, 4)
+    xq = np.zeros((A_, nv)); x = np.zeros((A_, nv)); obj = np.zeros(A_)
+    st = np.zeros((A_, 2), np.int32); it = np.zeros((A_, 2), np.int32)
+    lib().orc_solve_batch(ctypes.byref(p), A_, _ptr(x0), _ptr(ref), _ptr(foot), _ptr(ob), ob.shape[0], _ptr(nb),
+                          nb.shape[0], agent_offset, _ptr(xq), _ptr(x), _ptr(obj), _ptr(st), _ptr(it), nthreads)
+    return dict(x_qp=xq, x=x, obj=obj, status=st, iters=it)
+
+
+def fit_bezier(buf, X):
+    a = np.zeros(20)
+    lib().orc_fit_bezier(_ptr(_c(buf)), _ptr(_c(X)), _ptr(a))
+    return a.reshape(4, 5)
+
+
+# ---------------------------------------------------------------- genuine iSWIFT (oracle/_ref)
+def iswift_ref(Pd, c, A, b, G, h, order: str = "qd"):
+    """Solve with the compiled vendored iSWIFT.  order='md': min-degree (like Eigen AMD,
+    iswift_qp.cpp:201-205); order='qd': quasi-definite z|x|y elimination order (no zero
+    pivots, so iSWIFT's +-1e-7 pivot regularisation ldl.c:320-321 never fires)."""
+    import scipy.sparse as sp
+    P = np.diag(Pd) if np.ndim(Pd) == 1 else Pd
+    n = P.shape[0]; m = G.shape[0]; pp = A.shape[0]
+    R = ref_lib()
+    if order == "md":
+        x = np.zeros(n); it = ctypes.c_int(); ts = ctypes.c_double(); tv = ctypes.c_double()
+        arrs = [_c(a) for a in (P, c, A, b, G, h)]
+        f = R.iswift_ref_solve(n, m, pp, *[_ptr(a) for a in arrs], _ptr(x), ctypes.byref(it), ctypes.byref(ts),
+                               ctypes.byref(tv))
+        return x, f, it.value
+    perm = np.r_[np.arange(n + pp, n + pp + m), np.arange(n), np.arange(n, n + pp)].astype(np.int32)
+    keep = []
+    args = []
+    for M in (P, A, G):
+        S = sp.csc_matrix(M); S.eliminate_zeros(); S.sort_indices()
+        trip = (_c(S.indptr, np.int32), _c(S.indices, np.int32), _c(S.data))
+        keep.append(trip)
+        args += [_ptr(trip[0]), _ptr(trip[1]), _ptr(trip[2])]
+    cc, hh, bb = _c(c).copy(), _c(h).copy(), _c(b).copy()
+    x = np.zeros(n); it = ctypes.c_int()
+    f = R.iswift_ref_solve_ccs(n, m, pp, *args, _ptr(cc), _ptr(hh), _ptr(bb), _ptr(perm), _ptr(x), ctypes.byref(it))
+    return x, f, it.value
+
+
+def iswift_ref_ccs(n, m, pp, Pjc, Pir, Ppr, Ajc, Air, Apr, Gjc, Gir, Gpr, c, h, b, perm):
+    R = ref_lib()
+    arrs = [_c(Pjc, np.int32), _c(Pir, np.int32), _c(Ppr), _c(Ajc, np.int32), _c(Air, np.int32), _c(Apr),
+            _c(Gjc, np.int32), _c(Gir, np.int32), _c(Gpr)]
+    cc, hh, bb = _c(c).copy(), _c(h).copy(), _c(b).copy()
+    pr = _c(perm, np.int32)
+    x = np.zeros(n); it = ctypes.c_int()
+    f = R.iswift_ref_solve_ccs(n, m, pp, *[_ptr(a) for a in arrs], _ptr(cc), _ptr(hh), _ptr(bb), _ptr(pr), _ptr(x),
+                               ctypes.byref(it))
+    return x, f, it.value

@@ -1,0 +1,251 @@
+/*
+ * ORACLE (test infrastructure only): NLP stage.
+ *
+ * The reference solves (MPC_dist.cpp:402-427, dec_vars_constr_cost.h:148-438)
+ *     min 0.5 x'Q_qp x + f'x   s.t.  Aeq x = beq,  Gineq x <= hineq,
+ *         (x_k - o_x)^2 + (y_k - o_y)^2 + s >= 1.9f     (obstacle "CBF" rows, :262-265)
+ *         -0.35f <= xdot_k, ydot_k <= 0.35f            (velocity rows, :270-279)
+ * with SNOPT 7.7.7 warm-started from the QP solution (ExVariables, :99).  SNOPT is
+ * proprietary and not vendored, so this stage is OUR algorithm: a Mehrotra
+ * predictor-corrector primal-dual interior-point method on the same rows, with the
+ * exact Lagrangian Hessian  Q_qp - 2 sum_j z_kj I(x_k, y_k)  and inertia correction
+ * Hl + delta*I whenever the reduced Hessian on null(Aeq) is not positive definite.
+ * The GPU kernel implements the same iteration in condensed (null-space) form; this
+ * oracle solves the full-space system [Hl + J'W^-1 J, A'; A, 0] by LU so that the two
+ * share no linear-algebra code.  Independent pin: KKT certificate + SciPy (tests/).
+ *
+ * Row order (mirrors NeqConstraints::GetValues): [Gineq rows | obstacle rows k-major
+ * (k*K + j) | velocity rows +xdot_k, +ydot_k, -xdot_k, -ydot_k].  Two-sided velocity
+ * bounds become two one-sided rows.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+typedef struct {
+    int n, p, mq, K, N, mo, mv, m;
+    const double *Pd, *c, *A, *b, *G, *h, *obs, *eps;
+    int *gnz; double *gval;
+} nlp_t;
+
+static void rows_eval(const nlp_t *P, const double *x, double *g, double *Jv /* [m][4] */, int *Ji /* [m][4] */)
+{
+    const int n = P->n;
+    for (int r = 0; r < P->mq; r++) {
+        double s = 0;
+        for (int k = 0; k < 4; k++) {
+            int j = P->gnz[4 * r + k];
+            Ji[4 * r + k] = j; Jv[4 * r + k] = P->gval[4 * r + k];
+            if (j >= 0) s += P->gval[4 * r + k] * x[j];
+        }
+        g[r] = s;
+    }
+    int r = P->mq;
+    for (int k = 0; k < P->N; k++)
+        for (int j = 0; j < P->K; j++, r++) {
+            double dx = x[4 * k] - P->obs[(k * P->K + j) * 2];
+            double dy = x[4 * k + 2] - P->obs[(k * P->K + j) * 2 + 1];
+            g[r] = -(dx * dx + dy * dy) - x[n - 1];
+            Ji[4 * r + 0] = 4 * k;     Jv[4 * r + 0] = -2 * dx;
+            Ji[4 * r + 1] = 4 * k + 2; Jv[4 * r + 1] = -2 * dy;
+            Ji[4 * r + 2] = n - 1;     Jv[4 * r + 2] = -1.0;
+            Ji[4 * r + 3] = -1;        Jv[4 * r + 3] = 0.0;
+        }
+    for (int sg = 1; sg >= -1; sg -= 2)
+        for (int comp = 1; comp <= 3; comp += 2)
+            for (int k = 0; k < P->N; k++, r++) {
+                g[r] = sg * x[4 * k + comp];
+                Ji[4 * r] = 4 * k + comp; Jv[4 * r] = sg;
+                for (int t = 1; t < 4; t++) { Ji[4 * r + t] = -1; Jv[4 * r + t] = 0; }
+            }
+}
+
+static double dotv(const double *a, const double *b, int n) { double s = 0; for (int i = 0; i < n; i++) s += a[i] * b[i]; return s; }
+static double steplen(const double *v, const double *dv, int m)
+{
+    double a = 1e10; int f = 0;
+    for (int i = 0; i < m; i++)
+        if (dv[i] < 0 && (-v[i] / dv[i]) < a) { a = -(v[i] / dv[i]); f = 1; }
+    return f ? a : 1.0;
+}
+
+/* null-space basis of Aeq by forward rollout (used only for the PD test) */
+static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, int nz)
+{
+    const int N = pp->N, C = pp->C;
+    double Ad[16], Bd[8];
+    orc_lip(pp, Ad, Bd);
+    memset(Z, 0, sizeof(double) * (size_t)n * nz);
+    for (int j = 0; j < N; j++)
+        for (int i = 0; i < C - 1; i++) {
+            int col = j * (C - 1) + i;
+            double gg[2], v[4], t[4];
+            for (int d = 0; d < 2; d++) gg[d] = foot[(j * 2 + d) * C + i] - foot[(j * 2 + d) * C + C - 1];
+            Z[(size_t)(6 * N + C * j + i) * nz + col] = 1.0;
+            Z[(size_t)(6 * N + C * j + C - 1) * nz + col] = -1.0;
+            Z[(size_t)(4 * N + 2 * j) * nz + col] = gg[0];
+            Z[(size_t)(4 * N + 2 * j + 1) * nz + col] = gg[1];
+            for (int d = 0; d < 4; d++) v[d] = Bd[d * 2] * gg[0] + Bd[d * 2 + 1] * gg[1];
+            for (int k = j; k < N; k++) {
+                for (int d = 0; d < 4; d++) Z[(size_t)(4 * k + d) * nz + col] = v[d];
+                for (int d = 0; d < 4; d++) t[d] = Ad[d * 4] * v[0] + Ad[d * 4 + 1] * v[1] + Ad[d * 4 + 2] * v[2] + Ad[d * 4 + 3] * v[3];
+                memcpy(v, t, sizeof v);
+            }
+        }
+    Z[(size_t)(n - 1) * nz + nz - 1] = 1.0;
+}
+
+int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
+                  const double *Pd, const double *c, const double *A, const double *b,
+                  const double *G, const double *h,
+                  const double *obs, const double *eps,
+                  const double *x_init, double *x_out, int *iters_out)
+{
+    (void)x0;
+    nlp_t P;
+    P.N = pp->N; P.n = orc_nv(pp); P.p = orc_neq(pp); P.mq = orc_mqp(pp);
+    P.K = pp->K_obs + pp->K_nbr; P.mo = P.N * P.K; P.mv = 4 * P.N; P.m = P.mq + P.mo + P.mv;
+    P.Pd = Pd; P.c = c; P.A = A; P.b = b; P.G = G; P.h = h; P.obs = obs; P.eps = eps;
+    const int n = P.n, p = P.p, m = P.m, dim = n + p;
+    const int nz = P.N * (pp->C - 1) + 1;
+    P.gnz = malloc(sizeof(int) * 4 * P.mq); P.gval = malloc(sizeof(double) * 4 * P.mq);
+    for (int r = 0; r < P.mq; r++) {
+        int k = 0;
+        for (int j = 0; j < 4; j++) { P.gnz[4 * r + j] = -1; P.gval[4 * r + j] = 0; }
+        for (int j = 0; j < n && k < 4; j++)
+            if (G[(size_t)r * n + j] != 0.0) { P.gnz[4 * r + k] = j; P.gval[4 * r + k] = G[(size_t)r * n + j]; k++; }
+    }
+    double *hh = malloc(sizeof(double) * m);
+    for (int r = 0; r < P.mq; r++) hh[r] = h[r];
+    for (int r = 0; r < P.mo; r++) hh[P.mq + r] = -eps[r % P.K];
+    for (int r = 0; r < P.mv; r++) hh[P.mq + P.mo + r] = pp->vsat;
+
+    double *x = malloc(sizeof(double) * n), *q = calloc(n, sizeof(double));
+    double *s = malloc(sizeof(double) * m), *z = malloc(sizeof(double) * m);
+    double *g = malloc(sizeof(double) * m), *Jv = malloc(sizeof(double) * 4 * m);
+    int *Ji = malloc(sizeof(int) * 4 * m);
+    double *rx = malloc(sizeof(double) * n), *ry = malloc(sizeof(double) * (p + 1)), *rz = malloc(sizeof(double) * m);
+    double *lam = malloc(sizeof(double) * m), *wgt = malloc(sizeof(double) * m), *ds = malloc(sizeof(double) * m);
+    double *dsv = malloc(sizeof(double) * m), *dz = malloc(sizeof(double) * m), *r3 = malloc(sizeof(double) * m);
+    double *K = malloc(sizeof(double) * dim * dim), *Hl = malloc(sizeof(double) * n * n);
+    double *rhs = malloc(sizeof(double) * dim), *dx = malloc(sizeof(double) * n), *dq = malloc(sizeof(double) * n);
+    double *Z = malloc(sizeof(double) * (size_t)n * nz), *Hr = malloc(sizeof(double) * nz * nz), *HZ = malloc(sizeof(double) * (size_t)n * nz);
+    int *piv = malloc(sizeof(int) * dim);
+    int flag = 2, it = 0;
+    build_Z(pp, foot, Z, n, nz);
+
+    memcpy(x, x_init, sizeof(double) * n);
+    rows_eval(&P, x, g, Jv, Ji);
+    {   /* slacks: iSWIFT-style shift of h - g(x); duals 1 */
+        double mn = hh[0] - g[0];
+        for (int r = 1; r < m; r++) if (hh[r] - g[r] < mn) mn = hh[r] - g[r];
+        double ap = -mn;
+        for (int r = 0; r < m; r++) { s[r] = (ap < 0) ? hh[r] - g[r] : hh[r] - g[r] + (1 + ap); z[r] = 1.0; }
+    }
+    {   /* q = A'y, y = argmin |A'y + (Px + c + J'z)|  ->  (A A') y = -A v */
+        double *v = malloc(sizeof(double) * n), *AAt = malloc(sizeof(double) * (p ? p * p : 1)), *yy = malloc(sizeof(double) * (p + 1));
+        for (int j = 0; j < n; j++) v[j] = Pd[j] * x[j] + c[j];
+        for (int r = 0; r < m; r++) for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) v[Ji[4 * r + t]] += Jv[4 * r + t] * z[r];
+        for (int i = 0; i < p; i++) {
+            for (int j = 0; j < p; j++) AAt[i * p + j] = dotv(A + (size_t)i * n, A + (size_t)j * n, n);
+            yy[i] = -dotv(A + (size_t)i * n, v, n);
+        }
+        orc_chol(p, AAt); orc_chol_solve(p, AAt, yy);
+        for (int j = 0; j < n; j++) { double sacc = 0; for (int i = 0; i < p; i++) sacc += A[(size_t)i * n + j] * yy[i]; q[j] = sacc; }
+        free(v); free(AAt); free(yy);
+    }
+
+    const double tol = pp->tol, th = tol / sqrt(3.0);
+    for (int iter = 0; iter < pp->nlp_maxit; iter++) {
+        rows_eval(&P, x, g, Jv, Ji);
+        for (int j = 0; j < n; j++) rx[j] = -(Pd[j] * x[j] + c[j]) - q[j];
+        for (int r = 0; r < m; r++) for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) rx[Ji[4 * r + t]] -= Jv[4 * r + t] * z[r];
+        for (int k = 0; k < p; k++) ry[k] = b[k] - dotv(A + (size_t)k * n, x, n);
+        for (int r = 0; r < m; r++) rz[r] = hh[r] - s[r] - g[r];
+        double nrx = sqrt(dotv(rx, rx, n)), nrz = sqrt(dotv(rz, rz, m)), nry = sqrt(dotv(ry, ry, p));
+        double sz = dotv(s, z, m);
+        if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
+        if (nrx < th && nrz < th && nry < th && sz / m < tol) { flag = 0; break; }
+        for (int r = 0; r < m; r++) { lam[r] = sqrt(s[r] * z[r]); wgt[r] = s[r] / z[r]; }
+        double mu = dotv(lam, lam, m) / m;
+
+        /* Hl + J'W^-1 J (full space) */
+        memset(Hl, 0, sizeof(double) * n * n);
+        for (int j = 0; j < n; j++) Hl[j * n + j] = Pd[j];
+        for (int k = 0; k < P.N; k++) {
+            double zs = 0;
+            for (int j = 0; j < P.K; j++) zs += z[P.mq + k * P.K + j];
+            Hl[(4 * k) * n + 4 * k] -= 2 * zs; Hl[(4 * k + 2) * n + 4 * k + 2] -= 2 * zs;
+        }
+        for (int r = 0; r < m; r++) {
+            double iw = 1.0 / wgt[r];
+            for (int a = 0; a < 4; a++) {
+                int ia = Ji[4 * r + a]; if (ia < 0) continue;
+                for (int bb = 0; bb < 4; bb++) { int ib = Ji[4 * r + bb]; if (ib < 0) continue; Hl[ia * n + ib] += iw * Jv[4 * r + a] * Jv[4 * r + bb]; }
+            }
+        }
+        /* inertia correction: reduced Hessian Z'(H + delta I)Z must be PD */
+        double delta = 0.0; int ok = 0;
+        for (int tries = 0; tries < 14; tries++) {
+            for (int i = 0; i < n; i++)
+                for (int a = 0; a < nz; a++) {
+                    double sacc = 0;
+                    for (int j = 0; j < n; j++) sacc += Hl[i * n + j] * Z[(size_t)j * nz + a];
+                    HZ[(size_t)i * nz + a] = sacc + delta * Z[(size_t)i * nz + a];
+                }
+            for (int a = 0; a < nz; a++)
+                for (int bb = 0; bb < nz; bb++) {
+                    double sacc = 0;
+                    for (int i = 0; i < n; i++) sacc += Z[(size_t)i * nz + a] * HZ[(size_t)i * nz + bb];
+                    Hr[a * nz + bb] = sacc;
+                }
+            if (orc_chol(nz, Hr) == 0) { ok = 1; break; }
+            delta = (delta == 0.0) ? 1e-4 : delta * 10.0;
+        }
+        if (!ok) { flag = 1; break; }
+        /* full-space KKT [H + delta I, A'; A, 0] */
+        memset(K, 0, sizeof(double) * dim * dim);
+        for (int i = 0; i < n; i++) { for (int j = 0; j < n; j++) K[i * dim + j] = Hl[i * n + j]; K[i * dim + i] += delta; }
+        for (int k = 0; k < p; k++) for (int j = 0; j < n; j++) { K[(n + k) * dim + j] = A[(size_t)k * n + j]; K[j * dim + n + k] = A[(size_t)k * n + j]; }
+        if (orc_lu(dim, K, piv)) { flag = 1; break; }
+
+        for (int pass = 0; pass < 2; pass++) {
+            if (pass == 0) for (int r = 0; r < m; r++) ds[r] = -lam[r] * lam[r];
+            for (int r = 0; r < m; r++) r3[r] = rz[r] - ds[r] / z[r];
+            for (int j = 0; j < n; j++) rhs[j] = rx[j];
+            for (int r = 0; r < m; r++) for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) rhs[Ji[4 * r + t]] += Jv[4 * r + t] * r3[r] / wgt[r];
+            for (int k = 0; k < p; k++) rhs[n + k] = ry[k];
+            orc_lu_solve(dim, K, piv, rhs);
+            for (int j = 0; j < n; j++) dx[j] = rhs[j];
+            for (int r = 0; r < m; r++) {
+                double jd = 0;
+                for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) jd += Jv[4 * r + t] * dx[Ji[4 * r + t]];
+                dz[r] = (jd - r3[r]) / wgt[r];
+                dsv[r] = (ds[r] - s[r] * dz[r]) / z[r];
+            }
+            if (pass == 0) {
+                double ap = steplen(s, dsv, m), ad = steplen(z, dz, m), num = 0;
+                for (int r = 0; r < m; r++) num += (s[r] + ap * dsv[r]) * (z[r] + ad * dz[r]);
+                double rho = num / dotv(s, z, m), mr = rho < 1 ? rho : 1;
+                double sigma = mr * mr * mr; if (sigma < 0) sigma = 0;
+                for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) - dsv[r] * dz[r] + sigma * mu;
+            } else {
+                for (int j = 0; j < n; j++) dq[j] = 0;
+                for (int k = 0; k < p; k++) for (int j = 0; j < n; j++) dq[j] += A[(size_t)k * n + j] * rhs[n + k];  /* A' dy */
+            }
+        }
+        double ap = steplen(s, dsv, m), ad = steplen(z, dz, m);
+        ap = 0.99 * ap < 1.0 ? 0.99 * ap : 1.0;
+        ad = 0.99 * ad < 1.0 ? 0.99 * ad : 1.0;
+        for (int j = 0; j < n; j++) { x[j] += ap * dx[j]; q[j] += ad * dq[j]; }
+        for (int r = 0; r < m; r++) { s[r] += ap * dsv[r]; z[r] += ad * dz[r]; }
+        it++;
+    }
+    memcpy(x_out, x, sizeof(double) * n);
+    if (iters_out) *iters_out = it;
+    free(P.gnz); free(P.gval); free(hh); free(x); free(q); free(s); free(z); free(g); free(Jv); free(Ji);
+    free(rx); free(ry); free(rz); free(lam); free(wgt); free(ds); free(dsv); free(dz); free(r3); free(K); free(Hl);
+    free(rhs); free(dx); free(dq); free(Z); free(Hr); free(HZ); free(piv);
+    return flag;
+}

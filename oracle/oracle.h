@@ -1,0 +1,113 @@
+/*
+ * ORACLE -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement (plain C, fp64) of the reference's per-control-cycle NMPC path
+ *   MPC_dist::run_NMPC            /root/reference/src/MPC_dist.cpp:81-454
+ *   iSWIFT QP_SETUP/QP_SOLVE      /root/reference/optimization/iSWIFT/src/Prime.c:35-230
+ *   NLP rows (obstacle/velocity)  /root/reference/include/dec_vars_constr_cost.h:245-395
+ * Only tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg may load it,
+ * and only as the checker.  The product (srb-cbf-nmpc_amd/csrc) never links it.
+ *
+ * Linear algebra is deliberately FULL-SPACE and dense (Schur complement on the
+ * unreduced KKT for the QP stage, LU on [H A'; A 0] for the NLP stage) so that it
+ * shares no code path with the GPU kernel's condensed (null-space) linear algebra.
+ *
+ * Parity pins:
+ *   - QP stage == genuine vendored iSWIFT (oracle/_ref) -- same iteration count and
+ *     x to ~1e-10 under a quasi-definite elimination order;
+ *   - reconstructed print_file.out instance reproduces the reference's logged QP
+ *     output (SNOPT start point) to 5e-10;
+ *   - NLP stage (SNOPT in the reference; not vendored): KKT certificate + SciPy.
+ */
+#ifndef SRB_ORACLE_H
+#define SRB_ORACLE_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+typedef struct orc_params {
+    int N;          /* grid points in the horizon (reference: 4, MPC_dist.cpp:92)            */
+    int C;          /* stance contacts per grid (trot 2, stand 4; MPC_dist.cpp:132)          */
+    int K_obs;      /* nearest static obstacles per agent (reference: 1, MPC_dist.cpp:371-396) */
+    int K_nbr;      /* nearest neighbour agents used as moving obstacles (reference: 0)       */
+    double grav, hcom, Ts, mu;          /* 9.81, 0.29, 0.043, 0.7  (MPC_dist.cpp:90-104)      */
+    double Qw, Pw, Rw, Sw;              /* 300, 2000, 0.1, 3000    (MPC_dist.cpp:168-178)     */
+    double box;                         /* 1e3                     (MPC_dist.cpp:317-318)     */
+    double eps_obs, eps_nbr;            /* (double)1.9f, (double)2.2f (dec_vars_constr_cost.h:401-402) */
+    double vsat;                        /* (double)0.35f           (dec_vars_constr_cost.h:306) */
+    double tol;                         /* 1e-6                    (GlobalOptions.h:24-25)    */
+    int qp_maxit, nlp_maxit;            /* 25 (GlobalOptions.h:23), 50                        */
+    int use_nlp;                        /* MPC_dist::use_snopt                                */
+} orc_params;
+
+void orc_params_default(orc_params *p, int N, int C);
+
+/* sizes */
+int orc_nv(const orc_params *p);      /* (6+C)N+1                 */
+int orc_neq(const orc_params *p);     /* 7N                       */
+int orc_mqp(const orc_params *p);     /* 4(N-1)+12N+2CN           */
+int orc_mnlp(const orc_params *p);    /* mqp + 4N + N*(K_obs+K_nbr) */
+
+/* LIP discretisation, MPC_dist.cpp:99-127.  Ad row-major 4x4, Bd row-major 4x2. */
+void orc_lip(const orc_params *p, double Ad[16], double Bd[8]);
+
+/*
+ * Dense QP assembly exactly as MPC_dist.cpp:135-321, generalised to N grids and
+ * per-grid footholds foot[N][2][C] (the reference repeats one block, :1256-1260).
+ * Outputs (caller-allocated, row-major):
+ *   Pd[nv] (diagonal of Q_qp), c[nv], A[neq*nv], b[neq], G[mqp*nv], h[mqp]
+ */
+void orc_build_qp(const orc_params *p, const double x0[4], const double *ref, const double *foot,
+                  double *Pd, double *c, double *A, double *b, double *G, double *h);
+
+/*
+ * Per-grid obstacle list for the NLP rows (dec_vars_constr_cost.h:262-265 generalised):
+ * K_obs nearest static obstacles by current CoM position (MPC_dist.cpp:371-396; the
+ * strict '<' keeps the first index on ties) followed by K_nbr nearest other agents,
+ * each predicted at constant velocity to grid k: o_k = p + v*Ts*(k+1)
+ * (the intent of the commented line MPC_dist.cpp:391).
+ * obs_out[N][K][2], eps_out[K]; missing entries are parked far away (1e6).
+ */
+void orc_select_obstacles(const orc_params *p, const double x0[4],
+                          const double *obstacles, int n_obs,
+                          const double *nbr_state, int n_all, int self_idx,
+                          double *obs_out, double *eps_out);
+
+/* iSWIFT algorithm restated (Prime.c:127-230, Auxilary.c); returns 0..3 exit code. */
+int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
+                 const double *A, const double *b, const double *G, const double *h,
+                 int maxit, double tol, double *x_out, double *q_out, int *iters_out);
+
+/* NLP stage (replaces SnoptSolver::Solve, MPC_dist.cpp:402-427). */
+int orc_nlp_solve(const orc_params *p, const double x0[4], const double *foot,
+                  const double *Pd, const double *c, const double *A, const double *b,
+                  const double *G, const double *h,
+                  const double *obs, const double *eps,
+                  const double *x_init, double *x_out, int *iters_out);
+
+/* One agent end-to-end (run_NMPC minus planners): QP stage then (use_nlp) NLP stage. */
+int orc_solve_agent(const orc_params *p, const double x0[4], const double *ref, const double *foot,
+                    const double *obstacles, int n_obs, const double *nbr_state, int n_all, int self_idx,
+                    double *x_qp, double *x_out, double *obj, int status[2], int iters[2]);
+
+/* Agent batch on `nthreads` host threads (CPU baseline in bench.py). */
+int orc_solve_batch(const orc_params *p, int n_agents, const double *x0, const double *ref,
+                    const double *foot, const double *obstacles, int n_obs,
+                    const double *nbr_state, int n_all, int agent_offset,
+                    double *x_qp, double *x_out, double *obj, int *status, int *iters, int nthreads);
+
+/* fitComTrajectory_eventbase restated (MPC_dist.cpp:784-855): alpha[4][5] (row-major)
+ * from the buffer state (4) and the first 4 predicted states X[0..3]. */
+void orc_fit_bezier(const double buf[4], const double *X, double alpha[20]);
+
+/* dense helpers (linalg.c) */
+int orc_chol(int n, double *A);                               /* in place, lower */
+void orc_chol_solve(int n, const double *L, double *x);
+int orc_lu(int n, double *A, int *piv);
+void orc_lu_solve(int n, const double *LU, const int *piv, double *x);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

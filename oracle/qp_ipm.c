@@ -1,0 +1,232 @@
+/*
+ * ORACLE (test infrastructure only): the iSWIFT primal-dual interior-point method
+ * restated step for step from /root/reference/optimization/iSWIFT/src/Prime.c:127-230
+ * and src/Auxilary.c (kkt_initialize :680-755, computeresiduals :524-553,
+ * formlambda :462-465, form_ds :250-267, findsteplength :271-294, formrho :600-609,
+ * kktsolve_1/2 :334-398, updatevariables :224-227).
+ *
+ * Only the linear algebra differs: iSWIFT factors the sparse unreduced KKT
+ *     [P A' G'; A 0 0; G 0 -W]
+ * with a regularised up-looking LDL' (ldl.c:254-326); here the same system is solved
+ * densely by eliminating dz (W diagonal), then a Schur complement on dy with two
+ * Cholesky factorisations.  In exact arithmetic both give the same Newton step.
+ */
+#include <math.h>
+#include <stdlib.h>
+#include <string.h>
+#include "oracle.h"
+
+typedef struct {
+    int n, m, p;
+    const double *Pd, *A, *G;
+    int *gnz;      /* [m][4] column indices of row r's nonzeros (-1 padded) */
+    double *gval;  /* [m][4] */
+    double *H, *S, *HiAt, *t1, *t2;
+} kktws;
+
+static void ws_init(kktws *w, int n, int m, int p, const double *Pd, const double *A, const double *G)
+{
+    w->n = n; w->m = m; w->p = p; w->Pd = Pd; w->A = A; w->G = G;
+    w->gnz = (int *)malloc(sizeof(int) * 4 * (m ? m : 1));
+    w->gval = (double *)malloc(sizeof(double) * 4 * (m ? m : 1));
+    for (int r = 0; r < m; r++) {
+        int k = 0;
+        for (int j = 0; j < 4; j++) { w->gnz[4 * r + j] = -1; w->gval[4 * r + j] = 0; }
+        for (int j = 0; j < n && k < 4; j++)
+            if (G[(size_t)r * n + j] != 0.0) { w->gnz[4 * r + k] = j; w->gval[4 * r + k] = G[(size_t)r * n + j]; k++; }
+    }
+    w->H = (double *)malloc(sizeof(double) * n * n);
+    w->S = (double *)malloc(sizeof(double) * (p ? p * p : 1));
+    w->HiAt = (double *)malloc(sizeof(double) * (size_t)n * (p ? p : 1));
+    w->t1 = (double *)malloc(sizeof(double) * (n + p + m + 8));
+    w->t2 = (double *)malloc(sizeof(double) * (n + p + m + 8));
+}
+
+static void ws_free(kktws *w)
+{
+    free(w->gnz); free(w->gval); free(w->H); free(w->S); free(w->HiAt); free(w->t1); free(w->t2);
+}
+
+static void gmul(const kktws *w, const double *x, double *y)   /* y = G x */
+{
+    for (int r = 0; r < w->m; r++) {
+        double s = 0;
+        for (int k = 0; k < 4; k++) if (w->gnz[4 * r + k] >= 0) s += w->gval[4 * r + k] * x[w->gnz[4 * r + k]];
+        y[r] = s;
+    }
+}
+
+static void gtmul_add(const kktws *w, const double *v, double *y)   /* y += G' v */
+{
+    for (int r = 0; r < w->m; r++)
+        for (int k = 0; k < 4; k++) if (w->gnz[4 * r + k] >= 0) y[w->gnz[4 * r + k]] += w->gval[4 * r + k] * v[r];
+}
+
+/* factor for weights wgt (W = diag(wgt)); returns 0 on success */
+static int kkt_factor(kktws *w, const double *wgt)
+{
+    const int n = w->n, m = w->m, p = w->p;
+    double *H = w->H;
+    memset(H, 0, sizeof(double) * n * n);
+    for (int i = 0; i < n; i++) H[i * n + i] = w->Pd[i];
+    for (int r = 0; r < m; r++) {
+        double iw = 1.0 / wgt[r];
+        for (int a = 0; a < 4; a++) {
+            int ia = w->gnz[4 * r + a]; if (ia < 0) continue;
+            for (int bb = 0; bb < 4; bb++) {
+                int ib = w->gnz[4 * r + bb]; if (ib < 0) continue;
+                H[ia * n + ib] += iw * w->gval[4 * r + a] * w->gval[4 * r + bb];
+            }
+        }
+    }
+    if (orc_chol(n, H)) return -1;
+    for (int j = 0; j < p; j++) {
+        double *col = w->t1;
+        for (int i = 0; i < n; i++) col[i] = w->A[(size_t)j * n + i];
+        orc_chol_solve(n, H, col);
+        for (int i = 0; i < n; i++) w->HiAt[(size_t)i * p + j] = col[i];
+    }
+    for (int i = 0; i < p; i++)
+        for (int j = 0; j < p; j++) {
+            double s = 0;
+            for (int k = 0; k < n; k++) s += w->A[(size_t)i * n + k] * w->HiAt[(size_t)k * p + j];
+            w->S[i * p + j] = s;
+        }
+    if (p && orc_chol(p, w->S)) return -1;
+    return 0;
+}
+
+/* solve [P A' G'; A 0 0; G 0 -W][dx;dy;dz] = [r1;r2;r3] with the current factor */
+static void kkt_solve(kktws *w, const double *wgt, const double *r1, const double *r2, const double *r3,
+                      double *dx, double *dy, double *dz)
+{
+    const int n = w->n, m = w->m, p = w->p;
+    double *g = w->t1, *t = w->t2;
+    for (int i = 0; i < n; i++) g[i] = r1[i];
+    for (int r = 0; r < m; r++) t[r] = r3[r] / wgt[r];
+    gtmul_add(w, t, g);                                   /* g = r1 + G' W^-1 r3 */
+    for (int i = 0; i < n; i++) t[i] = g[i];
+    orc_chol_solve(n, w->H, t);                           /* t = H^-1 g */
+    for (int i = 0; i < p; i++) {
+        double s = 0;
+        for (int k = 0; k < n; k++) s += w->A[(size_t)i * n + k] * t[k];
+        dy[i] = s - r2[i];
+    }
+    if (p) orc_chol_solve(p, w->S, dy);                   /* dy = S^-1 (A H^-1 g - r2) */
+    for (int i = 0; i < n; i++) {
+        double s = g[i];
+        for (int j = 0; j < p; j++) s -= w->A[(size_t)j * n + i] * dy[j];
+        dx[i] = s;
+    }
+    orc_chol_solve(n, w->H, dx);                          /* dx = H^-1 (g - A' dy) */
+    gmul(w, dx, dz);
+    for (int r = 0; r < m; r++) dz[r] = (dz[r] - r3[r]) / wgt[r];
+}
+
+static double norm2(const double *v, int n) { double s = 0; for (int i = 0; i < n; i++) s += v[i] * v[i]; return sqrt(s); }
+static double dot(const double *a, const double *b, int n) { double s = 0; for (int i = 0; i < n; i++) s += a[i] * b[i]; return s; }
+
+/* findsteplength, Auxilary.c:271-294 */
+static double steplen(const double *v, const double *dv, int m)
+{
+    double a = 1e10; int f = 0;
+    for (int i = 0; i < m; i++)
+        if (dv[i] < 0 && (-v[i] / dv[i]) < a) { a = -(v[i] / dv[i]); f = 1; }
+    return f ? a : 1.0;
+}
+
+int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
+                 const double *A, const double *b, const double *G, const double *h,
+                 int maxit, double tol, double *x_out, double *q_out, int *iters_out)
+{
+    kktws w;
+    ws_init(&w, n, m, p, Pd, A, G);
+    double *x = calloc(n, sizeof(double)), *y = calloc(p + 1, sizeof(double));
+    double *s = calloc(m, sizeof(double)), *z = calloc(m, sizeof(double));
+    double *rx = calloc(n, sizeof(double)), *ry = calloc(p + 1, sizeof(double)), *rz = calloc(m, sizeof(double));
+    double *dx = calloc(n, sizeof(double)), *dy = calloc(p + 1, sizeof(double)), *dz = calloc(m, sizeof(double));
+    double *dsv = calloc(m, sizeof(double)), *ds = calloc(m, sizeof(double)), *lam = calloc(m, sizeof(double));
+    double *wgt = calloc(m, sizeof(double)), *r3 = calloc(m, sizeof(double)), *zi = calloc(m, sizeof(double));
+    double *nc = calloc(n, sizeof(double));
+    int flag = 3, it = 0;
+
+    /* kkt_initialize (Auxilary.c:680-755): W = I, rhs [-c; b; h] */
+    for (int r = 0; r < m; r++) wgt[r] = 1.0;
+    if (kkt_factor(&w, wgt)) { flag = 1; goto done; }
+    for (int i = 0; i < n; i++) nc[i] = -c[i];
+    kkt_solve(&w, wgt, nc, b, h, x, y, dz);
+    gmul(&w, x, zi);
+    for (int r = 0; r < m; r++) zi[r] = h[r] - zi[r];     /* z_inter = h - G x */
+    {
+        double mn = zi[0], mx = zi[0];
+        for (int r = 1; r < m; r++) { if (zi[r] < mn) mn = zi[r]; if (zi[r] > mx) mx = zi[r]; }
+        double ap = -mn, ad = mx;
+        for (int r = 0; r < m; r++) s[r] = (ap < 0) ? zi[r] : zi[r] + (1 + ap);
+        for (int r = 0; r < m; r++) z[r] = (ad < 0) ? -zi[r] : -zi[r] + (1 + ad);
+    }
+
+    double sigma = 100.0;                  /* options->sigma = SIGMA (GlobalOptions.h:26) */
+    const double sigma_d = 0.0;            /* iswift_qp.cpp:103 */
+    double alpha_p = 0, alpha_d = 0;
+    flag = 2;
+    for (int i = 0; i < maxit; i++) {
+        /* computeresiduals: rx = -Px - G'z - A'y - c; ry = -Ax + b; rz = -s - Gx + h */
+        for (int j = 0; j < n; j++) rx[j] = -Pd[j] * x[j] - c[j];
+        for (int r = 0; r < m; r++) lam[r] = -z[r];
+        gtmul_add(&w, lam, rx);
+        for (int k = 0; k < p; k++) {
+            double sy = 0;
+            for (int j = 0; j < n; j++) sy += A[(size_t)k * n + j] * x[j];
+            ry[k] = b[k] - sy;
+            for (int j = 0; j < n; j++) rx[j] -= A[(size_t)k * n + j] * y[k];
+        }
+        gmul(&w, x, rz);
+        for (int r = 0; r < m; r++) rz[r] = h[r] - s[r] - rz[r];
+        const double th = tol / sqrt(3.0);
+        if (norm2(rx, n) < th && norm2(rz, m) < th && (p == 0 || norm2(ry, p) < th) && dot(s, z, m) / m < tol) {
+            flag = 0; break;
+        }
+        for (int r = 0; r < m; r++) lam[r] = sqrt(s[r] * z[r]);
+        double mu = dot(lam, lam, m) / m;
+        if (sigma > sigma_d) {
+            /* updatekktmatrix(indicator 0) + ldl_numeric inside kktsolve_1 (Prime.c:165-177) */
+            for (int r = 0; r < m; r++) wgt[r] = s[r] / z[r];
+            if (kkt_factor(&w, wgt)) { flag = 1; break; }
+            for (int r = 0; r < m; r++) { ds[r] = -lam[r] * lam[r]; r3[r] = rz[r] - ds[r] / z[r]; }
+            kkt_solve(&w, wgt, rx, ry, r3, dx, dy, dz);       /* kktsolve_1: only dz, ds used */
+            for (int r = 0; r < m; r++) dsv[r] = (ds[r] - s[r] * dz[r]) / z[r];
+            alpha_p = steplen(s, dsv, m); alpha_d = steplen(z, dz, m);
+            double num = 0;
+            for (int r = 0; r < m; r++) num += (s[r] + alpha_p * dsv[r]) * (z[r] + alpha_d * dz[r]);
+            double rho = num / dot(s, z, m);
+            double mr = rho < 1 ? rho : 1;
+            sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
+            for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) - (dsv[r] * dz[r]) + sigma * mu;
+        } else {
+            /* Prime.c:193-196: no refactorisation -- kktsolve_2 reuses the previous factor */
+            sigma = sigma_d;
+            for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) + sigma * mu;
+        }
+        for (int r = 0; r < m; r++) r3[r] = rz[r] - ds[r] / z[r];
+        kkt_solve(&w, wgt, rx, ry, r3, dx, dy, dz);           /* kktsolve_2 */
+        for (int r = 0; r < m; r++) dsv[r] = (ds[r] - s[r] * dz[r]) / z[r];
+        alpha_p = steplen(s, dsv, m); alpha_d = steplen(z, dz, m);
+        alpha_p = 0.99 * alpha_p < 1.0 ? 0.99 * alpha_p : 1.0;
+        alpha_d = 0.99 * alpha_d < 1.0 ? 0.99 * alpha_d : 1.0;
+        for (int j = 0; j < n; j++) x[j] += dx[j] * alpha_p;
+        for (int k = 0; k < p; k++) y[k] += dy[k] * alpha_d;
+        for (int r = 0; r < m; r++) { s[r] += dsv[r] * alpha_p; z[r] += dz[r] * alpha_d; }
+        it++;
+    }
+done:
+    memcpy(x_out, x, sizeof(double) * n);
+    if (q_out) {                                   /* q = A' y (equality multipliers in x-space) */
+        for (int j = 0; j < n; j++) q_out[j] = 0;
+        for (int k = 0; k < p; k++) for (int j = 0; j < n; j++) q_out[j] += A[(size_t)k * n + j] * y[k];
+    }
+    if (iters_out) *iters_out = it;
+    free(x); free(y); free(s); free(z); free(rx); free(ry); free(rz); free(dx); free(dy); free(dz);
+    free(dsv); free(ds); free(lam); free(wgt); free(r3); free(zi); free(nc);
+    ws_free(&w);
+    return flag;
+}
