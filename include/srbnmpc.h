@@ -1,0 +1,118 @@
+/*
+ * srbnmpc -- batched CBF-NMPC solver for AMD Instinct MI355X (gfx950).  C ABI.
+ *
+ * Drop-in replacement for the per-control-cycle solve of the HDSRL/SRB-CBF-NMPC
+ * reference (MPC_dist::run_NMPC, /root/reference/src/MPC_dist.cpp:81-454):
+ *   - the QP stage iswiftQp_e(Q_qp, f_qp, Aeq, beq, Gineq, hineq, sol)
+ *       (/root/reference/optimization/iSWIFT/cpp_wrapper/iswift_qp.h:14-16, called at
+ *        MPC_dist.cpp:348), and
+ *   - the NLP stage nlp.AddVariableSet/AddConstraintSet/AddCostSet + SnoptSolver::Solve
+ *       (MPC_dist.cpp:402-427 with include/dec_vars_constr_cost.h),
+ * for a whole batch of agents per call.  Problem assembly (MPC_dist.cpp:99-321) and the
+ * closest-obstacle scan (:371-396) happen on the device from the per-agent inputs below.
+ *
+ * Conventions: plain C, fp64, agent-major arrays, caller-owned buffers, int status
+ * codes (0 = success; negative = API error), no exceptions across the ABI.  Solver exit
+ * codes mirror iSWIFT's (GlobalOptions.h:31-34): 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL.
+ * As in the reference (iswift_qp.cpp:126-151, MPC_dist.cpp:421), a non-optimal exit
+ * still returns the last iterate.
+ *
+ * Decision vector of one agent (the reference's mpc_state_eventbased_, MPC_dist.cpp:345):
+ *   x = [ X (4N: x, xdot, y, ydot per grid) | U (2N: CoP) | lambda (C*N) | s ]
+ *   nv = (6 + C) * N + 1
+ */
+#ifndef SRBNMPC_H
+#define SRBNMPC_H
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+#define SRB_OK 0
+#define SRB_ERR_ARG (-1)
+#define SRB_ERR_HIP (-2)
+#define SRB_ERR_SIZE (-3)
+
+/* solver exit codes (iSWIFT GlobalOptions.h:31-34) */
+#define SRB_OPTIMAL 0
+#define SRB_KKTFAIL 1
+#define SRB_MAXIT 2
+#define SRB_FATAL 3
+
+typedef struct srb_params {
+    int N;              /* grid points in the horizon (reference: 4, MPC_dist.cpp:92)               */
+    int C;              /* stance contacts per grid (trot 2, stand 4; MPC_dist.cpp:132)             */
+    int K_obs;          /* nearest static obstacles per agent (reference: 1, MPC_dist.cpp:371-396)  */
+    int K_nbr;          /* nearest other agents used as moving obstacles (reference: 0)             */
+    double grav, hcom, Ts, mu;       /* 9.81, 0.29, 0.043, 0.7 (MPC_dist.cpp:90-104)                */
+    double Qw, Pw, Rw, Sw;           /* 300, 2000, 0.1, 3000 (MPC_dist.cpp:172-175)                 */
+    double box;                      /* 1e3 (MPC_dist.cpp:317-318)                                  */
+    double eps_obs, eps_nbr;         /* (double)1.9f, (double)2.2f (dec_vars_constr_cost.h:401-402) */
+    double vsat;                     /* (double)0.35f (dec_vars_constr_cost.h:306-307)              */
+    double tol;                      /* 1e-6 (GlobalOptions.h:24-25)                                */
+    int qp_maxit, nlp_maxit;         /* 25 (GlobalOptions.h:23), 50                                 */
+    int use_nlp;                     /* MPC_dist::use_snopt (MPC_dist.hpp:139): 0 = QP only         */
+} srb_params;
+
+/* Reference defaults for horizon N and C contacts (K_obs = 1, K_nbr = 0, use_nlp = 1). */
+void srb_params_default(srb_params *p, int N, int C);
+int srb_nv(const srb_params *p);     /* (6+C)N+1 */
+
+/*
+ * One batch.  All pointers agent-major, fp64 unless noted.
+ *   x0        [A][4]        x, xdot, y, ydot             (MPC_dist.cpp:226-229; q[0],dq[0],q[1],dq[1])
+ *   ref       [A][4N]       com_desired_Traj_vec         (copPlanner_eventbase, MPC_dist.cpp:780)
+ *   foot      [A][N][2][C]  stance footholds per grid: row 0 = x, row 1 = y of the C
+ *                           contact legs in FR,FL,RR,RL order (footholdsPlanner, :1238-1260)
+ *   obstacles [n_obs][2]    Pobs_real columns, shared by the batch (MPC_dist.hpp:85)
+ *   nbr_state [n_all][4]    get_lastState() of every agent: x, y, xdot, ydot (MPC_dist.cpp:1272-1276);
+ *                           may be NULL when K_nbr == 0.  Local agent a is global agent
+ *                           agent_offset + a (itself excluded from its neighbours).
+ * Outputs:
+ *   x_qp      [A][nv]       QP-stage solution (qp_solution_eventbased_, :350-354); may be NULL
+ *   x         [A][nv]       final decision vector (mpc_state_eventbased_ after :423-426)
+ *   obj       [A]           0.5 x'Q_qp x + f'x (ExCost::GetCost)
+ *   status    [A][2] int    QP, NLP exit codes
+ *   iters     [A][2] int    QP, NLP interior-point iterations
+ */
+typedef struct srb_batch {
+    const double *x0, *ref, *foot, *obstacles, *nbr_state;
+    int n_obs, n_all, agent_offset;
+    double *x_qp, *x, *obj;
+    int *status, *iters;
+} srb_batch;
+
+typedef struct srb_ctx srb_ctx;
+
+/* Create a context on HIP device `device` for batches of up to max_agents agents. */
+int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out);
+int srb_ctx_destroy(srb_ctx *ctx);
+
+/* Host buffers: copies in, solves, copies out, synchronises.  n_agents <= max_agents. */
+int srb_solve_batch(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
+
+/* Same as srb_solve_batch with use_nlp forced to 0 (reference use_snopt == false). */
+int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
+
+/* Device buffers (all pointers in `dev_io` are device pointers), asynchronous on
+ * `stream` (a hipStream_t; NULL = the context's own stream).  Call srb_sync(). */
+int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
+int srb_sync(srb_ctx *ctx);
+
+/* Per-launch timing of the last srb_solve_batch_device call, measured with HIP events on
+ * the stream the kernels ran on (ms): knn kernel, solve kernel. */
+int srb_last_kernel_ms(srb_ctx *ctx, float *knn_ms, float *solve_ms);
+
+/* Dynamic LDS bytes one agent's workgroup uses (for occupancy reports). */
+int srb_lds_bytes(const srb_params *p);
+
+/* Bezier fit of the predicted CoM states (fitComTrajectory_eventbase, MPC_dist.cpp:784-855),
+ * host-side: alpha[4][5] from the buffer state buf[4] and X[0..3] (4 states). */
+void srb_fit_bezier(const double buf[4], const double *X, double alpha[20]);
+
+const char *srb_last_error(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

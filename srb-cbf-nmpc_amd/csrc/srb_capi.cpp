@@ -1,0 +1,317 @@
+// Host side of the C ABI declared in include/srbnmpc.h.
+//
+// The context owns device staging buffers sized for max_agents, one HIP stream and a
+// pair of events around each kernel, so bench.py can time the kernels on the stream
+// they actually run on.  Per-call work on the host is only the (tiny) LIP
+// discretisation shared by every agent and the launch.
+#include <hip/hip_runtime.h>
+#include <cmath>
+#include <cstdio>
+#include <cstring>
+#include <string>
+#include "srbnmpc.h"
+#include "srb_kernel_params.h"
+
+extern "C" __global__ void srb_nmpc_kernel(SrbKParams prm, int n_agents, const double *x0g, const double *refg,
+                                           const double *footg, const double *obstacles, int n_obs,
+                                           const double *nbr_state, const int *nbr_idx, double *x_qp_out,
+                                           double *x_out, double *obj_out, int *status_out, int *iters_out);
+extern "C" __global__ void srb_knn_kernel(int n_agents, int agent_offset, const double *state, int n_all, int K,
+                                          int *nbr_idx);
+
+static thread_local std::string g_err;
+
+static int fail(int code, const std::string &msg)
+{
+    g_err = msg;
+    return code;
+}
+
+#define HIPCHK(expr)                                                                   \
+    do {                                                                               \
+        hipError_t e_ = (expr);                                                        \
+        if (e_ != hipSuccess) return fail(SRB_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_)); \
+    } while (0)
+
+struct srb_ctx {
+    srb_params p;
+    int max_agents, device;
+    hipStream_t stream;
+    hipEvent_t ev[4];
+    // device staging
+    double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj;
+    int *status, *iters, *nbr_idx;
+    size_t cap_obs, cap_nbr;
+    float knn_ms, solve_ms;
+    bool timed;
+};
+
+extern "C" void srb_params_default(srb_params *p, int N, int C)
+{
+    std::memset(p, 0, sizeof(*p));
+    p->N = N; p->C = C; p->K_obs = 1; p->K_nbr = 0;
+    p->grav = 9.81; p->hcom = 0.29; p->Ts = 43 * 0.001; p->mu = 0.7;
+    p->Qw = 3e2; p->Pw = 2e3; p->Rw = 1e-1; p->Sw = 0.3e4;
+    p->box = 1e3;
+    p->eps_obs = (double)1.9f; p->eps_nbr = (double)2.2f; p->vsat = (double)0.35f;
+    p->tol = 1e-6; p->qp_maxit = 25; p->nlp_maxit = 50; p->use_nlp = 1;
+}
+
+extern "C" int srb_nv(const srb_params *p) { return (6 + p->C) * p->N + 1; }
+
+static void mm4(const double *X, const double *Y, double *Z)
+{
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 4; j++) {
+            double s = 0;
+            for (int k = 0; k < 4; k++) s += X[i * 4 + k] * Y[k * 4 + j];
+            Z[i * 4 + j] = s;
+        }
+}
+
+// LIP discretisation MPC_dist.cpp:99-127 (Ad by third-order series, Bd = A^-1 (Ad - I) B)
+static SrbKParams make_kparams(const srb_params *p, int use_nlp)
+{
+    SrbKParams k;
+    std::memset(&k, 0, sizeof k);
+    k.N = p->N; k.C = p->C; k.K_obs = p->K_obs; k.K_nbr = p->K_nbr;
+    k.n = (6 + p->C) * p->N + 1;
+    k.nz = p->N * (p->C - 1) + 1;
+    k.mq = 4 * (p->N - 1) + 12 * p->N + 2 * p->C * p->N;
+    k.use_nlp = use_nlp;
+    k.qp_maxit = p->qp_maxit; k.nlp_maxit = p->nlp_maxit;
+    const double w2 = p->grav / p->hcom, T = p->Ts;
+    double A[16] = {0}, B[8] = {0}, A2[16], A3[16];
+    A[1] = 1; A[4] = w2; A[11] = 1; A[14] = w2;
+    B[2] = -w2; B[7] = -w2;
+    mm4(A, A, A2); mm4(A2, A, A3);
+    for (int i = 0; i < 16; i++) k.Ad[i] = (i % 5 == 0 ? 1.0 : 0.0) + A[i] * T + 0.5 * A2[i] * T * T + A3[i] * T * T * T / 6;
+    double Ai[16] = {0}, AdI[16], M[16];
+    Ai[1] = 1.0 / w2; Ai[4] = 1.0; Ai[11] = 1.0 / w2; Ai[14] = 1.0;
+    for (int i = 0; i < 16; i++) AdI[i] = k.Ad[i] - (i % 5 == 0 ? 1.0 : 0.0);
+    mm4(Ai, AdI, M);
+    for (int i = 0; i < 4; i++)
+        for (int j = 0; j < 2; j++) {
+            double s = 0;
+            for (int q = 0; q < 4; q++) s += M[i * 4 + q] * B[q * 2 + j];
+            k.Bd[i * 2 + j] = s;
+        }
+    k.Qw = p->Qw; k.Pw = p->Pw; k.Rw = p->Rw; k.Sw = p->Sw; k.box = p->box;
+    k.fr = p->mu * p->hcom / std::sqrt(2.0);
+    k.eps_obs = p->eps_obs; k.eps_nbr = p->eps_nbr; k.vsat = p->vsat; k.tol = p->tol; k.Ts = p->Ts;
+    return k;
+}
+
+static int validate(const srb_params *p)
+{
+    if (!p) return fail(SRB_ERR_ARG, "null params");
+    if (p->N < 2 || p->C < 2 || p->C > 4) return fail(SRB_ERR_ARG, "need N >= 2 and 2 <= C <= 4");
+    if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs + p->K_nbr > SRB_MAX_K) return fail(SRB_ERR_ARG, "K_obs + K_nbr out of range");
+    if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 64 (one xi entry per lane)");
+    if ((6 + p->C) * p->N + 1 > SRB_MAX_NV) return fail(SRB_ERR_SIZE, "nv exceeds 256");
+    SrbKParams k = make_kparams(p, p->use_nlp);
+    if ((size_t)srb_lds_doubles(k) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
+    return SRB_OK;
+}
+
+extern "C" int srb_lds_bytes(const srb_params *p)
+{
+    SrbKParams k = make_kparams(p, p->use_nlp);
+    return srb_lds_doubles(k) * (int)sizeof(double);
+}
+
+extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out)
+{
+    if (!out || max_agents <= 0) return fail(SRB_ERR_ARG, "bad arguments");
+    int rc = validate(p);
+    if (rc) return rc;
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SRB_ERR_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    srb_ctx *c = new srb_ctx();
+    c->p = *p; c->max_agents = max_agents; c->device = device;
+    c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false;
+    const int N = p->N, C = p->C, nv = srb_nv(p), Kn = p->K_nbr > 0 ? p->K_nbr : 1;
+    const size_t A = (size_t)max_agents;
+    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    HIPCHK(hipMalloc(&c->x0, A * 4 * sizeof(double)));
+    HIPCHK(hipMalloc(&c->ref, A * 4 * N * sizeof(double)));
+    HIPCHK(hipMalloc(&c->foot, A * 2 * C * N * sizeof(double)));
+    HIPCHK(hipMalloc(&c->x_qp, A * nv * sizeof(double)));
+    HIPCHK(hipMalloc(&c->x, A * nv * sizeof(double)));
+    HIPCHK(hipMalloc(&c->obj, A * sizeof(double)));
+    HIPCHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&c->nbr_idx, A * Kn * sizeof(int)));
+    *out = c;
+    return SRB_OK;
+}
+
+extern "C" int srb_ctx_destroy(srb_ctx *c)
+{
+    if (!c) return SRB_OK;
+    (void)hipSetDevice(c->device);
+    (void)hipStreamSynchronize(c->stream);
+    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->nbr_idx, c->obstacles, c->nbr};
+    for (void *b : bufs)
+        if (b) (void)hipFree(b);
+    for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
+    (void)hipStreamDestroy(c->stream);
+    delete c;
+    return SRB_OK;
+}
+
+static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, int use_nlp)
+{
+    if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
+    if (n_agents == 0) return SRB_OK;
+    const srb_params *p = &c->p;
+    if (!d->x0 || !d->ref || !d->foot || !d->x || !d->obj || !d->status || !d->iters)
+        return fail(SRB_ERR_ARG, "missing buffer");
+    if (use_nlp && p->K_obs > 0 && (d->n_obs < 0 || (d->n_obs > 0 && !d->obstacles)))
+        return fail(SRB_ERR_ARG, "obstacles missing");
+    if (use_nlp && p->K_nbr > 0 && (!d->nbr_state || d->n_all <= 0 || d->agent_offset < 0 ||
+                                    d->agent_offset + n_agents > d->n_all))
+        return fail(SRB_ERR_ARG, "neighbour states missing or agent_offset out of range");
+    SrbKParams k = make_kparams(p, use_nlp);
+    const size_t lds = (size_t)srb_lds_doubles(k) * sizeof(double);
+    HIPCHK(hipSetDevice(c->device));
+    const int *nbr_idx = nullptr;
+    c->timed = true;
+    HIPCHK(hipEventRecord(c->ev[0], s));
+    if (use_nlp && p->K_nbr > 0) {
+        dim3 blk(256), grd((n_agents + 255) / 256);
+        hipLaunchKernelGGL(srb_knn_kernel, grd, blk, 0, s, n_agents, d->agent_offset, d->nbr_state, d->n_all,
+                           p->K_nbr, c->nbr_idx);
+        HIPCHK(hipGetLastError());
+        nbr_idx = c->nbr_idx;
+    }
+    HIPCHK(hipEventRecord(c->ev[1], s));
+    hipLaunchKernelGGL(srb_nmpc_kernel, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+                       d->obstacles, d->n_obs, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
+    HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[2], s));
+    return SRB_OK;
+}
+
+extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch *dev_io, void *stream)
+{
+    if (!c || !dev_io) return fail(SRB_ERR_ARG, "null argument");
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    return launch(c, n_agents, dev_io, s, c->p.use_nlp);
+}
+
+extern "C" int srb_sync(srb_ctx *c)
+{
+    if (!c) return fail(SRB_ERR_ARG, "null ctx");
+    HIPCHK(hipSetDevice(c->device));
+    HIPCHK(hipDeviceSynchronize());
+    return SRB_OK;
+}
+
+extern "C" int srb_last_kernel_ms(srb_ctx *c, float *knn_ms, float *solve_ms)
+{
+    if (!c || !c->timed) return fail(SRB_ERR_ARG, "no timed launch");
+    HIPCHK(hipEventSynchronize(c->ev[2]));
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
+    if (knn_ms) *knn_ms = a;
+    if (solve_ms) *solve_ms = b;
+    return SRB_OK;
+}
+
+static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
+{
+    if (!c || !h) return fail(SRB_ERR_ARG, "null argument");
+    if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
+    if (n_agents == 0) return SRB_OK;
+    const srb_params *p = &c->p;
+    const int N = p->N, C = p->C, nv = srb_nv(p);
+    const size_t A = (size_t)n_agents;
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = c->stream;
+    if (!h->x0 || !h->ref || !h->foot || !h->x || !h->obj || !h->status || !h->iters)
+        return fail(SRB_ERR_ARG, "missing buffer");
+    HIPCHK(hipMemcpyAsync(c->x0, h->x0, A * 4 * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->ref, h->ref, A * 4 * N * sizeof(double), hipMemcpyHostToDevice, s));
+    HIPCHK(hipMemcpyAsync(c->foot, h->foot, A * 2 * C * N * sizeof(double), hipMemcpyHostToDevice, s));
+    srb_batch d = *h;
+    d.x0 = c->x0; d.ref = c->ref; d.foot = c->foot;
+    d.x_qp = c->x_qp; d.x = c->x; d.obj = c->obj; d.status = c->status; d.iters = c->iters;
+    d.obstacles = nullptr; d.nbr_state = nullptr;
+    if (h->n_obs > 0 && h->obstacles) {
+        if ((size_t)h->n_obs > c->cap_obs) {
+            if (c->obstacles) HIPCHK(hipFree(c->obstacles));
+            HIPCHK(hipMalloc(&c->obstacles, (size_t)h->n_obs * 2 * sizeof(double)));
+            c->cap_obs = h->n_obs;
+        }
+        HIPCHK(hipMemcpyAsync(c->obstacles, h->obstacles, (size_t)h->n_obs * 2 * sizeof(double), hipMemcpyHostToDevice, s));
+        d.obstacles = c->obstacles;
+    }
+    if (h->n_all > 0 && h->nbr_state) {
+        if ((size_t)h->n_all > c->cap_nbr) {
+            if (c->nbr) HIPCHK(hipFree(c->nbr));
+            HIPCHK(hipMalloc(&c->nbr, (size_t)h->n_all * 4 * sizeof(double)));
+            c->cap_nbr = h->n_all;
+        }
+        HIPCHK(hipMemcpyAsync(c->nbr, h->nbr_state, (size_t)h->n_all * 4 * sizeof(double), hipMemcpyHostToDevice, s));
+        d.nbr_state = c->nbr;
+    }
+    int rc = launch(c, n_agents, &d, s, use_nlp);
+    if (rc) return rc;
+    if (h->x_qp) HIPCHK(hipMemcpyAsync(h->x_qp, c->x_qp, A * nv * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h->x, c->x, A * nv * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h->obj, c->obj, A * sizeof(double), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h->status, c->status, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipMemcpyAsync(h->iters, c->iters, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    HIPCHK(hipStreamSynchronize(s));
+    return SRB_OK;
+}
+
+extern "C" int srb_solve_batch(srb_ctx *c, int n_agents, const srb_batch *host_io)
+{
+    return solve_host(c, n_agents, host_io, c ? c->p.use_nlp : 0);
+}
+
+extern "C" int srb_solve_qp(srb_ctx *c, int n_agents, const srb_batch *host_io)
+{
+    return solve_host(c, n_agents, host_io, 0);
+}
+
+// fitComTrajectory_eventbase (MPC_dist.cpp:784-855).  With N == NDOMAIN the reference's
+// 24x24 KKT (whose 20x8 -> 20x4 block assignment keeps only the s = 0 end-point row)
+// has the unique solution of the 5-point Bernstein interpolation through
+// [buf, X0, X1, X2, X3] at s = 0, 1/4, 1/2, 3/4, 1, solved here per state row.
+extern "C" void srb_fit_bezier(const double buf[4], const double *X, double alpha[20])
+{
+    static const double binom[5] = {1, 4, 6, 4, 1};
+    for (int d = 0; d < 4; d++) {
+        double M[5][6];
+        for (int i = 0; i < 5; i++) {
+            double s = i * 0.25;
+            for (int j = 0; j < 5; j++) M[i][j] = binom[j] * std::pow(s, j) * std::pow(1 - s, 4 - j);
+            M[i][5] = (i == 0) ? buf[d] : X[(i - 1) * 4 + d];
+        }
+        for (int k = 0; k < 5; k++) {           // Gaussian elimination, partial pivoting
+            int piv = k;
+            for (int i = k + 1; i < 5; i++) if (std::fabs(M[i][k]) > std::fabs(M[piv][k])) piv = i;
+            if (piv != k) for (int j = 0; j < 6; j++) std::swap(M[k][j], M[piv][j]);
+            for (int i = k + 1; i < 5; i++) {
+                double l = M[i][k] / M[k][k];
+                for (int j = k; j < 6; j++) M[i][j] -= l * M[k][j];
+            }
+        }
+        double a[5];
+        for (int i = 4; i >= 0; i--) {
+            double s = M[i][5];
+            for (int j = i + 1; j < 5; j++) s -= M[i][j] * a[j];
+            a[i] = s / M[i][i];
+        }
+        for (int j = 0; j < 5; j++) alpha[d * 5 + j] = a[j];
+    }
+}
+
+extern "C" const char *srb_last_error(void) { return g_err.c_str(); }

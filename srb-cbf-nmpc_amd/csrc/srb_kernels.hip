@@ -1,0 +1,706 @@
+// Batched CBF-NMPC solver kernels for MI355X (gfx950).
+//
+// Replaces the per-control-cycle solve of MPC_dist::run_NMPC
+// (/root/reference/src/MPC_dist.cpp:81-454): the LIP/CoP/contact-weight QP of
+// :135-321 solved with the iSWIFT Mehrotra predictor-corrector
+// (/root/reference/optimization/iSWIFT/src/Prime.c:127-230), then the NLP stage with
+// the obstacle ("CBF") and velocity rows of include/dec_vars_constr_cost.h:245-395
+// (SNOPT in the reference) solved by a primal-dual interior-point method warm-started
+// from the QP solution (MPC_dist.cpp:403).
+//
+// Layout / execution model
+//   * one 64-lane wavefront (= one workgroup) per agent; the whole solve -- problem
+//     assembly, both interior-point loops, output -- runs inside that wave with all
+//     per-agent state in LDS, so there is no host round trip per iteration;
+//   * equality constraints (LIP dynamics, u_k = F_k lambda_k, sum lambda_k = 1) are
+//     eliminated by a null-space basis Z built from a forward rollout:
+//         x = xbar + Z xi,  xi = (lambda dofs of every grid, s),  nz = N(C-1)+1,
+//     so each Newton step is an nz x nz Cholesky (11 x 11 at N=10 trot) instead of
+//     the (nv+neq+m)-dimensional sparse LDL' of iSWIFT.  Iterates equal iSWIFT's in
+//     exact arithmetic: x, s, z are advanced exactly as Prime.c:208-216 and the
+//     equality multipliers are carried as q = A'y (q += alpha_d * A'dy), which is all
+//     the residual rx = -Px - A'y - G'z - c of computeresiduals needs;
+//   * inputs/outputs are agent-major fp64 arrays in HBM, read once / written once.
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "srb_kernel_params.h"
+
+#define WAVE 64
+
+// --------------------------------------------------------------------------- wave helpers
+__device__ __forceinline__ double wsum(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
+    return v;
+}
+__device__ __forceinline__ double wmin(double v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
+    return v;
+}
+__device__ __forceinline__ int wor(int v)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, WAVE);
+    return v;
+}
+
+// --------------------------------------------------------------------------- per-agent context
+struct Ctx {
+    const SrbKParams *P;
+    int N, C, K, n, nz, mq, m, nl;          // nl: NLP rows/terms active
+    int rFm, rXp, rXm, rUp, rUm, rLlo, rLhi, rO, rV;
+    // LDS arrays
+    double *Z, *x, *q, *rx, *dx, *tv, *D, *ref, *foot, *offv;
+    double *s, *z, *rz, *dz, *dsv, *dsT, *om, *jc, *obs, *eps;
+    double *Hc, *L, *ZtZ, *ZtZL, *hvec;
+    int tid;
+};
+
+__device__ __forceinline__ int col_stage(const Ctx &c, int a) { return (a == c.nz - 1) ? c.N : a / (c.C - 1); }
+
+// h of row r
+__device__ __forceinline__ double row_h(const Ctx &c, int r)
+{
+    if (r < c.rXp) return c.P->fr;
+    if (r < c.rLlo) return c.P->box;
+    if (r < c.rLhi) return 0.0;
+    if (r < c.mq) return 1.0;
+    if (r < c.rV) return -c.eps[(r - c.rO) % c.K];
+    return c.P->vsat;
+}
+
+// J_r . v  (for obstacle rows this is the Jacobian row at the point the coefficients were taken)
+__device__ __forceinline__ double row_dot(const Ctx &c, int r, const double *v)
+{
+    const int N = c.N;
+    if (r < c.rFm) { int i = r >> 1, d = r & 1; return v[4 * i + 2 * d] - v[4 * N + 2 * (i + 1) + d]; }
+    if (r < c.rXp) { int rr = r - c.rFm, i = rr >> 1, d = rr & 1; return -v[4 * i + 2 * d] + v[4 * N + 2 * (i + 1) + d]; }
+    if (r < c.rXm) return v[r - c.rXp];
+    if (r < c.rUp) return -v[r - c.rXm];
+    if (r < c.rUm) return v[4 * N + (r - c.rUp)];
+    if (r < c.rLlo) return -v[4 * N + (r - c.rUm)];
+    if (r < c.rLhi) return -v[6 * N + (r - c.rLlo)];
+    if (r < c.mq) return v[6 * N + (r - c.rLhi)];
+    if (r < c.rV) {
+        int o = r - c.rO, k = o / c.K;
+        return c.jc[2 * o] * v[4 * k] + c.jc[2 * o + 1] * v[4 * k + 2] - v[c.n - 1];
+    }
+    int rr = r - c.rV; double sg = (rr < 2 * N) ? 1.0 : -1.0;
+    int t = rr % (2 * N), comp = (t < N) ? 1 : 3, k = t % N;
+    return sg * v[4 * k + comp];
+}
+
+// (J' w)_v for every variable but s (s handled by a wave reduction)
+__device__ __forceinline__ double jt_gather(const Ctx &c, int v, const double *w)
+{
+    const int N = c.N;
+    double acc;
+    if (v < 4 * N) {
+        int k = v >> 2, cc = v & 3;
+        acc = w[c.rXp + v] - w[c.rXm + v];
+        if (!(cc & 1)) {
+            int d = cc >> 1;
+            if (k <= N - 2) acc += w[2 * k + d] - w[c.rFm + 2 * k + d];
+            if (c.nl)
+                for (int j = 0; j < c.K; j++) acc += c.jc[2 * (k * c.K + j) + d] * w[c.rO + k * c.K + j];
+        } else if (c.nl) {
+            int t = ((cc == 1) ? 0 : N) + k;
+            acc += w[c.rV + t] - w[c.rV + 2 * N + t];
+        }
+    } else if (v < 6 * N) {
+        int j = v - 4 * N, k = j >> 1, d = j & 1;
+        acc = w[c.rUp + j] - w[c.rUm + j];
+        if (k >= 1) acc += -w[2 * (k - 1) + d] + w[c.rFm + 2 * (k - 1) + d];
+    } else {
+        int j = v - 6 * N;
+        acc = -w[c.rLlo + j] + w[c.rLhi + j];
+    }
+    return acc;
+}
+
+// out[v] = base[v] + sign*(J' w)[v] for all v (s row by reduction).  Collective.
+__device__ void jt_apply(const Ctx &c, const double *w, double *out, const double *base, double sign)
+{
+    for (int v = c.tid; v < c.n - 1; v += WAVE) out[v] = (base ? base[v] : 0.0) + sign * jt_gather(c, v, w);
+    double ps = 0.0;
+    if (c.nl)
+        for (int o = c.tid; o < c.N * c.K; o += WAVE) ps -= w[c.rO + o];
+    ps = wsum(ps);
+    if (c.tid == 0) out[c.n - 1] = (base ? base[c.n - 1] : 0.0) + sign * ps;
+    __syncthreads();
+}
+
+__device__ __forceinline__ double Pdiag(const Ctx &c, int v)
+{
+    const int N = c.N;
+    if (v < 4 * N) return (v >= 4 * (N - 1)) ? c.P->Pw : c.P->Qw;
+    if (v < 6 * N) return c.P->Rw;
+    if (v < c.n - 1) return 0.0;
+    return c.P->Sw;
+}
+__device__ __forceinline__ double cvec(const Ctx &c, int v) { return (v < 4 * c.N) ? -Pdiag(c, v) * c.ref[v] : 0.0; }
+
+// Lagrangian-Hessian diagonal beyond P (NLP: -2 sum_j z_kj on x_k, y_k)
+__device__ __forceinline__ double hess_diag(const Ctx &c, int v)
+{
+    if (!c.nl || v >= 4 * c.N || (v & 1)) return 0.0;
+    int k = v >> 2;
+    double zs = 0.0;
+    for (int j = 0; j < c.K; j++) zs += c.z[c.rO + k * c.K + j];
+    return -2.0 * zs;
+}
+
+// obstacle Jacobian coefficients at the current x: jc = -2 (p_k - o_kj)
+__device__ void obstacle_coefs(const Ctx &c)
+{
+    for (int o = c.tid; o < c.N * c.K; o += WAVE) {
+        int k = o / c.K;
+        c.jc[2 * o] = -2.0 * (c.x[4 * k] - c.obs[2 * o]);
+        c.jc[2 * o + 1] = -2.0 * (c.x[4 * k + 2] - c.obs[2 * o + 1]);
+    }
+    __syncthreads();
+}
+
+// g_r(x) for all rows -> rz = h - s - g  (collective)
+__device__ void residual_rows(const Ctx &c)
+{
+    for (int r = c.tid; r < c.m; r += WAVE) {
+        double g;
+        if (r >= c.rO && r < c.rV) {
+            int o = r - c.rO, k = o / c.K;
+            double dx = c.x[4 * k] - c.obs[2 * o], dy = c.x[4 * k + 2] - c.obs[2 * o + 1];
+            g = -(dx * dx + dy * dy) - c.x[c.n - 1];
+        } else {
+            g = row_dot(c, r, c.x);
+        }
+        c.rz[r] = c.hvec[r] - c.s[r] - g;
+    }
+}
+
+// Build D (diag of H), offdiag values, then Hc = Z' H Z (+ delta ZtZ done by caller).
+// H = P + hess + delta I + J' diag(om) J.
+__device__ void build_H(const Ctx &c, double delta)
+{
+    const int N = c.N, n = c.n;
+    for (int v = c.tid; v < n - 1; v += WAVE) {
+        double d = Pdiag(c, v) + delta + hess_diag(c, v);
+        if (v < 4 * N) {
+            int k = v >> 2, cc = v & 3;
+            d += c.om[c.rXp + v] + c.om[c.rXm + v];
+            if (!(cc & 1)) {
+                int dd = cc >> 1;
+                if (k <= N - 2) d += c.om[2 * k + dd] + c.om[c.rFm + 2 * k + dd];
+                if (c.nl)
+                    for (int j = 0; j < c.K; j++) { double jj = c.jc[2 * (k * c.K + j) + dd]; d += c.om[c.rO + k * c.K + j] * jj * jj; }
+            } else if (c.nl) {
+                int t = ((cc == 1) ? 0 : N) + k;
+                d += c.om[c.rV + t] + c.om[c.rV + 2 * N + t];
+            }
+        } else if (v < 6 * N) {
+            int j = v - 4 * N, k = j >> 1, dd = j & 1;
+            d += c.om[c.rUp + j] + c.om[c.rUm + j];
+            if (k >= 1) d += c.om[2 * (k - 1) + dd] + c.om[c.rFm + 2 * (k - 1) + dd];
+        } else {
+            int j = v - 6 * N;
+            d += c.om[c.rLlo + j] + c.om[c.rLhi + j];
+        }
+        c.D[v] = d;
+    }
+    double ps = 0.0;
+    if (c.nl)
+        for (int o = c.tid; o < N * c.K; o += WAVE) ps += c.om[c.rO + o];
+    ps = wsum(ps);
+    if (c.tid == 0) c.D[n - 1] = Pdiag(c, n - 1) + delta + ps;
+    // off-diagonals: friction (i,d) -> (4i+2d, 4N+2(i+1)+d); obstacle stage k -> (xk,yk),(xk,s),(yk,s)
+    const int nf = 2 * (N - 1);
+    for (int e = c.tid; e < nf; e += WAVE) c.offv[e] = -(c.om[e] + c.om[c.rFm + e]);
+    if (c.nl)
+        for (int k = c.tid; k < N; k += WAVE) {
+            double xy = 0, xs = 0, ys = 0;
+            for (int j = 0; j < c.K; j++) {
+                int o = k * c.K + j;
+                double w = c.om[c.rO + o], jx = c.jc[2 * o], jy = c.jc[2 * o + 1];
+                xy += w * jx * jy; xs -= w * jx; ys -= w * jy;
+            }
+            c.offv[nf + 3 * k] = xy; c.offv[nf + 3 * k + 1] = xs; c.offv[nf + 3 * k + 2] = ys;
+        }
+    __syncthreads();
+    // Hc[a][b], a <= b
+    const int nz = c.nz, npair = nz * (nz + 1) / 2;
+    for (int pidx = c.tid; pidx < npair; pidx += WAVE) {
+        // decode pidx -> (a, b) with a <= b, row-major over b
+        int b = (int)((sqrt(8.0 * pidx + 1.0) - 1.0) * 0.5);
+        while (b * (b + 1) / 2 > pidx) b--;
+        while ((b + 1) * (b + 2) / 2 <= pidx) b++;
+        int a = pidx - b * (b + 1) / 2;
+        int ja = col_stage(c, a), jb = col_stage(c, b);
+        int k0 = ja > jb ? ja : jb;
+        double acc = 0.0;
+        // X rows of grids >= max stage (Z_X is block lower triangular)
+        for (int v = 4 * k0; v < 4 * N; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
+        if (ja == jb && ja < N) {
+            for (int v = 4 * N + 2 * ja; v < 4 * N + 2 * ja + 2; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
+            for (int v = 6 * N + c.C * ja; v < 6 * N + c.C * ja + c.C; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
+        }
+        if (ja == N && jb == N) acc += c.D[n - 1];
+        for (int e = 0; e < nf; e++) {
+            int i = e >> 1, d = e & 1, u = 4 * i + 2 * d, w = 4 * N + 2 * (i + 1) + d;
+            acc += c.offv[e] * (c.Z[u * nz + a] * c.Z[w * nz + b] + c.Z[w * nz + a] * c.Z[u * nz + b]);
+        }
+        if (c.nl)
+            for (int k = 0; k < N; k++) {
+                double xa = c.Z[(4 * k) * nz + a], ya = c.Z[(4 * k + 2) * nz + a], sa = c.Z[(n - 1) * nz + a];
+                double xb = c.Z[(4 * k) * nz + b], yb = c.Z[(4 * k + 2) * nz + b], sb = c.Z[(n - 1) * nz + b];
+                acc += c.offv[nf + 3 * k] * (xa * yb + ya * xb) + c.offv[nf + 3 * k + 1] * (xa * sb + sa * xb) +
+                       c.offv[nf + 3 * k + 2] * (ya * sb + sa * yb);
+            }
+        c.Hc[a * nz + b] = acc;
+        c.Hc[b * nz + a] = acc;
+    }
+    __syncthreads();
+}
+
+// In-place Cholesky of L (nz x nz, lower). Returns 0 on success (uniform).
+__device__ int chol_lds(const Ctx &c, double *L, int nz)
+{
+    for (int k = 0; k < nz; k++) {
+        __syncthreads();
+        double d = L[k * nz + k];
+        if (!(d > 0.0)) return -1;
+        d = sqrt(d);
+        __syncthreads();
+        if (c.tid == 0) L[k * nz + k] = d;
+        for (int i = k + 1 + c.tid; i < nz; i += WAVE) L[i * nz + k] /= d;
+        __syncthreads();
+        for (int i = k + 1 + c.tid; i < nz; i += WAVE) {
+            double lik = L[i * nz + k];
+            for (int j = k + 1; j <= i; j++) L[i * nz + j] -= lik * L[j * nz + k];
+        }
+    }
+    __syncthreads();
+    return 0;
+}
+
+// Solve (L L') y = b with b held one entry per lane (lane i < nz). Returns y in the same form.
+__device__ double chol_solve_reg(const Ctx &c, const double *L, int nz, double bi)
+{
+    for (int k = 0; k < nz; k++) {
+        double yk = __shfl(bi, k, WAVE) / L[k * nz + k];
+        if (c.tid == k) bi = yk;
+        else if (c.tid > k && c.tid < nz) bi -= L[c.tid * nz + k] * yk;
+    }
+    for (int k = nz - 1; k >= 0; k--) {
+        double xk = __shfl(bi, k, WAVE) / L[k * nz + k];
+        if (c.tid == k) bi = xk;
+        else if (c.tid < k) bi -= L[k * nz + c.tid] * xk;
+    }
+    return bi;
+}
+
+// xi-vector (one entry per lane) = Z' v
+__device__ __forceinline__ double zt_mul(const Ctx &c, const double *v)
+{
+    double acc = 0.0;
+    if (c.tid < c.nz) {
+        int a = c.tid, ja = col_stage(c, a);
+        if (ja < c.N) {
+            for (int r = 4 * ja; r < 4 * c.N; r++) acc += c.Z[r * c.nz + a] * v[r];
+            for (int r = 4 * c.N + 2 * ja; r < 4 * c.N + 2 * ja + 2; r++) acc += c.Z[r * c.nz + a] * v[r];
+            for (int r = 6 * c.N + c.C * ja; r < 6 * c.N + c.C * ja + c.C; r++) acc += c.Z[r * c.nz + a] * v[r];
+        } else {
+            acc = v[c.n - 1];
+        }
+    }
+    return acc;
+}
+
+// out = Z xi  (xi one entry per lane)
+__device__ void z_mul(const Ctx &c, double xi, double *out)
+{
+    for (int v = c.tid; v < c.n; v += WAVE) out[v] = 0.0;
+    // every lane needs every xi_a: loop a with shuffles (uniform)
+    double accs[4] = {0, 0, 0, 0};
+    for (int a = 0; a < c.nz; a++) {
+        double xa = __shfl(xi, a, WAVE);
+#pragma unroll
+        for (int t = 0; t < 4; t++) {
+            int v = c.tid + t * WAVE;
+            if (v < c.n) accs[t] += c.Z[v * c.nz + a] * xa;
+        }
+    }
+#pragma unroll
+    for (int t = 0; t < 4; t++) { int v = c.tid + t * WAVE; if (v < c.n) out[v] = accs[t]; }
+    __syncthreads();
+}
+
+// Newton solve with the current factor L and weights om:
+//   [H A' J'; A 0 0; J 0 -W][dx;dy;dz] = [r1; 0; r3], W^-1 = om
+// r1 (n) given, r3 in dz on entry (overwritten with dz).  dx -> c.dx.  Uses c.tv.
+__device__ void newton_solve(const Ctx &c, const double *r1, double *r3dz)
+{
+    // tv = r1 + J' (om .* r3); om .* r3 staged in the dsv scratch (callers recompute dsv)
+    double *w = c.dsv;                      // scratch m-vector (caller recomputes dsv after)
+    for (int r = c.tid; r < c.m; r += WAVE) w[r] = c.om[r] * r3dz[r];
+    __syncthreads();
+    jt_apply(c, w, c.tv, r1, 1.0);
+    double g = zt_mul(c, c.tv);
+    double xi = chol_solve_reg(c, c.L, c.nz, g);
+    z_mul(c, xi, c.dx);
+    for (int r = c.tid; r < c.m; r += WAVE) r3dz[r] = c.om[r] * (row_dot(c, r, c.dx) - r3dz[r]);
+    __syncthreads();
+}
+
+// findsteplength (Auxilary.c:271-294): uniform result
+__device__ __forceinline__ double steplen(const Ctx &c, const double *v, const double *dv)
+{
+    double a = 1e10; int f = 0;
+    for (int r = c.tid; r < c.m; r += WAVE)
+        if (dv[r] < 0.0) { double t = -(v[r] / dv[r]); if (t < a) a = t; f = 1; }
+    a = wmin(a); f = wor(f);
+    return f ? a : 1.0;
+}
+
+// One interior-point solve (QP stage: nl = 0, iSWIFT; NLP stage: nl = 1).
+// Returns exit code; *iters gets the number of steps taken.
+__device__ int ipm(Ctx &c, int maxit, int *iters)
+{
+    const double tol = c.P->tol, th = tol / sqrt(3.0);
+    double sigma = 100.0;               // options->sigma = SIGMA
+    const double sigma_d = 0.0;
+    int flag = 2, it = 0;
+    double delta = 0.0;
+    for (int iter = 0; iter < maxit; iter++) {
+        if (c.nl) obstacle_coefs(c);
+        residual_rows(c);
+        // rx = -(P x + c) - q - J' z
+        __syncthreads();
+        for (int v = c.tid; v < c.n; v += WAVE) c.tv[v] = -(Pdiag(c, v) * c.x[v] + cvec(c, v)) - c.q[v];
+        __syncthreads();
+        jt_apply(c, c.z, c.rx, c.tv, -1.0);
+        double nrx = 0, nrz = 0, sz = 0;
+        for (int v = c.tid; v < c.n; v += WAVE) nrx += c.rx[v] * c.rx[v];
+        for (int r = c.tid; r < c.m; r += WAVE) { nrz += c.rz[r] * c.rz[r]; sz += c.s[r] * c.z[r]; }
+        nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz);
+        if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
+        if (nrx < th && nrz < th && sz / c.m < tol) { flag = 0; break; }
+        double mu = 0;
+        for (int r = c.tid; r < c.m; r += WAVE) { double l = sqrt(c.s[r] * c.z[r]); mu += l * l; }
+        mu = wsum(mu) / c.m;
+        const int pc = c.nl || (sigma > sigma_d);
+        if (pc) {
+            // weights W^-1 = 1/(s/z) (updatekktmatrix, Auxilary.c:197-205) and factor
+            for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0 / (c.s[r] / c.z[r]);
+            __syncthreads();
+            delta = 0.0;
+            int ok = 0;
+            for (int tries = 0; tries < (c.nl ? 14 : 1); tries++) {
+                build_H(c, delta);
+                for (int i = c.tid; i < c.nz * c.nz; i += WAVE) c.L[i] = c.Hc[i];
+                __syncthreads();
+                if (chol_lds(c, c.L, c.nz) == 0) { ok = 1; break; }
+                delta = (delta == 0.0) ? 1e-4 : delta * 10.0;
+            }
+            if (!ok) { flag = 1; break; }
+            // predictor: ds = -lambda.*lambda
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                double l = sqrt(c.s[r] * c.z[r]);
+                c.dsT[r] = -l * l;
+                c.dz[r] = c.rz[r] - c.dsT[r] / c.z[r];
+            }
+            __syncthreads();
+            newton_solve(c, c.rx, c.dz);
+            for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) / c.z[r];
+            __syncthreads();
+            double ap = steplen(c, c.s, c.dsv), ad = steplen(c, c.z, c.dz);
+            double num = 0, den = 0;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                num += (c.s[r] + ap * c.dsv[r]) * (c.z[r] + ad * c.dz[r]);
+                den += c.s[r] * c.z[r];
+            }
+            num = wsum(num); den = wsum(den);
+            double rho = num / den, mr = rho < 1.0 ? rho : 1.0;
+            sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                double l = sqrt(c.s[r] * c.z[r]);
+                c.dsT[r] = -(l * l) - (c.dsv[r] * c.dz[r]) + sigma * mu;
+            }
+        } else {
+            // Prime.c:193-196: centring step with the previous factor
+            sigma = sigma_d;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                double l = sqrt(c.s[r] * c.z[r]);
+                c.dsT[r] = -(l * l) + sigma * mu;
+            }
+        }
+        __syncthreads();
+        for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.rz[r] - c.dsT[r] / c.z[r];
+        __syncthreads();
+        newton_solve(c, c.rx, c.dz);
+        for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) / c.z[r];
+        __syncthreads();
+        // dq = A'dy = rx - (P + hess + delta) dx - J' dz
+        for (int v = c.tid; v < c.n; v += WAVE)
+            c.tv[v] = c.rx[v] - (Pdiag(c, v) + hess_diag(c, v) + (c.nl ? delta : 0.0)) * c.dx[v];
+        __syncthreads();
+        double ap = steplen(c, c.s, c.dsv), ad = steplen(c, c.z, c.dz);
+        ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
+        ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
+        // tv - J'dz needs the dz of this step: apply before updating z (hess uses old z)
+        jt_apply(c, c.dz, c.tv, c.tv, -1.0);
+        for (int v = c.tid; v < c.n; v += WAVE) { c.x[v] += c.dx[v] * ap; c.q[v] += c.tv[v] * ad; }
+        for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] += c.dsv[r] * ap; c.z[r] += c.dz[r] * ad; }
+        __syncthreads();
+        it++;
+    }
+    *iters = it;
+    return flag;
+}
+
+// --------------------------------------------------------------------------- main kernel
+extern "C" __global__ void __launch_bounds__(WAVE)
+srb_nmpc_kernel(SrbKParams prm, int n_agents,
+                const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
+                const double *__restrict__ obstacles, int n_obs,
+                const double *__restrict__ nbr_state, const int *__restrict__ nbr_idx,
+                double *__restrict__ x_qp_out, double *__restrict__ x_out,
+                double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out)
+{
+    extern __shared__ __attribute__((aligned(16))) double lds[];
+    const int agent = blockIdx.x;
+    if (agent >= n_agents) return;
+    Ctx c;
+    c.P = &prm; c.tid = threadIdx.x;
+    c.N = prm.N; c.C = prm.C; c.K = prm.K_obs + prm.K_nbr;
+    c.n = prm.n; c.nz = prm.nz; c.mq = prm.mq;
+    const int N = c.N, C = c.C, n = c.n, nz = c.nz, K = c.K;
+    c.rFm = 2 * (N - 1); c.rXp = 4 * (N - 1); c.rXm = c.rXp + 4 * N; c.rUp = c.rXm + 4 * N;
+    c.rUm = c.rUp + 2 * N; c.rLlo = c.rUm + 2 * N; c.rLhi = c.rLlo + C * N;
+    c.rO = c.mq; c.rV = c.mq + N * K;
+    const int mmax = prm.use_nlp ? (c.mq + N * K + 4 * N) : c.mq;
+    // carve LDS (offsets must match srb_lds_doubles())
+    double *p = lds;
+    c.Z = p; p += n * nz;
+    c.x = p; p += n; c.q = p; p += n; c.rx = p; p += n; c.dx = p; p += n; c.tv = p; p += n; c.D = p; p += n;
+    c.ref = p; p += 4 * N; c.foot = p; p += 2 * C * N; c.offv = p; p += 2 * (N - 1) + 3 * N;
+    c.s = p; p += mmax; c.z = p; p += mmax; c.rz = p; p += mmax; c.dz = p; p += mmax;
+    c.dsv = p; p += mmax; c.dsT = p; p += mmax; c.om = p; p += mmax; c.hvec = p; p += mmax;
+    c.jc = p; p += 2 * N * K + 2; c.obs = p; p += 2 * N * K + 2; c.eps = p; p += K + 1;
+    c.Hc = p; p += nz * nz; c.L = p; p += nz * nz; c.ZtZ = p; p += nz * nz; c.ZtZL = p; p += nz * nz;
+
+    // ---- load inputs (a1/a2/a3: x0, reference window, footholds)
+    const double *x0 = x0g + 4 * (size_t)agent;
+    for (int i = c.tid; i < 4 * N; i += WAVE) c.ref[i] = refg[(size_t)agent * 4 * N + i];
+    for (int i = c.tid; i < 2 * C * N; i += WAVE) c.foot[i] = footg[(size_t)agent * 2 * C * N + i];
+    __syncthreads();
+    const double px = x0[0], py = x0[2];
+
+    // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
+    for (int i = c.tid; i < n * nz; i += WAVE) c.Z[i] = 0.0;
+    __syncthreads();
+    if (c.tid == 0) {
+        double X[4] = {x0[0], x0[1], x0[2], x0[3]};
+        for (int k = 0; k < N; k++) {
+            double u0 = c.foot[(k * 2 + 0) * C + C - 1], u1 = c.foot[(k * 2 + 1) * C + C - 1];
+            double Xn[4];
+            for (int d = 0; d < 4; d++)
+                Xn[d] = prm.Ad[d * 4] * X[0] + prm.Ad[d * 4 + 1] * X[1] + prm.Ad[d * 4 + 2] * X[2] + prm.Ad[d * 4 + 3] * X[3] +
+                        prm.Bd[d * 2] * u0 + prm.Bd[d * 2 + 1] * u1;
+            for (int d = 0; d < 4; d++) { X[d] = Xn[d]; c.x[4 * k + d] = Xn[d]; }
+            c.x[4 * N + 2 * k] = u0; c.x[4 * N + 2 * k + 1] = u1;
+            for (int j = 0; j < C; j++) c.x[6 * N + C * k + j] = (j == C - 1) ? 1.0 : 0.0;
+        }
+        c.x[n - 1] = 0.0;
+    }
+    for (int col = c.tid; col < nz - 1; col += WAVE) {
+        int j = col / (C - 1), i = col % (C - 1);
+        double g0 = c.foot[(j * 2 + 0) * C + i] - c.foot[(j * 2 + 0) * C + C - 1];
+        double g1 = c.foot[(j * 2 + 1) * C + i] - c.foot[(j * 2 + 1) * C + C - 1];
+        c.Z[(6 * N + C * j + i) * nz + col] = 1.0;
+        c.Z[(6 * N + C * j + C - 1) * nz + col] = -1.0;
+        c.Z[(4 * N + 2 * j) * nz + col] = g0;
+        c.Z[(4 * N + 2 * j + 1) * nz + col] = g1;
+        double v[4];
+        for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1;
+        for (int k = j; k < N; k++) {
+            for (int d = 0; d < 4; d++) c.Z[(4 * k + d) * nz + col] = v[d];
+            double t[4];
+            for (int d = 0; d < 4; d++) t[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3];
+            for (int d = 0; d < 4; d++) v[d] = t[d];
+        }
+    }
+    if (c.tid == 0) c.Z[(n - 1) * nz + nz - 1] = 1.0;
+    __syncthreads();
+
+    // =========================== QP stage (iSWIFT, Prime.c:35-230) ===========================
+    c.m = c.mq; c.nl = 0;
+    for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
+    for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0;     // kkt_initialize: -I block
+    __syncthreads();
+    int qp_flag = 3, qp_it = 0;
+    build_H(c, 0.0);
+    for (int i = c.tid; i < nz * nz; i += WAVE) c.L[i] = c.Hc[i];
+    __syncthreads();
+    if (chol_lds(c, c.L, nz) != 0) {
+        qp_flag = 1;
+    } else {
+        // r1 = -c - P xbar ; r3 = h - G xbar   ->  dx ; x = xbar + dx
+        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
+        for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.hvec[r] - row_dot(c, r, c.x);
+        __syncthreads();
+        for (int v = c.tid; v < n; v += WAVE) c.rx[v] = c.tv[v];
+        __syncthreads();
+        newton_solve(c, c.rx, c.dz);   // dz <- G x - h (z of the init system)
+        for (int v = c.tid; v < n; v += WAVE) c.x[v] += c.dx[v];
+        __syncthreads();
+        // q = A'y = -c - P x - G'(G x - h)
+        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
+        __syncthreads();
+        jt_apply(c, c.dz, c.q, c.tv, -1.0);
+        // s, z from z_inter = h - G x (Auxilary.c:716-746)
+        double mn = 1e300, mx = -1e300;
+        for (int r = c.tid; r < c.m; r += WAVE) {
+            double zi = c.hvec[r] - row_dot(c, r, c.x);
+            c.rz[r] = zi;
+            mn = fmin(mn, zi); mx = fmax(mx, zi);
+        }
+        mn = wmin(mn); mx = -wmin(-mx);
+        double ap = -mn, ad = mx;
+        for (int r = c.tid; r < c.m; r += WAVE) {
+            double zi = c.rz[r];
+            c.s[r] = (ap < 0) ? zi : zi + (1 + ap);
+            c.z[r] = (ad < 0) ? -zi : -zi + (1 + ad);
+        }
+        __syncthreads();
+        qp_flag = ipm(c, prm.qp_maxit, &qp_it);
+    }
+    if (x_qp_out)
+        for (int v = c.tid; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = c.x[v];
+
+    // =========================== NLP stage (replaces SnoptSolver::Solve) ===========================
+    int nlp_flag = 0, nlp_it = 0;
+    if (prm.use_nlp) {
+        c.nl = 1; c.m = mmax;
+        // obstacle list per grid: K_obs nearest static (MPC_dist.cpp:371-396) + K_nbr neighbours
+        if (c.tid == 0) {
+            int chosen[SRB_MAX_K];
+            for (int j = 0; j < prm.K_obs; j++) {
+                double best = 1e300; int bi = -1;
+                for (int i = 0; i < n_obs; i++) {
+                    int used = 0;
+                    for (int t = 0; t < j; t++) used |= (chosen[t] == i);
+                    if (used) continue;
+                    double dx = px - obstacles[2 * i], dy = py - obstacles[2 * i + 1];
+                    double d = dx * dx + dy * dy;
+                    if (d < best) { best = d; bi = i; }
+                }
+                chosen[j] = bi;
+                c.eps[j] = prm.eps_obs;
+                for (int k = 0; k < N; k++) {
+                    c.obs[2 * (k * K + j)] = bi >= 0 ? obstacles[2 * bi] : 1e6;
+                    c.obs[2 * (k * K + j) + 1] = bi >= 0 ? obstacles[2 * bi + 1] : 1e6;
+                }
+            }
+            for (int j = 0; j < prm.K_nbr; j++) {
+                int bi = nbr_idx ? nbr_idx[(size_t)agent * prm.K_nbr + j] : -1;
+                c.eps[prm.K_obs + j] = prm.eps_nbr;
+                for (int k = 0; k < N; k++) {
+                    double t = prm.Ts * (k + 1);
+                    c.obs[2 * (k * K + prm.K_obs + j)] = bi >= 0 ? nbr_state[4 * (size_t)bi] + nbr_state[4 * (size_t)bi + 2] * t : 1e6;
+                    c.obs[2 * (k * K + prm.K_obs + j) + 1] = bi >= 0 ? nbr_state[4 * (size_t)bi + 1] + nbr_state[4 * (size_t)bi + 3] * t : 1e6;
+                }
+            }
+        }
+        __syncthreads();
+        for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
+        __syncthreads();
+        obstacle_coefs(c);
+        // slacks: shifted h - g(x); duals 1
+        double mn = 1e300;
+        for (int r = c.tid; r < c.m; r += WAVE) {
+            double g;
+            if (r >= c.rO && r < c.rV) {
+                int o = r - c.rO, k = o / K;
+                double dx = c.x[4 * k] - c.obs[2 * o], dy = c.x[4 * k + 2] - c.obs[2 * o + 1];
+                g = -(dx * dx + dy * dy) - c.x[n - 1];
+            } else g = row_dot(c, r, c.x);
+            c.rz[r] = c.hvec[r] - g;
+            mn = fmin(mn, c.rz[r]);
+        }
+        mn = wmin(mn);
+        double ap = -mn;
+        for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] = (ap < 0) ? c.rz[r] : c.rz[r] + (1 + ap); c.z[r] = 1.0; }
+        // Z'Z and its factor (projection for q0; inertia correction metric)
+        for (int pidx = c.tid; pidx < nz * nz; pidx += WAVE) {
+            int a = pidx / nz, b = pidx % nz;
+            double acc = 0;
+            for (int v = 0; v < n; v++) acc += c.Z[v * nz + a] * c.Z[v * nz + b];
+            c.ZtZ[pidx] = acc; c.ZtZL[pidx] = acc;
+        }
+        __syncthreads();
+        chol_lds(c, c.ZtZL, nz);
+        // v = P x + c + J'z ; rx0 = -Z (Z'Z)^-1 Z' v ; q = -v - rx0
+        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = Pdiag(c, v) * c.x[v] + cvec(c, v);
+        __syncthreads();
+        jt_apply(c, c.z, c.rx, c.tv, 1.0);
+        double g = zt_mul(c, c.rx);
+        double t = chol_solve_reg(c, c.ZtZL, nz, g);
+        z_mul(c, t, c.dx);
+        for (int v = c.tid; v < n; v += WAVE) c.q[v] = -c.rx[v] + c.dx[v];
+        __syncthreads();
+        // the inertia-correction term delta*Z'Z is added inside build_H's caller via D (full-space delta I)
+        nlp_flag = ipm(c, prm.nlp_maxit, &nlp_it);
+    }
+
+    // ---- outputs
+    for (int v = c.tid; v < n; v += WAVE) x_out[(size_t)agent * n + v] = c.x[v];
+    double f = 0;
+    for (int v = c.tid; v < n; v += WAVE) f += 0.5 * Pdiag(c, v) * c.x[v] * c.x[v] + cvec(c, v) * c.x[v];
+    f = wsum(f);
+    if (c.tid == 0) {
+        obj_out[agent] = f;
+        status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
+        iters_out[2 * agent] = qp_it; iters_out[2 * agent + 1] = nlp_it;
+    }
+}
+
+// --------------------------------------------------------------------------- k nearest neighbours
+// One thread per agent; neighbour states streamed through LDS tiles.  Order: (d^2, index)
+// ascending -- the order the reference's strict-'<' argmin scan produces (MPC_dist.cpp:373-382).
+extern "C" __global__ void __launch_bounds__(256)
+srb_knn_kernel(int n_agents, int agent_offset, const double *__restrict__ state, int n_all, int K,
+               int *__restrict__ nbr_idx)
+{
+    __shared__ double tile[1024 * 2];
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    const int self = agent_offset + a;
+    double px = 0, py = 0;
+    if (a < n_agents) { px = state[4 * (size_t)self]; py = state[4 * (size_t)self + 1]; }
+    double bd[SRB_MAX_K]; int bi[SRB_MAX_K];
+    for (int j = 0; j < SRB_MAX_K; j++) { bd[j] = 1e300; bi[j] = -1; }
+    for (int base = 0; base < n_all; base += 1024) {
+        int cnt = n_all - base < 1024 ? n_all - base : 1024;
+        __syncthreads();
+        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
+            tile[2 * i] = state[4 * (size_t)(base + i)];
+            tile[2 * i + 1] = state[4 * (size_t)(base + i) + 1];
+        }
+        __syncthreads();
+        if (a < n_agents)
+            for (int i = 0; i < cnt; i++) {
+                int gi = base + i;
+                if (gi == self) continue;
+                double dx = px - tile[2 * i], dy = py - tile[2 * i + 1];
+                double d = dx * dx + dy * dy;
+                if (d < bd[K - 1] || (d == bd[K - 1] && gi < bi[K - 1])) {
+                    int j = K - 1;
+                    while (j > 0 && (d < bd[j - 1] || (d == bd[j - 1] && gi < bi[j - 1]))) { bd[j] = bd[j - 1]; bi[j] = bi[j - 1]; j--; }
+                    bd[j] = d; bi[j] = gi;
+                }
+            }
+    }
+    if (a < n_agents)
+        for (int j = 0; j < K; j++) nbr_idx[(size_t)a * K + j] = bi[j];
+}

@@ -1,0 +1,193 @@
+"""srbnmpc -- batched CBF-NMPC solver for MI355X, Python host side.
+
+Thin ctypes layer over the C ABI in include/srbnmpc.h (libsrbnmpc.so, HIP kernels for
+gfx950).  There is no CPU fallback: if the library is missing, or no GPU is visible,
+constructing a solver raises.
+
+    BatchSolver   -- whole agent batch per call (host numpy or device torch buffers)
+    MPCDist       -- per-agent object with the reference's MPC_dist call surface
+                     (/root/reference/include/MPC_dist.hpp:137-190)
+    workload      -- synthetic agent batches with the SURVEY.md §8d distributions
+"""
+from __future__ import annotations
+
+import ctypes
+import os
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "libsrbnmpc.so")
+
+_dp = ctypes.POINTER(ctypes.c_double)
+_ip = ctypes.POINTER(ctypes.c_int)
+
+OPTIMAL, KKTFAIL, MAXIT, FATAL = 0, 1, 2, 3
+
+
+class Params(ctypes.Structure):
+    """Mirror of srb_params (include/srbnmpc.h)."""
+    _fields_ = [("N", ctypes.c_int), ("C", ctypes.c_int), ("K_obs", ctypes.c_int), ("K_nbr", ctypes.c_int),
+                ("grav", ctypes.c_double), ("hcom", ctypes.c_double), ("Ts", ctypes.c_double), ("mu", ctypes.c_double),
+                ("Qw", ctypes.c_double), ("Pw", ctypes.c_double), ("Rw", ctypes.c_double), ("Sw", ctypes.c_double),
+                ("box", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
+                ("vsat", ctypes.c_double), ("tol", ctypes.c_double),
+                ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int), ("use_nlp", ctypes.c_int)]
+
+    @property
+    def nv(self) -> int:
+        return (6 + self.C) * self.N + 1
+
+    def as_dict(self):
+        return {k: getattr(self, k) for k, _ in self._fields_}
+
+
+class Batch(ctypes.Structure):
+    """Mirror of srb_batch."""
+    _fields_ = [("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
+                ("n_obs", ctypes.c_int), ("n_all", ctypes.c_int), ("agent_offset", ctypes.c_int),
+                ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip)]
+
+
+_lib = None
+
+
+def lib():
+    """Load libsrbnmpc.so; raise loudly when it is missing (no fallback path exists)."""
+    global _lib
+    if _lib is None:
+        if not os.path.exists(LIB_PATH):
+            raise RuntimeError(f"srbnmpc: {LIB_PATH} not built (run __graft_entry__.build() or make -C srb-cbf-nmpc_amd)")
+        L = ctypes.CDLL(LIB_PATH)
+        L.srb_params_default.argtypes = [ctypes.POINTER(Params), ctypes.c_int, ctypes.c_int]
+        L.srb_nv.argtypes = [ctypes.POINTER(Params)]
+        L.srb_lds_bytes.argtypes = [ctypes.POINTER(Params)]
+        L.srb_ctx_create.argtypes = [ctypes.POINTER(Params), ctypes.c_int, ctypes.c_int, ctypes.POINTER(ctypes.c_void_p)]
+        L.srb_ctx_destroy.argtypes = [ctypes.c_void_p]
+        for f in ("srb_solve_batch", "srb_solve_qp"):
+            getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch)]
+        L.srb_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_void_p]
+        L.srb_sync.argtypes = [ctypes.c_void_p]
+        L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+        L.srb_fit_bezier.argtypes = [_dp, _dp, _dp]
+        L.srb_last_error.restype = ctypes.c_char_p
+        _lib = L
+    return _lib
+
+
+def default_params(N: int = 4, C: int = 4, **overrides) -> Params:
+    p = Params()
+    lib().srb_params_default(ctypes.byref(p), N, C)
+    for k, v in overrides.items():
+        setattr(p, k, v)
+    return p
+
+
+def lds_bytes(p: Params) -> int:
+    return lib().srb_lds_bytes(ctypes.byref(p))
+
+
+def _check(rc: int):
+    if rc != 0:
+        raise RuntimeError(f"srbnmpc error {rc}: {lib().srb_last_error().decode()}")
+
+
+def _f64(a):
+    return np.ascontiguousarray(a, dtype=np.float64)
+
+
+def _p(a):
+    if a is None:
+        return None
+    if a.dtype == np.float64:
+        return a.ctypes.data_as(_dp)
+    return a.ctypes.data_as(_ip)
+
+
+class BatchSolver:
+    """One HIP context solving batches of up to `max_agents` agents.
+
+    solve(...)        host numpy in/out (srb_solve_batch, synchronous)
+    solve_device(...) torch CUDA tensors in/out (srb_solve_batch_device, async on a stream)
+    """
+
+    def __init__(self, params: Params, max_agents: int, device: int = 0):
+        self.params = params
+        self.max_agents = int(max_agents)
+        self.device = int(device)
+        h = ctypes.c_void_p()
+        _check(lib().srb_ctx_create(ctypes.byref(params), self.max_agents, self.device, ctypes.byref(h)))
+        self._h = h
+
+    def close(self):
+        if getattr(self, "_h", None) is not None and self._h.value:
+            lib().srb_ctx_destroy(self._h)
+            self._h = None
+
+    def __del__(self):
+        try:
+            self.close()
+        except Exception:
+            pass
+
+    # --------------------------------------------------------------- host path
+    def solve(self, x0, ref, foot, obstacles=None, nbr_state=None, agent_offset: int = 0, qp_only: bool = False):
+        p = self.params
+        x0 = _f64(x0).reshape(-1, 4)
+        A = x0.shape[0]
+        ref = _f64(ref).reshape(A, 4 * p.N)
+        foot = _f64(foot).reshape(A, p.N * 2 * p.C)
+        ob = _f64(obstacles if obstacles is not None else np.zeros((0, 2))).reshape(-1, 2)
+        nb = _f64(nbr_state).reshape(-1, 4) if nbr_state is not None else None
+        out = dict(x_qp=np.zeros((A, p.nv)), x=np.zeros((A, p.nv)), obj=np.zeros(A),
+                   status=np.zeros((A, 2), np.int32), iters=np.zeros((A, 2), np.int32))
+        b = Batch(_p(x0), _p(ref), _p(foot), _p(ob) if ob.size else None, _p(nb) if nb is not None else None,
+                  ob.shape[0], nb.shape[0] if nb is not None else 0, int(agent_offset),
+                  _p(out["x_qp"]), _p(out["x"]), _p(out["obj"]), _p(out["status"]), _p(out["iters"]))
+        fn = lib().srb_solve_qp if qp_only else lib().srb_solve_batch
+        _check(fn(self._h, A, ctypes.byref(b)))
+        return out
+
+    # --------------------------------------------------------------- device path
+    def solve_device(self, x0, ref, foot, obstacles, nbr_state, out, agent_offset: int = 0, stream=None):
+        """All arguments torch tensors on this solver's device (float64 / int32), contiguous.
+        `out` is a dict with x_qp (or None), x, obj, status, iters.  Asynchronous."""
+        def dptr(t):
+            return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
+
+        def iptr(t):
+            return ctypes.cast(ctypes.c_void_p(t.data_ptr()), _ip)
+        A = x0.shape[0]
+        b = Batch(dptr(x0), dptr(ref), dptr(foot), dptr(obstacles), dptr(nbr_state),
+                  0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],
+                  int(agent_offset), dptr(out.get("x_qp")), dptr(out["x"]), dptr(out["obj"]),
+                  iptr(out["status"]), iptr(out["iters"]))
+        s = ctypes.c_void_p(stream) if stream is not None else None
+        _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), s))
+
+    def sync(self):
+        _check(lib().srb_sync(self._h))
+
+    def last_kernel_ms(self):
+        a = ctypes.c_float(); b = ctypes.c_float()
+        _check(lib().srb_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
+        return a.value, b.value
+
+
+def fit_bezier(buf, X):
+    """fitComTrajectory_eventbase (MPC_dist.cpp:784-855): alpha_COM (4x5)."""
+    a = np.zeros(20)
+    lib().srb_fit_bezier(_p(_f64(buf)), _p(_f64(X)), _p(a))
+    return a.reshape(4, 5)
+
+
+def split(params: Params, x):
+    """Split decision vectors (..., nv) into X (...,N,4), U (...,N,2), lambda (...,N,C), s (...)."""
+    N, C = params.N, params.C
+    x = np.asarray(x)
+    return (x[..., :4 * N].reshape(*x.shape[:-1], N, 4), x[..., 4 * N:6 * N].reshape(*x.shape[:-1], N, 2),
+            x[..., 6 * N:6 * N + C * N].reshape(*x.shape[:-1], N, C), x[..., -1])
+
+
+from .mpc_dist import MPCDist  # noqa: E402
+from . import workload  # noqa: E402
