@@ -1,0 +1,197 @@
+#!/usr/bin/env python3
+"""Benchmark: batched CBF-NMPC solves on MI355X (BASELINE.json metric).
+
+    python bench.py [--gpus N --steps K --warmup W] [--config 2] [--agents A]
+
+One "step" = one pass of the hot path over one batch: (configs with inter-agent rows:
+all-gather of the neighbour snapshot over RCCL) + kNN + QP stage + NLP stage for every
+agent of the batch, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun),
+agents sharded agent-major, weak scaling (fixed agents per GPU).  Rank 0 prints one JSON
+line.  Configs (BASELINE.json "configs"):
+    1  1 agent, N=4 reference mode (KAT-2 shape)            -- CPU plumbing case
+    2  64 agents/GPU, N=10, trot, 3 static obstacles        -- default (configs[1])
+    3  1024 agents/GPU, N=10, 3 static + 8 nearest agents   -- configs[2]
+    4  1024 agents/GPU, as 3 with the RCCL all-gather       -- configs[3] (8 GPUs = 8192)
+    5  2048 agents/GPU, N=20, 3 static + 8 nearest agents   -- configs[4] shape, fp64
+"""
+import argparse
+import json
+import os
+import sys
+import time
+
+import numpy as np
+import torch
+import torch.distributed as dist
+
+ROOT = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(ROOT, "srb-cbf-nmpc_amd"))
+
+import srbnmpc  # noqa: E402
+from srbnmpc import dist as sdist, workload  # noqa: E402
+
+METRIC = "NMPC solves/sec (whole node) + p99 solve latency, N-agent batch horizon=10"
+FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 (vector and matrix) dense peak, spec
+CONFIGS = {
+    1: dict(agents=1, N=4, C=4, K_obs=1, K_nbr=0, name="1 agent, N=4, stand (reference mode, KAT-2 shape)"),
+    2: dict(agents=64, N=10, C=2, K_obs=3, K_nbr=0, name="64 agents/GPU, horizon 10, trot, 3 static CBF obstacles, fp64"),
+    3: dict(agents=1024, N=10, C=2, K_obs=3, K_nbr=8, name="1024 agents/GPU, horizon 10, 3 static + 8-nearest inter-agent CBF, fp64"),
+    4: dict(agents=1024, N=10, C=2, K_obs=3, K_nbr=8, name="1024 agents/GPU + RCCL all-gather of neighbour CoM states, horizon 10, fp64"),
+    5: dict(agents=2048, N=20, C=2, K_obs=3, K_nbr=8, name="2048 agents/GPU, horizon 20, 3 static + 8-nearest, fp64"),
+}
+
+
+def dense_equiv_flops(p, iters):
+    """SURVEY.md §8d per-iteration figure: (2/3) d^3 + 4 d^2 with d = nv + neq (the unreduced
+    dense KKT of the north-star formulation), times the actual per-agent iteration counts."""
+    d = p.nv + 7 * p.N
+    return float(iters.sum()) * ((2.0 / 3.0) * d ** 3 + 4.0 * d ** 2)
+
+
+def io_bytes(p, n_agents, n_obs, n_all):
+    """Algorithmic HBM bytes per launch: inputs + outputs once."""
+    per = 8 * (4 + 4 * p.N + 2 * p.C * p.N) + 8 * (2 * p.nv + 1) + 16
+    return n_agents * per + 16 * n_obs + 32 * n_all
+
+
+def cpu_baseline(cfg, b, budget_s):
+    """Oracle (CPU restatement of the same algorithm, oracle/) timed on this host's cores
+    on a bounded sample of the same workload."""
+    sys.path.insert(0, ROOT)
+    import oracle
+    nthreads = max(1, min(16, os.cpu_count() or 1))
+    p = oracle.params(cfg["N"], cfg["C"], K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"])
+    A = b["x0"].shape[0]
+    sample = min(A, max(nthreads * 2, 16))
+    t0 = time.perf_counter(); solved = 0
+    while True:
+        oracle.solve_batch(p, b["x0"][:sample], b["ref"][:sample], b["foot"][:sample], b["obstacles"],
+                           b["nbr_state"], nthreads=nthreads)
+        solved += sample
+        if time.perf_counter() - t0 > budget_s:
+            break
+    dt = time.perf_counter() - t0
+    return {"value": solved / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
+            "sample": f"{solved} solves ({sample}-agent slices of the same batch) in {dt:.1f} s, QP+NLP, "
+                      f"{nthreads} threads"}
+
+
+def main():
+    ap = argparse.ArgumentParser()
+    ap.add_argument("--gpus", type=int, default=1)
+    ap.add_argument("--steps", type=int, default=50)
+    ap.add_argument("--warmup", type=int, default=5)
+    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--agents", type=int, default=0, help="agents per GPU (override)")
+    ap.add_argument("--cpu-seconds", type=float, default=12.0)
+    ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    args = ap.parse_args()
+
+    world = int(os.environ.get("WORLD_SIZE", "1"))
+    rank = int(os.environ.get("RANK", "0"))
+    local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
+    torch.cuda.set_device(local_rank)
+    dev = torch.device("cuda", local_rank)
+
+    cfg = dict(CONFIGS[args.config])
+    A_local = args.agents or cfg["agents"]
+    A_total = A_local * world
+    N, C = cfg["N"], cfg["C"]
+    p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
+    # the whole swarm is generated identically on every rank; each rank keeps its shard
+    b = workload.make_batch(A_total, N, C, seed=1234)
+    lo, hi = sdist.shard_range(A_total, world, rank)
+    sh = {k: (v[lo:hi] if k not in ("obstacles", "nbr_state") else v) for k, v in b.items()}
+    t = {k: torch.as_tensor(np.ascontiguousarray(v).reshape(v.shape[0], -1), dtype=torch.float64, device=dev)
+         for k, v in sh.items()}
+    nbr_local = t["nbr_state"][lo:hi].contiguous()
+    nbr_all = t["nbr_state"] if cfg["K_nbr"] > 0 else None
+    n_loc = hi - lo
+    out = dict(x_qp=None, x=torch.zeros((n_loc, p.nv), dtype=torch.float64, device=dev),
+               obj=torch.zeros(n_loc, dtype=torch.float64, device=dev),
+               status=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
+               iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev))
+    solver = srbnmpc.BatchSolver(p, n_loc, local_rank)
+    stream = torch.cuda.current_stream(dev)
+    exchange = cfg["K_nbr"] > 0 and world > 1
+
+    def step():
+        nb = sdist.gather_states(nbr_local, A_total, world) if exchange else nbr_all
+        solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nb, out, agent_offset=lo,
+                            stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    kern = []
+    for _ in range(3):            # kernel duration on the stream it runs on (HIP events in the C ABI)
+        step()
+        kern.append(solver.last_kernel_ms())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_step = np.array([a.elapsed_time(bb) for a, bb in ev])
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+        lat = torch.as_tensor(per_step, dtype=torch.float64, device=dev)
+        gl = [torch.empty_like(lat) for _ in range(world)]
+        dist.all_gather(gl, lat)
+        per_step = torch.cat(gl).cpu().numpy()
+    ms_per_step = elapsed * 1e3 / args.steps
+    value = A_total * args.steps / elapsed
+
+    status = out["status"].cpu().numpy(); iters = out["iters"].cpu().numpy()
+    solve_ms = float(np.median([k[1] for k in kern]))
+    flops = dense_equiv_flops(p, iters)
+    achieved = flops / (solve_ms * 1e-3) / 1e12
+    traffic = None
+    if os.path.exists(args.traffic_json):
+        try:
+            tj = json.load(open(args.traffic_json))
+            if tj.get("config") == args.config and tj.get("agents") == n_loc:
+                traffic = tj.get("hbm_bytes_per_launch")
+        except Exception:
+            traffic = None
+    line = {
+        "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+        "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
+        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": cfg["name"], "agents_per_gpu": A_local, "agents_total": A_total, "horizon": N,
+                   "contacts": C, "K_obs": cfg["K_obs"], "K_nbr": cfg["K_nbr"], "parallelism": f"agents sharded x{world}"},
+        "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
+        "optimal_frac": float((status == 0).all(1).mean()),
+        "iters_mean": [float(iters[:, 0].mean()), float(iters[:, 1].mean())],
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "kernel": "srb_nmpc_kernel", "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
+                     "flop_model": "dense-equivalent unreduced KKT per IPM iteration, SURVEY.md 8(d)",
+                     "io_bytes_per_launch": io_bytes(p, n_loc, sh["obstacles"].shape[0], A_total if cfg["K_nbr"] else 0)},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        line["cpu_baseline"] = cpu_baseline(cfg, sh, args.cpu_seconds)
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    solver.close()
+    if world > 1:
+        dist.destroy_process_group()
+
+
+if __name__ == "__main__":
+    main()

@@ -124,6 +124,24 @@ def qp_solve(Pd, c, A, b, G, h, maxit=25, tol=1e-6):
     return x, f, it.value, q
 
 
+def qp_solve_full(P, c, A, b, G, h, maxit=25, tol=1e-6):
+    """iSWIFT restatement with a general symmetric P (KAT-1, Matrices_small.h)."""
+    n = P.shape[0]; m = G.shape[0]; pp = A.shape[0]
+    x = np.zeros(n); it = ctypes.c_int()
+    arrs = [_c(a) for a in (P, c, A, b, G, h)]
+    f = lib().orc_qp_solve_full(n, m, pp, *[_ptr(a) for a in arrs], maxit, ctypes.c_double(tol), _ptr(x),
+                                ctypes.byref(it))
+    return x, f, it.value
+
+
+def ccs_to_dense(rows, cols, jc, ir, pr):
+    D = np.zeros((rows, cols))
+    for j in range(cols):
+        for k in range(int(jc[j]), int(jc[j + 1])):
+            D[int(ir[k]), j] += pr[k]
+    return D
+
+
 def select_obstacles(p: OrcParams, x0, obstacles, nbr_state=None, self_idx=-1):
     K = p.K_obs + p.K_nbr
     obs = np.zeros((p.N, max(K, 1), 2)); eps = np.zeros(max(K, 1))

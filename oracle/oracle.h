@@ -79,6 +79,10 @@ int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
                  const double *A, const double *b, const double *G, const double *h,
                  int maxit, double tol, double *x_out, double *q_out, int *iters_out);
 
+int orc_qp_solve_full(int n, int m, int p, const double *P, const double *c,
+                      const double *A, const double *b, const double *G, const double *h,
+                      int maxit, double tol, double *x_out, int *iters_out);
+
 /* NLP stage (replaces SnoptSolver::Solve, MPC_dist.cpp:402-427). */
 int orc_nlp_solve(const orc_params *p, const double x0[4], const double *foot,
                   const double *Pd, const double *c, const double *A, const double *b,

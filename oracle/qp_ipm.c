@@ -18,15 +18,17 @@
 
 typedef struct {
     int n, m, p;
-    const double *Pd, *A, *G;
+    const double *Pd, *Pf, *A, *G;   /* P diagonal (Pd) or full row-major (Pf, when non-NULL) */
     int *gnz;      /* [m][4] column indices of row r's nonzeros (-1 padded) */
     double *gval;  /* [m][4] */
     double *H, *S, *HiAt, *t1, *t2;
+    int use_lu;          /* general (possibly indefinite) P: LU on [H A'; A 0] instead of Schur */
+    double *K; int *piv;
 } kktws;
 
 static void ws_init(kktws *w, int n, int m, int p, const double *Pd, const double *A, const double *G)
 {
-    w->n = n; w->m = m; w->p = p; w->Pd = Pd; w->A = A; w->G = G;
+    w->n = n; w->m = m; w->p = p; w->Pd = Pd; w->Pf = NULL; w->A = A; w->G = G;
     w->gnz = (int *)malloc(sizeof(int) * 4 * (m ? m : 1));
     w->gval = (double *)malloc(sizeof(double) * 4 * (m ? m : 1));
     for (int r = 0; r < m; r++) {
@@ -40,11 +42,15 @@ static void ws_init(kktws *w, int n, int m, int p, const double *Pd, const doubl
     w->HiAt = (double *)malloc(sizeof(double) * (size_t)n * (p ? p : 1));
     w->t1 = (double *)malloc(sizeof(double) * (n + p + m + 8));
     w->t2 = (double *)malloc(sizeof(double) * (n + p + m + 8));
+    w->use_lu = 0;
+    w->K = (double *)malloc(sizeof(double) * (size_t)(n + p) * (n + p));
+    w->piv = (int *)malloc(sizeof(int) * (n + p));
 }
 
 static void ws_free(kktws *w)
 {
     free(w->gnz); free(w->gval); free(w->H); free(w->S); free(w->HiAt); free(w->t1); free(w->t2);
+    free(w->K); free(w->piv);
 }
 
 static void gmul(const kktws *w, const double *x, double *y)   /* y = G x */
@@ -68,7 +74,8 @@ static int kkt_factor(kktws *w, const double *wgt)
     const int n = w->n, m = w->m, p = w->p;
     double *H = w->H;
     memset(H, 0, sizeof(double) * n * n);
-    for (int i = 0; i < n; i++) H[i * n + i] = w->Pd[i];
+    if (w->Pf) memcpy(H, w->Pf, sizeof(double) * n * n);
+    else for (int i = 0; i < n; i++) H[i * n + i] = w->Pd[i];
     for (int r = 0; r < m; r++) {
         double iw = 1.0 / wgt[r];
         for (int a = 0; a < 4; a++) {
@@ -78,6 +85,17 @@ static int kkt_factor(kktws *w, const double *wgt)
                 H[ia * n + ib] += iw * w->gval[4 * r + a] * w->gval[4 * r + bb];
             }
         }
+    }
+    if (w->use_lu) {
+        const int d = n + p;
+        memset(w->K, 0, sizeof(double) * (size_t)d * d);
+        for (int i = 0; i < n; i++) for (int j = 0; j < n; j++) w->K[(size_t)i * d + j] = H[i * n + j];
+        for (int k = 0; k < p; k++)
+            for (int j = 0; j < n; j++) {
+                w->K[(size_t)(n + k) * d + j] = w->A[(size_t)k * n + j];
+                w->K[(size_t)j * d + n + k] = w->A[(size_t)k * n + j];
+            }
+        return orc_lu(d, w->K, w->piv);
     }
     if (orc_chol(n, H)) return -1;
     for (int j = 0; j < p; j++) {
@@ -105,6 +123,16 @@ static void kkt_solve(kktws *w, const double *wgt, const double *r1, const doubl
     for (int i = 0; i < n; i++) g[i] = r1[i];
     for (int r = 0; r < m; r++) t[r] = r3[r] / wgt[r];
     gtmul_add(w, t, g);                                   /* g = r1 + G' W^-1 r3 */
+    if (w->use_lu) {
+        for (int i = 0; i < n; i++) t[i] = g[i];
+        for (int k = 0; k < p; k++) t[n + k] = r2[k];
+        orc_lu_solve(n + p, w->K, w->piv, t);
+        for (int i = 0; i < n; i++) dx[i] = t[i];
+        for (int k = 0; k < p; k++) dy[k] = t[n + k];
+        gmul(w, dx, dz);
+        for (int r = 0; r < m; r++) dz[r] = (dz[r] - r3[r]) / wgt[r];
+        return;
+    }
     for (int i = 0; i < n; i++) t[i] = g[i];
     orc_chol_solve(n, w->H, t);                           /* t = H^-1 g */
     for (int i = 0; i < p; i++) {
@@ -135,12 +163,14 @@ static double steplen(const double *v, const double *dv, int m)
     return f ? a : 1.0;
 }
 
-int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
-                 const double *A, const double *b, const double *G, const double *h,
-                 int maxit, double tol, double *x_out, double *q_out, int *iters_out)
+static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf, const double *c,
+                         const double *A, const double *b, const double *G, const double *h,
+                         int maxit, double tol, double *x_out, double *q_out, int *iters_out)
 {
     kktws w;
     ws_init(&w, n, m, p, Pd, A, G);
+    w.Pf = Pf;
+    w.use_lu = (Pf != NULL);
     double *x = calloc(n, sizeof(double)), *y = calloc(p + 1, sizeof(double));
     double *s = calloc(m, sizeof(double)), *z = calloc(m, sizeof(double));
     double *rx = calloc(n, sizeof(double)), *ry = calloc(p + 1, sizeof(double)), *rz = calloc(m, sizeof(double));
@@ -171,7 +201,12 @@ int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
     flag = 2;
     for (int i = 0; i < maxit; i++) {
         /* computeresiduals: rx = -Px - G'z - A'y - c; ry = -Ax + b; rz = -s - Gx + h */
-        for (int j = 0; j < n; j++) rx[j] = -Pd[j] * x[j] - c[j];
+        for (int j = 0; j < n; j++) {
+            double px = 0;
+            if (Pf) for (int k = 0; k < n; k++) px += Pf[(size_t)j * n + k] * x[k];
+            else px = Pd[j] * x[j];
+            rx[j] = -px - c[j];
+        }
         for (int r = 0; r < m; r++) lam[r] = -z[r];
         gtmul_add(&w, lam, rx);
         for (int k = 0; k < p; k++) {
@@ -229,4 +264,19 @@ done:
     free(dsv); free(ds); free(lam); free(wgt); free(r3); free(zi); free(nc);
     ws_free(&w);
     return flag;
+}
+
+int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
+                 const double *A, const double *b, const double *G, const double *h,
+                 int maxit, double tol, double *x_out, double *q_out, int *iters_out)
+{
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out);
+}
+
+/* general (full, symmetric) P -- used for iSWIFT's own test QP (Matrices_small.h) */
+int orc_qp_solve_full(int n, int m, int p, const double *P, const double *c,
+                      const double *A, const double *b, const double *G, const double *h,
+                      int maxit, double tol, double *x_out, int *iters_out)
+{
+    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out);
 }

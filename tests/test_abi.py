@@ -1,0 +1,120 @@
+"""CPU tests of the product library's C ABI and host logic (no GPU compute calls)."""
+import ctypes
+import os
+import re
+
+import numpy as np
+import pytest
+from conftest import ROOT
+
+import oracle
+import srbnmpc
+from srbnmpc import workload
+
+
+def _declared_functions():
+    txt = open(os.path.join(ROOT, "include", "srbnmpc.h")).read()
+    txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
+    return sorted(set(re.findall(r"\b(srb_\w+)\s*\(", txt)))
+
+
+def test_library_exports_every_declared_symbol():
+    names = _declared_functions()
+    assert len(names) >= 12
+    lib = ctypes.CDLL(srbnmpc.LIB_PATH)
+    for n in names:
+        assert hasattr(lib, n), n
+
+
+def test_library_contains_gfx950_code_object():
+    data = open(srbnmpc.LIB_PATH, "rb").read()
+    assert b"gfx950" in data
+    assert b"srb_nmpc_kernel" in data and b"srb_knn_kernel" in data
+
+
+def test_param_defaults_are_the_reference_constants():
+    p = srbnmpc.default_params(4, 4)
+    o = oracle.params(4, 4)
+    for k, _ in srbnmpc.Params._fields_:
+        assert getattr(p, k) == getattr(o, k), k
+    assert (p.N, p.C, p.K_obs, p.K_nbr) == (4, 4, 1, 0)             # MPC_dist.cpp:92,132,371-396
+    assert (p.Qw, p.Pw, p.Rw, p.Sw) == (300.0, 2000.0, 0.1, 3000.0)  # MPC_dist.cpp:172-175
+    assert p.eps_obs == float(np.float32(1.9)) and p.vsat == float(np.float32(0.35))   # float constants
+    assert p.tol == 1e-6 and p.qp_maxit == 25                         # GlobalOptions.h:23-25
+    assert p.nv == 41
+
+
+@pytest.mark.parametrize("N,C,K", [(4, 4, 1), (10, 2, 3), (10, 2, 11), (20, 2, 11), (10, 4, 3)])
+def test_lds_fits_and_sizes(N, C, K):
+    p = srbnmpc.default_params(N, C, K_obs=min(K, 3), K_nbr=max(K - 3, 0))
+    b = srbnmpc.lds_bytes(p)
+    assert 0 < b <= 160 * 1024
+    assert b % 8 == 0
+
+
+def test_fit_bezier_host_matches_oracle():
+    rng = np.random.default_rng(0)
+    for _ in range(5):
+        buf = rng.normal(size=4); X = rng.normal(size=(4, 4))
+        np.testing.assert_allclose(srbnmpc.fit_bezier(buf, X), oracle.fit_bezier(buf, X), atol=1e-12)
+
+
+def test_ctx_create_rejects_bad_params():
+    lib = srbnmpc.lib()
+    p = srbnmpc.default_params(40, 4)          # nz = 121 > 64 lanes
+    h = ctypes.c_void_p()
+    rc = lib.srb_ctx_create(ctypes.byref(p), 8, 0, ctypes.byref(h))
+    assert rc != 0
+    assert b"exceeds" in lib.srb_last_error()
+
+
+def test_no_silent_cpu_fallback_without_gpu():
+    """Without a GPU the solver must fail loudly, never compute on the CPU."""
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        srbnmpc.BatchSolver(srbnmpc.default_params(4, 4), 4)
+
+
+def test_workload_shapes_and_determinism():
+    a = workload.make_batch(16, 10, 2, seed=1)
+    b = workload.make_batch(16, 10, 2, seed=1)
+    for k in a:
+        np.testing.assert_array_equal(a[k], b[k])
+    assert a["x0"].shape == (16, 4) and a["ref"].shape == (16, 40) and a["foot"].shape == (16, 10, 2, 2)
+    assert a["nbr_state"].shape == (16, 4)
+    # footholds: each grid holds one trot diagonal of the default stance
+    F = a["foot"][0, 0]
+    assert np.isclose(F[0, 0] - F[0, 1], 0.2188 + 0.1472) or np.isclose(F[0, 0] - F[0, 1], -(0.2188 + 0.1472))
+
+
+def test_mpcdist_host_planners():
+    """copPlanner_eventbase / footholdsPlanner (MPC_dist.cpp:702-782, 1204-1266) on the host."""
+    m = srbnmpc.MPCDist()
+    m.setAgentID(1)
+    m.setPstart(np.array([0.0, 0.0, 2.0, -1.0, 0, 0, 0, 0]))
+    T = 40
+    Pr = np.arange(8 * T, dtype=float).reshape(8, T)
+    m.setReferenceTrajectory(Pr, -Pr)
+    m.gaitDomain_ = 2
+    ref = m.copPlanner_eventbase(4)
+    np.testing.assert_array_equal(ref.reshape(4, 4)[:, 0], Pr[2, 8:12])    # x of grids
+    np.testing.assert_array_equal(ref.reshape(4, 4)[:, 1], -Pr[2, 8:12])   # xdot
+    np.testing.assert_array_equal(ref.reshape(4, 4)[:, 2], Pr[3, 8:12])    # y
+    m.gaitDomain_ = 0
+    m.contactInd = np.array([1, 0, 0, 1])
+    F = m.footholdsPlanner()
+    np.testing.assert_allclose(F, [[2.0 + 0.2188, 2.0 - 0.1472], [-1.0 - 0.1320, -1.0 + 0.1320]])
+    m.contactInd = np.array([0, 1, 1, 0])
+    F = m.footholdsPlanner()
+    np.testing.assert_allclose(F, [[2.0 + 0.2188, 2.0 - 0.1472], [-1.0 + 0.1320, -1.0 - 0.1320]])
+    np.testing.assert_array_equal(m.get_lastState(), np.zeros(4))
+
+
+def test_split_layout():
+    p = srbnmpc.default_params(10, 2)
+    x = np.arange(p.nv, dtype=float)
+    X, U, L, s = srbnmpc.split(p, x)
+    assert X.shape == (10, 4) and U.shape == (10, 2) and L.shape == (10, 2) and s == p.nv - 1
+    assert X[1, 0] == 4 and U[0, 0] == 40 and L[0, 0] == 60

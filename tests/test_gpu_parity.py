@@ -1,0 +1,251 @@
+"""GPU parity tests: the HIP path (through the C ABI) against the oracle and the goldens.
+
+Tolerances (written here, from SURVEY.md §8c / BASELINE.json north star):
+  * QP stage: X, U, s within 1e-6 abs of the genuine iSWIFT (its own tolerance); in
+    practice ~1e-8 and identical iteration counts.  lambda compared only for C = 2
+    (non-unique for 4 contacts).
+  * NLP stage: X, U, s within 1e-4 abs of the oracle / KKT-certified goldens (north star
+    "||.||_inf < 1e-4"); in practice ~1e-8 with identical iteration counts.
+"""
+import numpy as np
+import pytest
+from conftest import load_golden
+
+import oracle
+from kkt import certify, nlp_rows
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+import srbnmpc  # noqa: E402
+from srbnmpc import workload  # noqa: E402
+
+QP_TOL = 1e-6
+NLP_TOL = 1e-4
+_solvers = {}
+
+
+def solver(N, C, K_obs=1, K_nbr=0, use_nlp=1, max_agents=2048):
+    key = (N, C, K_obs, K_nbr, use_nlp, max_agents)
+    if key not in _solvers:
+        p = srbnmpc.default_params(N, C, K_obs=K_obs, K_nbr=K_nbr, use_nlp=use_nlp)
+        _solvers[key] = srbnmpc.BatchSolver(p, max_agents)
+    return _solvers[key]
+
+
+def xus(N, x):
+    x = np.asarray(x)
+    return np.concatenate([x[..., :6 * N], x[..., -1:]], -1)
+
+
+# ----------------------------------------------------------------------------- goldens
+def test_kat2_reference_instance(kat2):
+    """The reference's logged instance: QP stage == the reference's own logged output and
+    genuine iSWIFT; NLP stage == KKT-certified optimum."""
+    s = solver(4, 4, K_obs=1)
+    foot = np.repeat(kat2["F"][None], 4, 0)
+    out = s.solve(kat2["x0"][None], kat2["ref"][None], foot[None], np.asarray(kat2["obstacle"])[None])
+    assert out["status"][0].tolist() == [0, 0]
+    assert out["iters"][0, 0] == kat2["iters_qp_qd"]
+    xq = out["x_qp"][0]
+    np.testing.assert_allclose(xq[:24], kat2["logged_qp_x"], atol=2e-9, rtol=0)
+    np.testing.assert_allclose(xus(4, xq), xus(4, kat2["x_qp_iswift_qd"]), atol=1e-8, rtol=0)
+    np.testing.assert_allclose(xus(4, out["x"][0]), xus(4, kat2["x_nlp"]), atol=1e-6, rtol=0)
+    assert abs(out["obj"][0] - kat2["obj_nlp"]) < 1e-6
+
+
+def test_qp_random_vs_genuine_iswift():
+    cases = load_golden("qp_random.json")["cases"]
+    groups = {}
+    for cs in cases:
+        groups.setdefault((cs["N"], cs["C"]), []).append(cs)
+    for (N, C), cl in groups.items():
+        s = solver(N, C, use_nlp=0)
+        x0 = np.array([c["x0"] for c in cl]); ref = np.array([c["ref"] for c in cl]); foot = np.array([c["foot"] for c in cl])
+        out = s.solve(x0, ref, foot, qp_only=True)
+        xr = np.array([c["x"] for c in cl])
+        assert (out["status"][:, 0] == 0).all()
+        np.testing.assert_array_equal(out["iters"][:, 0], [c["iters"] for c in cl])
+        np.testing.assert_allclose(xus(N, out["x"]), xus(N, xr), atol=QP_TOL, rtol=0)
+        assert np.abs(xus(N, out["x"]) - xus(N, xr)).max() < 1e-8
+        if C == 2:
+            np.testing.assert_allclose(out["x"], xr, atol=QP_TOL, rtol=0)
+
+
+def test_nlp_random_vs_certified_goldens():
+    cases = load_golden("nlp_random.json")["cases"]
+    N, C = cases[0]["N"], cases[0]["C"]
+    s = solver(N, C, K_obs=cases[0]["K_obs"])
+    obstacles = np.asarray(cases[0]["obstacles"])
+    x0 = np.array([c["x0"] for c in cases]); ref = np.array([c["ref"] for c in cases]); foot = np.array([c["foot"] for c in cases])
+    out = s.solve(x0, ref, foot, obstacles)
+    xr = np.array([c["x"] for c in cases])
+    assert (out["status"] == 0).all()
+    np.testing.assert_array_equal(out["iters"][:, 1], [c["iters"] for c in cases])
+    np.testing.assert_allclose(xus(N, out["x"]), xus(N, xr), atol=NLP_TOL, rtol=0)
+    np.testing.assert_allclose(out["x"], xr, atol=1e-6, rtol=0)
+    np.testing.assert_allclose(out["obj"], [c["obj"] for c in cases], atol=1e-6, rtol=0)
+
+
+# ----------------------------------------------------------------------------- vs oracle
+CONFIGS = [
+    # N, C, K_obs, K_nbr, agents, use_nlp
+    (4, 4, 1, 0, 16, 1),      # reference mode (run_NMPC as written)
+    (4, 2, 1, 0, 16, 1),      # reference mode, trot domain
+    (10, 2, 3, 0, 64, 1),     # BASELINE configs[1]
+    (10, 2, 3, 8, 96, 1),     # configs[2] shape (inter-agent rows), small batch
+    (20, 2, 3, 0, 24, 1),     # horizon 20
+    (10, 4, 3, 0, 16, 1),     # standing, 4 contacts
+    (10, 2, 0, 0, 32, 1),     # no obstacles: velocity rows only
+]
+
+
+@pytest.mark.parametrize("N,C,Ko,Kn,A,nlp", CONFIGS)
+def test_gpu_matches_oracle(N, C, Ko, Kn, A, nlp):
+    b = workload.make_batch(A, N, C, seed=7 * N + C + Kn)
+    out = solver(N, C, Ko, Kn, nlp).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn, use_nlp=nlp), b["x0"], b["ref"], b["foot"],
+                           b["obstacles"], b["nbr_state"], nthreads=8)
+    np.testing.assert_array_equal(out["status"], r["status"])
+    assert np.mean(np.all(out["iters"] == r["iters"], 1)) >= 0.95
+    np.testing.assert_allclose(xus(N, out["x_qp"]), xus(N, r["x_qp"]), atol=QP_TOL, rtol=0)
+    np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+    if C == 2:
+        np.testing.assert_allclose(out["x"], r["x"], atol=NLP_TOL, rtol=0)
+    np.testing.assert_allclose(out["obj"], r["obj"], rtol=1e-7, atol=1e-6)
+
+
+# ----------------------------------------------------------------------------- full-size properties
+def _dynamics_residual(p, x0, x):
+    Ad, Bd = oracle.lip(oracle.params(p.N, p.C))
+    N = p.N
+    X = x[:, :4 * N].reshape(-1, N, 4); U = x[:, 4 * N:6 * N].reshape(-1, N, 2)
+    prev = x0
+    err = 0.0
+    for k in range(N):
+        pred = prev @ Ad.T + U[:, k] @ Bd.T
+        err = max(err, np.abs(pred - X[:, k]).max())
+        prev = X[:, k]
+    return err
+
+
+@pytest.mark.parametrize("A,Kn", [(64, 0), (1024, 8)])
+def test_full_size_properties(A, Kn):
+    """BASELINE configs[1] and configs[2] at full size: size-independent properties."""
+    N, C, Ko = 10, 2, 3
+    b = workload.make_batch(A, N, C, seed=11)
+    s = solver(N, C, Ko, Kn)
+    out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    p = s.params
+    assert (out["status"] == 0).mean() >= 0.99
+    x = out["x"]
+    assert _dynamics_residual(p, b["x0"], x) < 1e-9                          # Aeq x = beq (dynamics)
+    Xs, U, L, sl = srbnmpc.split(p, x)
+    np.testing.assert_allclose(L.sum(-1), 1.0, atol=1e-9)                      # sum lambda = 1
+    np.testing.assert_allclose(U, np.einsum("akdc,akc->akd", b["foot"], L), atol=1e-9)   # u = F lambda
+    assert L.min() > -1e-7 and L.max() < 1 + 1e-7
+    fr = p.mu * p.hcom / np.sqrt(2)
+    com_cop = np.abs(Xs[:, :-1][..., [0, 2]] - U[:, 1:])
+    assert com_cop.max() < fr + 1e-6
+    assert np.abs(Xs[..., [1, 3]]).max() < p.vsat + 1e-6                        # velocity rows
+    # obstacle / inter-agent rows: d^2 + s >= eps
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    rng = np.random.default_rng(0)
+    for a in rng.choice(A, size=min(A, 24), replace=False):
+        obs, eps = oracle.select_obstacles(op, b["x0"][a], b["obstacles"], b["nbr_state"], int(a))
+        d2 = ((Xs[a][:, None, [0, 2]] - obs) ** 2).sum(-1)
+        assert (d2 + sl[a] - eps[None, :]).min() > -1e-6
+        Pd, c, Aeq, beq, G, h = oracle.build_qp(op, b["x0"][a], b["ref"][a], b["foot"][a])
+        gJ, hh = nlp_rows(N, C, Pd.size, G, h, obs, eps, p.vsat)
+        cert = certify(Pd, c, Aeq, beq, gJ, hh, x[a])
+        assert cert["stat"] < 1e-4 and cert["prim"] < 1e-6 and cert["zmin"] >= 0, (a, cert)
+
+
+def test_knn_matches_bruteforce():
+    """Inter-agent neighbour selection == (d^2, index) order of the reference's argmin scan."""
+    N, C, Ko, Kn, A = 10, 2, 0, 8, 512
+    b = workload.make_batch(A, N, C, seed=3)
+    nb = b["nbr_state"].copy()
+    nb[10:20, :2] = nb[5, :2]                     # exact distance ties: lower index first
+    out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], nb)
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], b["obstacles"],
+                           nb, nthreads=8)
+    np.testing.assert_array_equal(out["status"], r["status"])
+    np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+
+
+def test_qp_only_equals_qp_stage():
+    N, C = 10, 2
+    b = workload.make_batch(32, N, C, seed=21)
+    full = solver(N, C, 3, 0, 1).solve(b["x0"], b["ref"], b["foot"], b["obstacles"])
+    qp = solver(N, C, 3, 0, 0).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], qp_only=True)
+    np.testing.assert_array_equal(qp["x"], full["x_qp"])
+    assert (qp["iters"][:, 1] == 0).all()
+
+
+def test_device_api_matches_host():
+    N, C, A = 10, 2, 64
+    b = workload.make_batch(A, N, C, seed=4)
+    s = solver(N, C, 3, 8)
+    host = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    dev = torch.device("cuda:0")
+    t = {k: torch.as_tensor(np.ascontiguousarray(v), dtype=torch.float64, device=dev) for k, v in b.items()}
+    out = dict(x_qp=torch.zeros((A, s.params.nv), dtype=torch.float64, device=dev),
+               x=torch.zeros((A, s.params.nv), dtype=torch.float64, device=dev),
+               obj=torch.zeros(A, dtype=torch.float64, device=dev),
+               status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+               iters=torch.zeros((A, 2), dtype=torch.int32, device=dev))
+    s.solve_device(t["x0"], t["ref"], t["foot"].reshape(A, -1), t["obstacles"], t["nbr_state"], out)
+    s.sync()
+    np.testing.assert_array_equal(out["x"].cpu().numpy(), host["x"])
+    np.testing.assert_array_equal(out["status"].cpu().numpy(), host["status"])
+
+
+def test_edge_cases():
+    N, C = 10, 2
+    s = solver(N, C, 3, 0, 1, max_agents=8)
+    b = workload.make_batch(8, N, C, seed=9)
+    # empty batch is a no-op
+    out = s.solve(b["x0"][:0], b["ref"][:0], b["foot"][:0], b["obstacles"])
+    assert out["x"].shape == (0, s.params.nv)
+    # more agents than the context holds -> error, not a fault
+    with pytest.raises(RuntimeError):
+        s.solve(np.tile(b["x0"], (2, 1)), np.tile(b["ref"], (2, 1)), np.tile(b["foot"], (2, 1, 1, 1)), b["obstacles"])
+    # fewer obstacles than K_obs: missing ones are parked far away (same as the oracle)
+    few = b["obstacles"][:1]
+    out = s.solve(b["x0"], b["ref"], b["foot"], few)
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=3), b["x0"], b["ref"], b["foot"], few)
+    np.testing.assert_array_equal(out["status"], r["status"])
+    np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL)
+    # identical agents give identical answers (no cross-agent interference in the batch)
+    same = s.solve(np.repeat(b["x0"][:1], 8, 0), np.repeat(b["ref"][:1], 8, 0), np.repeat(b["foot"][:1], 8, 0),
+                   b["obstacles"])
+    assert (same["x"] == same["x"][0]).all()
+
+
+def test_mpcdist_surface_on_reference_instance(kat2):
+    """MPC_dist call sequence (src/A1_Sim.cpp:180-197) through MPCDist on the logged instance."""
+    m = srbnmpc.MPCDist()
+    m.setAgentID(0)
+    m.setPstart(np.zeros(8))
+    obst = np.asarray(kat2["obstacle"])
+    m.setPobs_real(np.c_[obst, [50.0, 50.0]])
+    ref = np.asarray(kat2["ref"]).reshape(4, 4)          # grid-major (x, xdot, y, ydot)
+    Pr = np.zeros((8, 8)); Prd = np.zeros((8, 8))
+    Pr[0, :4] = ref[:, 0]; Prd[0, :4] = ref[:, 1]; Pr[1, :4] = ref[:, 2]; Prd[1, :4] = ref[:, 3]
+    m.setReferenceTrajectory(Pr, Prd)
+    q = np.zeros(18); dq = np.zeros(18)
+    x0 = kat2["x0"]
+    q[0], dq[0], q[1], dq[1] = x0[0], x0[1], x0[2], x0[3]
+    m.updateState(q, dq, [1, 1, 1, 1], np.zeros((3, 4)), np.zeros(4))
+    m.use_snopt = True
+    m.run_NMPC()
+    np.testing.assert_allclose(m.get_MPCsol().ravel(), np.asarray(kat2["x_nlp"])[:16], atol=1e-6)
+    np.testing.assert_allclose(m.qp_solution_eventbased_[:24], kat2["logged_qp_x"], atol=2e-9)
+    alpha = m.get_alphaCOM()
+    np.testing.assert_allclose(alpha, oracle.fit_bezier([0, 0, 0, 0], np.asarray(kat2["x_nlp"])[:16].reshape(4, 4)),
+                               atol=1e-6)
+    assert m.gaitDomain_ == 1

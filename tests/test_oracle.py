@@ -1,0 +1,164 @@
+"""CPU tests: pin the oracle (CPU restatement) against the reference's own outputs and
+test data, and against the genuine vendored iSWIFT when oracle/_ref was built here.
+
+Anchors
+  KAT-1  optimization/iSWIFT/include/Matrices_small.h -- iSWIFT's own test QP
+  KAT-2  print_file.out -- the reference's logged run_NMPC instance: its QP-stage output
+         (SNOPT start point = iswiftQp_e solution, MPC_dist.cpp:348-361) printed to 9 digits
+"""
+import numpy as np
+import pytest
+from conftest import load_golden
+
+import oracle
+from kkt import certify, nlp_rows
+
+
+def _kat1_dense(d):
+    n, m, p = d["n"], d["m"], d["p"]
+    P = oracle.ccs_to_dense(n, n, d["Pjc"], d["Pir"], d["Ppr"])
+    A = oracle.ccs_to_dense(p, n, d["Ajc"], d["Air"], d["Apr"])
+    G = oracle.ccs_to_dense(m, n, d["Gjc"], d["Gir"], d["Gpr"])
+    return P, np.asarray(d["c"]), A, np.asarray(d["b"]), G, np.asarray(d["h"])
+
+
+def test_kat1_golden_is_iswift_optimal():
+    d = load_golden("kat1.json")
+    assert d["flag"] == 0 and d["iters"] == 7          # flag 0 in 7 iterations
+
+
+def test_kat1_oracle_matches_iswift():
+    d = load_golden("kat1.json")
+    P, c, A, b, G, h = _kat1_dense(d)
+    x, flag, it = oracle.qp_solve_full(P, c, A, b, G, h)
+    assert flag == 0
+    assert it == d["iters"]
+    np.testing.assert_allclose(x, d["x_iswift"], atol=1e-8, rtol=0)
+
+
+@pytest.mark.skipif(not oracle.ref_available(), reason="oracle/_ref (genuine iSWIFT) not built here")
+def test_kat1_reference_build_reproduces_golden():
+    d = load_golden("kat1.json")
+    x, flag, it = oracle.iswift_ref_ccs(d["n"], d["m"], d["p"], d["Pjc"], d["Pir"], d["Ppr"], d["Ajc"], d["Air"],
+                                        d["Apr"], d["Gjc"], d["Gir"], d["Gpr"], d["c"], d["h"], d["b"], d["P"])
+    assert (flag, it) == (d["flag"], d["iters"])
+    np.testing.assert_array_equal(x, d["x_iswift"])
+
+
+def test_kat2_builder_reproduces_logged_reference_qp(kat2):
+    """Assembly (MPC_dist.cpp:135-321) + iSWIFT algorithm reproduce the reference's own
+    logged QP output (print_file.out derivative-check x, 9 significant digits)."""
+    p = oracle.params(4, 4)
+    foot = np.repeat(kat2["F"][None], 4, 0)
+    Pd, c, A, b, G, h = oracle.build_qp(p, kat2["x0"], kat2["ref"], foot)
+    x, flag, it, _ = oracle.qp_solve(Pd, c, A, b, G, h)
+    assert flag == 0
+    assert it == kat2["iters_qp_qd"] == 8
+    np.testing.assert_allclose(x[:24], kat2["logged_qp_x"], atol=2e-9, rtol=0)
+    assert abs(x[40] - kat2["logged_qp_s"]) < 1e-12
+    # equal to the genuine iSWIFT (quasi-definite order) to round-off on X, U, s
+    np.testing.assert_allclose(x[:24], np.asarray(kat2["x_qp_iswift_qd"])[:24], atol=1e-10, rtol=0)
+
+
+def test_kat2_objective_gradient_matches_log(kat2):
+    """The logged objective gradient Q_qp x + f at the start point (print_file.out) is
+    reproduced by our cost (Q = 300/2000 on X, 0.1 on U)."""
+    p = oracle.params(4, 4)
+    foot = np.repeat(kat2["F"][None], 4, 0)
+    Pd, c, *_ = oracle.build_qp(p, kat2["x0"], kat2["ref"], foot)
+    xs = np.asarray(kat2["logged_qp_x"])
+    g = Pd[:24] * xs + c[:24]
+    np.testing.assert_allclose(g, kat2["logged_qp_grad"], rtol=2e-8, atol=2e-9)
+
+
+def test_qp_random_oracle_vs_genuine_iswift():
+    cases = load_golden("qp_random.json")["cases"]
+    for cs in cases:
+        N, C = cs["N"], cs["C"]
+        p = oracle.params(N, C)
+        Pd, c, A, b, G, h = oracle.build_qp(p, cs["x0"], cs["ref"], np.asarray(cs["foot"]))
+        x, flag, it, _ = oracle.qp_solve(Pd, c, A, b, G, h)
+        xr = np.asarray(cs["x"])
+        assert flag == cs["flag"] == 0
+        assert it == cs["iters"], (N, C)
+        sel = np.r_[np.arange(6 * N), [Pd.size - 1]]      # X, U, s (lambda non-unique for C = 4)
+        np.testing.assert_allclose(x[sel], xr[sel], atol=1e-7, rtol=0)
+        if C == 2:
+            np.testing.assert_allclose(x, xr, atol=1e-7, rtol=0)
+        # min-degree order (what Eigen AMD does): regularised pivots perturb the steps,
+        # but the answer stays inside iSWIFT's own 1e-6 tolerance
+        np.testing.assert_allclose(x[sel], np.asarray(cs["x_md"])[sel], atol=1e-6, rtol=0)
+
+
+def test_nlp_random_oracle_kkt_certified():
+    cases = load_golden("nlp_random.json")["cases"]
+    for cs in cases:
+        N, C = cs["N"], cs["C"]
+        p = oracle.params(N, C, K_obs=cs["K_obs"])
+        foot = np.asarray(cs["foot"])
+        Pd, c, A, b, G, h = oracle.build_qp(p, cs["x0"], cs["ref"], foot)
+        obs, eps = oracle.select_obstacles(p, cs["x0"], np.asarray(cs["obstacles"]))
+        np.testing.assert_array_equal(obs, cs["obs"])
+        x, flag, it = oracle.nlp_solve(p, cs["x0"], foot, Pd, c, A, b, G, h, obs, eps, np.asarray(cs["x_qp"]))
+        assert flag == 0 and it == cs["iters"]
+        np.testing.assert_allclose(x, cs["x"], atol=1e-9, rtol=0)
+        gJ, hh = nlp_rows(N, C, Pd.size, G, h, obs, eps, p.vsat)
+        cert = certify(Pd, c, A, b, gJ, hh, x)
+        assert cert["stat"] < 1e-5 and cert["prim"] < 1e-8 and cert["eq"] < 1e-10 and cert["zmin"] >= 0
+        obj = 0.5 * Pd @ (x * x) + c @ x
+        assert obj <= cs["slsqp_obj"] + 1e-3      # at least as good as SciPy SLSQP from the same start
+
+
+def test_kat2_nlp_certified_and_beats_logged_snopt(kat2):
+    p = oracle.params(4, 4)
+    foot = np.repeat(kat2["F"][None], 4, 0)
+    Pd, c, A, b, G, h = oracle.build_qp(p, kat2["x0"], kat2["ref"], foot)
+    obs = np.tile(kat2["obstacle"], (4, 1, 1)); eps = np.array([p.eps_obs])
+    x, flag, it = oracle.nlp_solve(p, kat2["x0"], foot, Pd, c, A, b, G, h, obs, eps, kat2["x_qp_iswift_qd"])
+    assert flag == 0
+    np.testing.assert_allclose(x, kat2["x_nlp"], atol=1e-9)
+    gJ, hh = nlp_rows(4, 4, Pd.size, G, h, obs, eps, p.vsat)
+    cert = certify(Pd, c, A, b, gJ, hh, x)
+    assert cert["stat"] < 1e-6 and cert["prim"] < 1e-9
+    # SNOPT's logged point (INFO 3, not converged) violates an obstacle row by ~3e-4
+    g_snopt, _ = gJ(np.asarray(kat2["snopt_final_x"]))
+    assert (g_snopt - hh).max() > 1e-4
+    assert abs((0.5 * Pd @ (x * x) + c @ x) - kat2["slsqp_obj"]) < 1e-4
+
+
+def test_select_obstacles_matches_bruteforce():
+    rng = np.random.default_rng(3)
+    p = oracle.params(10, 2, K_obs=3, K_nbr=4)
+    obstacles = rng.uniform(0, 9, (20, 2))
+    nbr = np.c_[rng.uniform(0, 9, (30, 2)), rng.uniform(-.3, .3, (30, 2))]
+    for self_idx in (0, 7, 29):
+        x0 = np.array([nbr[self_idx, 0], nbr[self_idx, 2], nbr[self_idx, 1], nbr[self_idx, 3]])
+        obs, eps = oracle.select_obstacles(p, x0, obstacles, nbr, self_idx)
+        d = np.hypot(*(obstacles - x0[[0, 2]]).T)
+        np.testing.assert_array_equal(obs[0, :3], obstacles[np.argsort(d, kind="stable")[:3]])
+        dn = np.hypot(*(nbr[:, :2] - x0[[0, 2]]).T); dn[self_idx] = np.inf
+        nn = np.argsort(dn, kind="stable")[:4]
+        for k in range(10):
+            np.testing.assert_allclose(obs[k, 3:], nbr[nn, :2] + nbr[nn, 2:] * p.Ts * (k + 1), rtol=0, atol=1e-15)
+        assert np.all(eps[:3] == p.eps_obs) and np.all(eps[3:] == p.eps_nbr)
+
+
+def test_oracle_batch_threads_deterministic():
+    from srbnmpc import workload
+    b = workload.make_batch(12, 10, 2, seed=5)
+    p = oracle.params(10, 2, K_obs=3)
+    r1 = oracle.solve_batch(p, b["x0"], b["ref"], b["foot"], b["obstacles"], nthreads=1)
+    r4 = oracle.solve_batch(p, b["x0"], b["ref"], b["foot"], b["obstacles"], nthreads=4)
+    for k in r1:
+        np.testing.assert_array_equal(r1[k], r4[k])
+    assert (r1["status"] == 0).all()
+
+
+def test_bezier_fit_interpolates():
+    rng = np.random.default_rng(1)
+    buf = rng.normal(size=4); X = rng.normal(size=(4, 4))
+    alpha = oracle.fit_bezier(buf, X)
+    from math import comb
+    for i, s in enumerate([0, .25, .5, .75, 1.0]):
+        val = sum(comb(4, j) * s ** j * (1 - s) ** (4 - j) * alpha[:, j] for j in range(5))
+        np.testing.assert_allclose(val, buf if i == 0 else X[i - 1], atol=1e-12)
