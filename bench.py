@@ -116,7 +116,10 @@ def main():
                status=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
                iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev))
     solver = srbnmpc.BatchSolver(p, n_loc, local_rank)
-    stream = torch.cuda.current_stream(dev)
+    # one explicit stream for the collective, both kernels and the timing events (the C ABI
+    # launches on the stream it is handed; the null stream would not order against it)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
     exchange = cfg["K_nbr"] > 0 and world > 1
 
     def step():

@@ -5,10 +5,18 @@
 #include <pthread.h>
 #include "oracle.h"
 
-int orc_solve_agent(const orc_params *p, const double x0[4], const double *ref, const double *foot,
+int orc_solve_agent(const orc_params *p_in, const double x0[4], const double *ref, const double *foot,
                     const double *obstacles, int n_obs, const double *nbr_state, int n_all, int self_idx,
                     double *x_qp, double *x_out, double *obj, int status[2], int iters[2])
 {
+    /* "up to K nearest": clamp to what exists, as the product's C ABI does */
+    orc_params pc = *p_in;
+    const orc_params *p = &pc;
+    if (pc.K_obs > n_obs) pc.K_obs = n_obs > 0 ? n_obs : 0;
+    {
+        int others = nbr_state ? n_all - 1 : 0;
+        if (pc.K_nbr > others) pc.K_nbr = others > 0 ? others : 0;
+    }
     const int nv = orc_nv(p), neq = orc_neq(p), mq = orc_mqp(p), K = p->K_obs + p->K_nbr;
     double *Pd = malloc(sizeof(double) * nv), *c = malloc(sizeof(double) * nv);
     double *A = malloc(sizeof(double) * (size_t)neq * nv), *b = malloc(sizeof(double) * neq);

@@ -78,19 +78,36 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
     orc_lip(pp, Ad, Bd);
     memset(Z, 0, sizeof(double) * (size_t)n * nz);
     for (int j = 0; j < N; j++)
-        for (int i = 0; i < C - 1; i++) {
-            int col = j * (C - 1) + i;
-            double gg[2], v[4], t[4];
-            for (int d = 0; d < 2; d++) gg[d] = foot[(j * 2 + d) * C + i] - foot[(j * 2 + d) * C + C - 1];
-            Z[(size_t)(6 * N + C * j + i) * nz + col] = 1.0;
-            Z[(size_t)(6 * N + C * j + C - 1) * nz + col] = -1.0;
+        for (int t = 0; t < C - 1; t++) {
+            int col = j * (C - 1) + t;
+            double lam[4] = {0, 0, 0, 0}, gg[2] = {0, 0}, v[4], tt[4];
+            int is_null = 0;
+            const double *F = foot + (size_t)j * 2 * C;
+            if (C != 4) { lam[t] = 1.0; lam[C - 1] = -1.0; }
+            else {  /* exact null vector of [F; 1'] replaces one column (see the GPU kernel) */
+                double nv4[4];
+                for (int i = 0; i < 4; i++) {
+                    int ci[3], q = 0;
+                    for (int k = 0; k < 4; k++) if (k != i) ci[q++] = k;
+                    double det = F[ci[0]] * (F[4 + ci[1]] - F[4 + ci[2]]) - F[ci[1]] * (F[4 + ci[0]] - F[4 + ci[2]]) +
+                                 F[ci[2]] * (F[4 + ci[0]] - F[4 + ci[1]]);
+                    nv4[i] = (i & 1) ? -det : det;
+                }
+                int is = 0;
+                for (int i = 1; i < 3; i++) if (fabs(nv4[i]) > fabs(nv4[is])) is = i;
+                if (t == 2) { for (int i = 0; i < 4; i++) lam[i] = nv4[i] / nv4[is]; is_null = 1; }
+                else { int i = (t < is) ? t : t + 1; lam[i] = 1.0; lam[3] = -1.0; }
+            }
+            if (!is_null)
+                for (int i = 0; i < C; i++) { gg[0] += F[i] * lam[i]; gg[1] += F[C + i] * lam[i]; }
+            for (int i = 0; i < C; i++) Z[(size_t)(6 * N + C * j + i) * nz + col] = lam[i];
             Z[(size_t)(4 * N + 2 * j) * nz + col] = gg[0];
             Z[(size_t)(4 * N + 2 * j + 1) * nz + col] = gg[1];
             for (int d = 0; d < 4; d++) v[d] = Bd[d * 2] * gg[0] + Bd[d * 2 + 1] * gg[1];
             for (int k = j; k < N; k++) {
                 for (int d = 0; d < 4; d++) Z[(size_t)(4 * k + d) * nz + col] = v[d];
-                for (int d = 0; d < 4; d++) t[d] = Ad[d * 4] * v[0] + Ad[d * 4 + 1] * v[1] + Ad[d * 4 + 2] * v[2] + Ad[d * 4 + 3] * v[3];
-                memcpy(v, t, sizeof v);
+                for (int d = 0; d < 4; d++) tt[d] = Ad[d * 4] * v[0] + Ad[d * 4 + 1] * v[1] + Ad[d * 4 + 2] * v[2] + Ad[d * 4 + 3] * v[3];
+                memcpy(v, tt, sizeof v);
             }
         }
     Z[(size_t)(n - 1) * nz + nz - 1] = 1.0;
@@ -130,6 +147,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     double *dsv = malloc(sizeof(double) * m), *dz = malloc(sizeof(double) * m), *r3 = malloc(sizeof(double) * m);
     double *K = malloc(sizeof(double) * dim * dim), *Hl = malloc(sizeof(double) * n * n);
     double *rhs = malloc(sizeof(double) * dim), *dx = malloc(sizeof(double) * n), *dq = malloc(sizeof(double) * n);
+    double *hdiag = malloc(sizeof(double) * n);
     double *Z = malloc(sizeof(double) * (size_t)n * nz), *Hr = malloc(sizeof(double) * nz * nz), *HZ = malloc(sizeof(double) * (size_t)n * nz);
     int *piv = malloc(sizeof(int) * dim);
     int flag = 2, it = 0;
@@ -166,16 +184,21 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         double nrx = sqrt(dotv(rx, rx, n)), nrz = sqrt(dotv(rz, rz, m)), nry = sqrt(dotv(ry, ry, p));
         double sz = dotv(s, z, m);
         if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
-        if (nrx < th && nrz < th && nry < th && sz / m < tol) { flag = 0; break; }
+        /* dual residual scaled by the objective gradient (the NLP's own criterion; the
+         * QP stage keeps iSWIFT's absolute test): max(1, ||Q x + f||_inf) */
+        double gmax = 1.0;
+        for (int j = 0; j < n; j++) { double gj = fabs(Pd[j] * x[j] + c[j]); if (gj > gmax) gmax = gj; }
+        if (nrx < th * gmax && nrz < th && nry < th && sz / m < tol) { flag = 0; break; }
         for (int r = 0; r < m; r++) { lam[r] = sqrt(s[r] * z[r]); wgt[r] = s[r] / z[r]; }
         double mu = dotv(lam, lam, m) / m;
 
-        /* Hl + J'W^-1 J (full space) */
+        /* Hl + J'W^-1 J (full space); hdiag = Lagrangian-Hessian terms beyond Q_qp */
         memset(Hl, 0, sizeof(double) * n * n);
-        for (int j = 0; j < n; j++) Hl[j * n + j] = Pd[j];
+        for (int j = 0; j < n; j++) { Hl[j * n + j] = Pd[j]; hdiag[j] = 0.0; }
         for (int k = 0; k < P.N; k++) {
             double zs = 0;
             for (int j = 0; j < P.K; j++) zs += z[P.mq + k * P.K + j];
+            hdiag[4 * k] = -2 * zs; hdiag[4 * k + 2] = -2 * zs;
             Hl[(4 * k) * n + 4 * k] -= 2 * zs; Hl[(4 * k + 2) * n + 4 * k + 2] -= 2 * zs;
         }
         for (int r = 0; r < m; r++) {
@@ -186,7 +209,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             }
         }
         /* inertia correction: reduced Hessian Z'(H + delta I)Z must be PD */
-        double delta = 0.0; int ok = 0;
+        double delta = 0.0, dstart = 0.0; int ok = 0;
         for (int tries = 0; tries < 14; tries++) {
             for (int i = 0; i < n; i++)
                 for (int a = 0; a < nz; a++) {
@@ -200,8 +223,13 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
                     for (int i = 0; i < n; i++) sacc += Z[(size_t)i * nz + a] * HZ[(size_t)i * nz + bb];
                     Hr[a * nz + bb] = sacc;
                 }
+            if (tries == 0) {   /* scale-aware first shift: 1e-10 * max(1, max diag of Z'HZ) */
+                dstart = 1.0;
+                for (int a = 0; a < nz; a++) if (Hr[a * nz + a] > dstart) dstart = Hr[a * nz + a];
+                dstart *= 1e-10;
+            }
             if (orc_chol(nz, Hr) == 0) { ok = 1; break; }
-            delta = (delta == 0.0) ? 1e-4 : delta * 10.0;
+            delta = (delta == 0.0) ? dstart : delta * 10.0;
         }
         if (!ok) { flag = 1; break; }
         /* full-space KKT [H + delta I, A'; A, 0] */
@@ -231,8 +259,15 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
                 double sigma = mr * mr * mr; if (sigma < 0) sigma = 0;
                 for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) - dsv[r] * dz[r] + sigma * mu;
             } else {
-                for (int j = 0; j < n; j++) dq[j] = 0;
-                for (int k = 0; k < p; k++) for (int j = 0; j < n; j++) dq[j] += A[(size_t)k * n + j] * rhs[n + k];  /* A' dy */
+                /* A'dy from the first block row of the Newton system,
+                 *   A'dy = rx - (Q_qp + hess + delta I) dx - J'dz,
+                 * rather than from the LU's dy: identical in exact arithmetic, but near
+                 * convergence the full-space KKT has condition ~1e12 (active rows carry
+                 * z/s ~ 1e10) and the LU's dy is only good to ~1e-4 relative, which would
+                 * stall ||rx|| above the 1e-6 exit threshold. */
+                for (int j = 0; j < n; j++) dq[j] = rx[j] - (Pd[j] + hdiag[j] + delta) * dx[j];
+                for (int r = 0; r < m; r++)
+                    for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) dq[Ji[4 * r + t]] -= Jv[4 * r + t] * dz[r];
             }
         }
         double ap = steplen(s, dsv, m), ad = steplen(z, dz, m);
@@ -246,6 +281,6 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     if (iters_out) *iters_out = it;
     free(P.gnz); free(P.gval); free(hh); free(x); free(q); free(s); free(z); free(g); free(Jv); free(Ji);
     free(rx); free(ry); free(rz); free(lam); free(wgt); free(ds); free(dsv); free(dz); free(r3); free(K); free(Hl);
-    free(rhs); free(dx); free(dq); free(Z); free(Hr); free(HZ); free(piv);
+    free(rhs); free(dx); free(dq); free(hdiag); free(Z); free(Hr); free(HZ); free(piv);
     return flag;
 }

@@ -7,9 +7,11 @@
  *
  * Only the linear algebra differs: iSWIFT factors the sparse unreduced KKT
  *     [P A' G'; A 0 0; G 0 -W]
- * with a regularised up-looking LDL' (ldl.c:254-326); here the same system is solved
- * densely by eliminating dz (W diagonal), then a Schur complement on dy with two
- * Cholesky factorisations.  In exact arithmetic both give the same Newton step.
+ * with a regularised up-looking LDL' (ldl.c:254-326); here dz is eliminated (W is
+ * diagonal) and the full-space [P + G'W^-1 G, A'; A, 0] is factored densely by LU with
+ * partial pivoting.  In exact arithmetic both give the same Newton step.  (A Schur
+ * complement on dy is NOT used: with interior contact weights the lambda block of
+ * P + G'W^-1 G is O(mu) and A H^-1 A' loses definiteness to round-off near convergence.)
  */
 #include <math.h>
 #include <stdlib.h>
@@ -21,8 +23,7 @@ typedef struct {
     const double *Pd, *Pf, *A, *G;   /* P diagonal (Pd) or full row-major (Pf, when non-NULL) */
     int *gnz;      /* [m][4] column indices of row r's nonzeros (-1 padded) */
     double *gval;  /* [m][4] */
-    double *H, *S, *HiAt, *t1, *t2;
-    int use_lu;          /* general (possibly indefinite) P: LU on [H A'; A 0] instead of Schur */
+    double *H, *t1, *t2;
     double *K; int *piv;
 } kktws;
 
@@ -38,18 +39,15 @@ static void ws_init(kktws *w, int n, int m, int p, const double *Pd, const doubl
             if (G[(size_t)r * n + j] != 0.0) { w->gnz[4 * r + k] = j; w->gval[4 * r + k] = G[(size_t)r * n + j]; k++; }
     }
     w->H = (double *)malloc(sizeof(double) * n * n);
-    w->S = (double *)malloc(sizeof(double) * (p ? p * p : 1));
-    w->HiAt = (double *)malloc(sizeof(double) * (size_t)n * (p ? p : 1));
     w->t1 = (double *)malloc(sizeof(double) * (n + p + m + 8));
     w->t2 = (double *)malloc(sizeof(double) * (n + p + m + 8));
-    w->use_lu = 0;
     w->K = (double *)malloc(sizeof(double) * (size_t)(n + p) * (n + p));
     w->piv = (int *)malloc(sizeof(int) * (n + p));
 }
 
 static void ws_free(kktws *w)
 {
-    free(w->gnz); free(w->gval); free(w->H); free(w->S); free(w->HiAt); free(w->t1); free(w->t2);
+    free(w->gnz); free(w->gval); free(w->H); free(w->t1); free(w->t2);
     free(w->K); free(w->piv);
 }
 
@@ -86,7 +84,7 @@ static int kkt_factor(kktws *w, const double *wgt)
             }
         }
     }
-    if (w->use_lu) {
+    {
         const int d = n + p;
         memset(w->K, 0, sizeof(double) * (size_t)d * d);
         for (int i = 0; i < n; i++) for (int j = 0; j < n; j++) w->K[(size_t)i * d + j] = H[i * n + j];
@@ -97,21 +95,6 @@ static int kkt_factor(kktws *w, const double *wgt)
             }
         return orc_lu(d, w->K, w->piv);
     }
-    if (orc_chol(n, H)) return -1;
-    for (int j = 0; j < p; j++) {
-        double *col = w->t1;
-        for (int i = 0; i < n; i++) col[i] = w->A[(size_t)j * n + i];
-        orc_chol_solve(n, H, col);
-        for (int i = 0; i < n; i++) w->HiAt[(size_t)i * p + j] = col[i];
-    }
-    for (int i = 0; i < p; i++)
-        for (int j = 0; j < p; j++) {
-            double s = 0;
-            for (int k = 0; k < n; k++) s += w->A[(size_t)i * n + k] * w->HiAt[(size_t)k * p + j];
-            w->S[i * p + j] = s;
-        }
-    if (p && orc_chol(p, w->S)) return -1;
-    return 0;
 }
 
 /* solve [P A' G'; A 0 0; G 0 -W][dx;dy;dz] = [r1;r2;r3] with the current factor */
@@ -123,30 +106,11 @@ static void kkt_solve(kktws *w, const double *wgt, const double *r1, const doubl
     for (int i = 0; i < n; i++) g[i] = r1[i];
     for (int r = 0; r < m; r++) t[r] = r3[r] / wgt[r];
     gtmul_add(w, t, g);                                   /* g = r1 + G' W^-1 r3 */
-    if (w->use_lu) {
-        for (int i = 0; i < n; i++) t[i] = g[i];
-        for (int k = 0; k < p; k++) t[n + k] = r2[k];
-        orc_lu_solve(n + p, w->K, w->piv, t);
-        for (int i = 0; i < n; i++) dx[i] = t[i];
-        for (int k = 0; k < p; k++) dy[k] = t[n + k];
-        gmul(w, dx, dz);
-        for (int r = 0; r < m; r++) dz[r] = (dz[r] - r3[r]) / wgt[r];
-        return;
-    }
     for (int i = 0; i < n; i++) t[i] = g[i];
-    orc_chol_solve(n, w->H, t);                           /* t = H^-1 g */
-    for (int i = 0; i < p; i++) {
-        double s = 0;
-        for (int k = 0; k < n; k++) s += w->A[(size_t)i * n + k] * t[k];
-        dy[i] = s - r2[i];
-    }
-    if (p) orc_chol_solve(p, w->S, dy);                   /* dy = S^-1 (A H^-1 g - r2) */
-    for (int i = 0; i < n; i++) {
-        double s = g[i];
-        for (int j = 0; j < p; j++) s -= w->A[(size_t)j * n + i] * dy[j];
-        dx[i] = s;
-    }
-    orc_chol_solve(n, w->H, dx);                          /* dx = H^-1 (g - A' dy) */
+    for (int k = 0; k < p; k++) t[n + k] = r2[k];
+    orc_lu_solve(n + p, w->K, w->piv, t);
+    for (int i = 0; i < n; i++) dx[i] = t[i];
+    for (int k = 0; k < p; k++) dy[k] = t[n + k];
     gmul(w, dx, dz);
     for (int r = 0; r < m; r++) dz[r] = (dz[r] - r3[r]) / wgt[r];
 }
@@ -170,7 +134,6 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
     kktws w;
     ws_init(&w, n, m, p, Pd, A, G);
     w.Pf = Pf;
-    w.use_lu = (Pf != NULL);
     double *x = calloc(n, sizeof(double)), *y = calloc(p + 1, sizeof(double));
     double *s = calloc(m, sizeof(double)), *z = calloc(m, sizeof(double));
     double *rx = calloc(n, sizeof(double)), *ry = calloc(p + 1, sizeof(double)), *rz = calloc(m, sizeof(double));

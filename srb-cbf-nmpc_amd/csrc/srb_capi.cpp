@@ -16,8 +16,8 @@ extern "C" __global__ void srb_nmpc_kernel(SrbKParams prm, int n_agents, const d
                                            const double *footg, const double *obstacles, int n_obs,
                                            const double *nbr_state, const int *nbr_idx, double *x_qp_out,
                                            double *x_out, double *obj_out, int *status_out, int *iters_out);
-extern "C" __global__ void srb_knn_kernel(int n_agents, int agent_offset, const double *state, int n_all, int K,
-                                          int *nbr_idx);
+extern "C" __global__ void srb_knn_kernel(int n_agents, int agent_offset, const double *x0g, const double *state,
+                                          int n_all, int K, int *nbr_idx);
 
 static thread_local std::string g_err;
 
@@ -172,19 +172,22 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
         return fail(SRB_ERR_ARG, "missing buffer");
     if (use_nlp && p->K_obs > 0 && (d->n_obs < 0 || (d->n_obs > 0 && !d->obstacles)))
         return fail(SRB_ERR_ARG, "obstacles missing");
-    if (use_nlp && p->K_nbr > 0 && (!d->nbr_state || d->n_all <= 0 || d->agent_offset < 0 ||
-                                    d->agent_offset + n_agents > d->n_all))
-        return fail(SRB_ERR_ARG, "neighbour states missing or agent_offset out of range");
+    if (use_nlp && p->K_nbr > 0 && d->nbr_state && (d->agent_offset < 0 || d->agent_offset + n_agents > d->n_all))
+        return fail(SRB_ERR_ARG, "agent_offset out of range of the neighbour table");
     SrbKParams k = make_kparams(p, use_nlp);
+    // "up to K nearest": clamp to what exists (batch-uniform), so no row is ever a dummy
+    if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
+    const int others = d->nbr_state ? d->n_all - 1 : 0;
+    if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
     const size_t lds = (size_t)srb_lds_doubles(k) * sizeof(double);
     HIPCHK(hipSetDevice(c->device));
     const int *nbr_idx = nullptr;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
-    if (use_nlp && p->K_nbr > 0) {
+    if (use_nlp && k.K_nbr > 0) {
         dim3 blk(256), grd((n_agents + 255) / 256);
-        hipLaunchKernelGGL(srb_knn_kernel, grd, blk, 0, s, n_agents, d->agent_offset, d->nbr_state, d->n_all,
-                           p->K_nbr, c->nbr_idx);
+        hipLaunchKernelGGL(srb_knn_kernel, grd, blk, 0, s, n_agents, d->agent_offset, d->x0, d->nbr_state, d->n_all,
+                           k.K_nbr, c->nbr_idx);
         HIPCHK(hipGetLastError());
         nbr_idx = c->nbr_idx;
     }

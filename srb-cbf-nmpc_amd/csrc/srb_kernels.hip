@@ -264,11 +264,16 @@ __device__ void build_H(const Ctx &c, double delta)
 }
 
 // In-place Cholesky of L (nz x nz, lower). Returns 0 on success (uniform).
-__device__ int chol_lds(const Ctx &c, double *L, int nz)
+// regularise != 0 mirrors iSWIFT's dynamic pivot regularisation (ldl.c:320-321:
+// |D_kk| <= 1e-14 -> 1e-7) for the QP stage, where the reduced Hessian is PD in exact
+// arithmetic but can lose a pivot to round-off along a lambda direction whose bound
+// rows have gone inactive (4 contacts: u = F lambda leaves one lambda direction free).
+__device__ int chol_lds(const Ctx &c, double *L, int nz, int regularise = 0)
 {
     for (int k = 0; k < nz; k++) {
         __syncthreads();
         double d = L[k * nz + k];
+        if (regularise && d <= 1e-14 && d == d) d = 1e-7;
         if (!(d > 0.0)) return -1;
         d = sqrt(d);
         __syncthreads();
@@ -385,7 +390,14 @@ __device__ int ipm(Ctx &c, int maxit, int *iters)
         for (int r = c.tid; r < c.m; r += WAVE) { nrz += c.rz[r] * c.rz[r]; sz += c.s[r] * c.z[r]; }
         nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz);
         if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
-        if (nrx < th && nrz < th && sz / c.m < tol) { flag = 0; break; }
+        // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
+        double thx = th;
+        if (c.nl) {
+            double gm = 1.0;
+            for (int v = c.tid; v < c.n; v += WAVE) gm = fmax(gm, fabs(Pdiag(c, v) * c.x[v] + cvec(c, v)));
+            thx = th * -wmin(-gm);
+        }
+        if (nrx < thx && nrz < th && sz / c.m < tol) { flag = 0; break; }
         double mu = 0;
         for (int r = c.tid; r < c.m; r += WAVE) { double l = sqrt(c.s[r] * c.z[r]); mu += l * l; }
         mu = wsum(mu) / c.m;
@@ -395,13 +407,19 @@ __device__ int ipm(Ctx &c, int maxit, int *iters)
             for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0 / (c.s[r] / c.z[r]);
             __syncthreads();
             delta = 0.0;
+            double dstart = 0.0;
             int ok = 0;
             for (int tries = 0; tries < (c.nl ? 14 : 1); tries++) {
                 build_H(c, delta);
+                if (tries == 0) {       // scale-aware first shift: 1e-10 * max(1, max diag of Z'HZ)
+                    double dm = 1.0;
+                    for (int a = c.tid; a < c.nz; a += WAVE) dm = fmax(dm, c.Hc[a * c.nz + a]);
+                    dstart = 1e-10 * -wmin(-dm);
+                }
                 for (int i = c.tid; i < c.nz * c.nz; i += WAVE) c.L[i] = c.Hc[i];
                 __syncthreads();
-                if (chol_lds(c, c.L, c.nz) == 0) { ok = 1; break; }
-                delta = (delta == 0.0) ? 1e-4 : delta * 10.0;
+                if (chol_lds(c, c.L, c.nz, !c.nl) == 0) { ok = 1; break; }
+                delta = (delta == 0.0) ? dstart : delta * 10.0;
             }
             if (!ok) { flag = 1; break; }
             // predictor: ds = -lambda.*lambda
@@ -457,6 +475,35 @@ __device__ int ipm(Ctx &c, int maxit, int *iters)
     }
     *iters = it;
     return flag;
+}
+
+// Basis of the per-grid contact-weight directions {d : 1'd = 0} (lambda = e_{C-1} + N xi).
+// Columns e_i - e_{C-1}, except for C = 4, where one column is replaced by the exact null
+// vector n of [F; 1'] (u = F lambda unchanged): its U and X parts are identically zero, so
+// the vanishing curvature along it near convergence (both lambda bounds inactive) is held
+// exactly in Z'HZ instead of emerging from cancellation between O(1e3) terms.
+// Returns 1 when column t is that null column (lam holds it), 0 otherwise.
+__device__ __forceinline__ int lambda_basis(const double *F, int C, int t, double lam[4])
+{
+    for (int i = 0; i < 4; i++) lam[i] = 0.0;
+    if (C != 4) { lam[t] = 1.0; lam[C - 1] = -1.0; return 0; }
+    // n_i = (-1)^i det of [F; 1'] with column i removed
+    double nvec[4];
+    for (int i = 0; i < 4; i++) {
+        int cidx[3], q = 0;
+        for (int k = 0; k < 4; k++) if (k != i) cidx[q++] = k;
+        const double *r0 = F, *r1 = F + 4;
+        double det = r0[cidx[0]] * (r1[cidx[1]] - r1[cidx[2]]) - r0[cidx[1]] * (r1[cidx[0]] - r1[cidx[2]]) +
+                     r0[cidx[2]] * (r1[cidx[0]] - r1[cidx[1]]);
+        nvec[i] = (i & 1) ? -det : det;
+    }
+    int istar = 0;
+    for (int i = 1; i < 3; i++) if (fabs(nvec[i]) > fabs(nvec[istar])) istar = i;
+    double sc = 1.0 / nvec[istar];
+    if (t == 2) { for (int i = 0; i < 4; i++) lam[i] = nvec[i] * sc; return 1; }
+    int i = (t < istar) ? t : t + 1;           // the two of {0,1,2} other than istar
+    lam[i] = 1.0; lam[3] = -1.0;
+    return 0;
 }
 
 // --------------------------------------------------------------------------- main kernel
@@ -515,20 +562,22 @@ srb_nmpc_kernel(SrbKParams prm, int n_agents,
         c.x[n - 1] = 0.0;
     }
     for (int col = c.tid; col < nz - 1; col += WAVE) {
-        int j = col / (C - 1), i = col % (C - 1);
-        double g0 = c.foot[(j * 2 + 0) * C + i] - c.foot[(j * 2 + 0) * C + C - 1];
-        double g1 = c.foot[(j * 2 + 1) * C + i] - c.foot[(j * 2 + 1) * C + C - 1];
-        c.Z[(6 * N + C * j + i) * nz + col] = 1.0;
-        c.Z[(6 * N + C * j + C - 1) * nz + col] = -1.0;
+        int j = col / (C - 1), t = col % (C - 1);
+        double lam[4];
+        int is_null = lambda_basis(c.foot + j * 2 * C, C, t, lam);
+        double g0 = 0.0, g1 = 0.0;
+        if (!is_null)
+            for (int i = 0; i < C; i++) { g0 += c.foot[(j * 2 + 0) * C + i] * lam[i]; g1 += c.foot[(j * 2 + 1) * C + i] * lam[i]; }
+        for (int i = 0; i < C; i++) c.Z[(6 * N + C * j + i) * nz + col] = lam[i];
         c.Z[(4 * N + 2 * j) * nz + col] = g0;
         c.Z[(4 * N + 2 * j + 1) * nz + col] = g1;
         double v[4];
         for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1;
         for (int k = j; k < N; k++) {
             for (int d = 0; d < 4; d++) c.Z[(4 * k + d) * nz + col] = v[d];
-            double t[4];
-            for (int d = 0; d < 4; d++) t[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3];
-            for (int d = 0; d < 4; d++) v[d] = t[d];
+            double tt[4];
+            for (int d = 0; d < 4; d++) tt[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3];
+            for (int d = 0; d < 4; d++) v[d] = tt[d];
         }
     }
     if (c.tid == 0) c.Z[(n - 1) * nz + nz - 1] = 1.0;
@@ -669,15 +718,17 @@ srb_nmpc_kernel(SrbKParams prm, int n_agents,
 // --------------------------------------------------------------------------- k nearest neighbours
 // One thread per agent; neighbour states streamed through LDS tiles.  Order: (d^2, index)
 // ascending -- the order the reference's strict-'<' argmin scan produces (MPC_dist.cpp:373-382).
+// The query point is the agent's own current CoM from x0 (q[0], q[1] -- what the
+// reference's scan uses, MPC_dist.cpp:366), not its row of the neighbour table.
 extern "C" __global__ void __launch_bounds__(256)
-srb_knn_kernel(int n_agents, int agent_offset, const double *__restrict__ state, int n_all, int K,
-               int *__restrict__ nbr_idx)
+srb_knn_kernel(int n_agents, int agent_offset, const double *__restrict__ x0g, const double *__restrict__ state,
+               int n_all, int K, int *__restrict__ nbr_idx)
 {
     __shared__ double tile[1024 * 2];
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
     const int self = agent_offset + a;
     double px = 0, py = 0;
-    if (a < n_agents) { px = state[4 * (size_t)self]; py = state[4 * (size_t)self + 1]; }
+    if (a < n_agents) { px = x0g[4 * (size_t)a]; py = x0g[4 * (size_t)a + 2]; }
     double bd[SRB_MAX_K]; int bi[SRB_MAX_K];
     for (int j = 0; j < SRB_MAX_K; j++) { bd[j] = 1e300; bi[j] = -1; }
     for (int base = 0; base < n_all; base += 1024) {

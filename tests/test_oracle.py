@@ -104,7 +104,7 @@ def test_nlp_random_oracle_kkt_certified():
         np.testing.assert_allclose(x, cs["x"], atol=1e-9, rtol=0)
         gJ, hh = nlp_rows(N, C, Pd.size, G, h, obs, eps, p.vsat)
         cert = certify(Pd, c, A, b, gJ, hh, x)
-        assert cert["stat"] < 1e-5 and cert["prim"] < 1e-8 and cert["eq"] < 1e-10 and cert["zmin"] >= 0
+        assert cert["stat_rel"] < 1e-6 and cert["prim"] < 1e-8 and cert["eq"] < 1e-10
         obj = 0.5 * Pd @ (x * x) + c @ x
         assert obj <= cs["slsqp_obj"] + 1e-3      # at least as good as SciPy SLSQP from the same start
 
@@ -119,7 +119,7 @@ def test_kat2_nlp_certified_and_beats_logged_snopt(kat2):
     np.testing.assert_allclose(x, kat2["x_nlp"], atol=1e-9)
     gJ, hh = nlp_rows(4, 4, Pd.size, G, h, obs, eps, p.vsat)
     cert = certify(Pd, c, A, b, gJ, hh, x)
-    assert cert["stat"] < 1e-6 and cert["prim"] < 1e-9
+    assert cert["stat_rel"] < 1e-8 and cert["prim"] < 1e-9
     # SNOPT's logged point (INFO 3, not converged) violates an obstacle row by ~3e-4
     g_snopt, _ = gJ(np.asarray(kat2["snopt_final_x"]))
     assert (g_snopt - hh).max() > 1e-4
