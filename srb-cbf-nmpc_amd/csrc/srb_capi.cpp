@@ -12,12 +12,16 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
-extern "C" __global__ void srb_nmpc_kernel(SrbKParams prm, int n_agents, const double *x0g, const double *refg,
-                                           const double *footg, const double *obstacles, int n_obs,
-                                           const double *nbr_state, const int *nbr_idx, double *x_qp_out,
-                                           double *x_out, double *obj_out, int *status_out, int *iters_out);
+#define DECL_NMPC(NAME)                                                                                       \
+    extern "C" __global__ void NAME(SrbKParams prm, int n_agents, const double *x0g, const double *refg,      \
+                                    const double *footg, const double *obstacles, const int *obs_idx,          \
+                                    const double *nbr_state, const int *nbr_idx, double *x_qp_out,             \
+                                    double *x_out, double *obj_out, int *status_out, int *iters_out);
+DECL_NMPC(srb_nmpc_kernel_nz16)
+DECL_NMPC(srb_nmpc_kernel_nz32)
+DECL_NMPC(srb_nmpc_kernel_nz64)
 extern "C" __global__ void srb_knn_kernel(int n_agents, int agent_offset, const double *x0g, const double *state,
-                                          int n_all, int K, int *nbr_idx);
+                                          int stride, int n_all, int K, int *nbr_idx);
 
 static thread_local std::string g_err;
 
@@ -40,7 +44,7 @@ struct srb_ctx {
     hipEvent_t ev[4];
     // device staging
     double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj;
-    int *status, *iters, *nbr_idx;
+    int *status, *iters, *nbr_idx, *obs_idx;
     size_t cap_obs, cap_nbr;
     float knn_ms, solve_ms;
     bool timed;
@@ -106,7 +110,8 @@ static int validate(const srb_params *p)
 {
     if (!p) return fail(SRB_ERR_ARG, "null params");
     if (p->N < 2 || p->C < 2 || p->C > 4) return fail(SRB_ERR_ARG, "need N >= 2 and 2 <= C <= 4");
-    if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs + p->K_nbr > SRB_MAX_K) return fail(SRB_ERR_ARG, "K_obs + K_nbr out of range");
+    if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs + p->K_nbr > SRB_MAX_K || p->K_nbr > SRB_KNN_MAX)
+        return fail(SRB_ERR_ARG, "K_obs + K_nbr out of range (K_nbr <= 16, K_obs + K_nbr <= 32)");
     if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 64 (one xi entry per lane)");
     if ((6 + p->C) * p->N + 1 > SRB_MAX_NV) return fail(SRB_ERR_SIZE, "nv exceeds 256");
     SrbKParams k = make_kparams(p, p->use_nlp);
@@ -145,6 +150,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
     HIPCHK(hipMalloc(&c->nbr_idx, A * Kn * sizeof(int)));
+    HIPCHK(hipMalloc(&c->obs_idx, A * (p->K_obs > 0 ? p->K_obs : 1) * sizeof(int)));
     *out = c;
     return SRB_OK;
 }
@@ -154,7 +160,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->nbr_idx, c->obstacles, c->nbr};
+    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->nbr_idx, c->obs_idx, c->obstacles, c->nbr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -184,16 +190,29 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     const int *nbr_idx = nullptr;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
-    if (use_nlp && k.K_nbr > 0) {
-        dim3 blk(256), grd((n_agents + 255) / 256);
-        hipLaunchKernelGGL(srb_knn_kernel, grd, blk, 0, s, n_agents, d->agent_offset, d->x0, d->nbr_state, d->n_all,
-                           k.K_nbr, c->nbr_idx);
+    dim3 kblk(256), kgrd((n_agents + 255) / 256);
+    if (use_nlp && k.K_obs > 0) {       // K_obs nearest static obstacles (MPC_dist.cpp:371-396)
+        hipLaunchKernelGGL(srb_knn_kernel, kgrd, kblk, 0, s, n_agents, -1, d->x0, d->obstacles, 2, d->n_obs,
+                           k.K_obs, c->obs_idx);
+        HIPCHK(hipGetLastError());
+    }
+    if (use_nlp && k.K_nbr > 0) {       // K_nbr nearest other agents
+        hipLaunchKernelGGL(srb_knn_kernel, kgrd, kblk, 0, s, n_agents, d->agent_offset, d->x0, d->nbr_state, 4,
+                           d->n_all, k.K_nbr, c->nbr_idx);
         HIPCHK(hipGetLastError());
         nbr_idx = c->nbr_idx;
     }
     HIPCHK(hipEventRecord(c->ev[1], s));
-    hipLaunchKernelGGL(srb_nmpc_kernel, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
-                       d->obstacles, d->n_obs, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
+    // kernel instance by the register-resident bound on nz (one row of Z'HZ per lane)
+    if (k.nz <= 16)
+        hipLaunchKernelGGL(srb_nmpc_kernel_nz16, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
+    else if (k.nz <= 32)
+        hipLaunchKernelGGL(srb_nmpc_kernel_nz32, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
+    else
+        hipLaunchKernelGGL(srb_nmpc_kernel_nz64, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[2], s));
     return SRB_OK;
@@ -318,3 +337,17 @@ extern "C" void srb_fit_bezier(const double buf[4], const double *X, double alph
 }
 
 extern "C" const char *srb_last_error(void) { return g_err.c_str(); }
+
+#ifdef SRB_STAMPS
+extern __device__ unsigned long long srb_stamp_buf[32];
+extern "C" int srb_debug_stamps(unsigned long long *out, int reset)
+{
+    HIPCHK(hipDeviceSynchronize());
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_stamp_buf), sizeof(unsigned long long) * 32));
+    if (reset) {
+        unsigned long long z[32] = {0};
+        HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(srb_stamp_buf), z, sizeof z));
+    }
+    return SRB_OK;
+}
+#endif

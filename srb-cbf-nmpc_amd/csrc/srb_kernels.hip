@@ -11,7 +11,7 @@
 // Layout / execution model
 //   * one 64-lane wavefront (= one workgroup) per agent; the whole solve -- problem
 //     assembly, both interior-point loops, output -- runs inside that wave with all
-//     per-agent state in LDS, so there is no host round trip per iteration;
+//     per-agent vectors in LDS, so there is no host round trip per iteration;
 //   * equality constraints (LIP dynamics, u_k = F_k lambda_k, sum lambda_k = 1) are
 //     eliminated by a null-space basis Z built from a forward rollout:
 //         x = xbar + Z xi,  xi = (lambda dofs of every grid, s),  nz = N(C-1)+1,
@@ -20,6 +20,12 @@
 //     exact arithmetic: x, s, z are advanced exactly as Prime.c:208-216 and the
 //     equality multipliers are carried as q = A'y (q += alpha_d * A'dy), which is all
 //     the residual rx = -Px - A'y - G'z - c of computeresiduals needs;
+//   * the solve is latency-bound (one wave per agent, a few thousand flops per
+//     iteration), so the dense factor and both triangular solves live in registers,
+//     one row of the nz x nz system per lane, with cross-lane values moved by
+//     v_readlane (NZM = compile-time bound on nz: 16 or 32); Z'HZ is assembled from
+//     its structurally nonzero terms only; per-row reciprocals are formed once per
+//     iteration;
 //   * inputs/outputs are agent-major fp64 arrays in HBM, read once / written once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
@@ -40,12 +46,36 @@ __device__ __forceinline__ double wmin(double v)
     for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
     return v;
 }
+__device__ __forceinline__ double wmax(double v) { return -wmin(-v); }
 __device__ __forceinline__ int wor(int v)
 {
 #pragma unroll
     for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, WAVE);
     return v;
 }
+// value of lane `lane` (wave-uniform index, SGPR) -> wave-uniform value
+__device__ __forceinline__ double readlane_d(double v, int lane)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// --------------------------------------------------------------------------- diagnostic stamps
+// Built only with -DSRB_STAMPS (make stamps -> srbnmpc/libsrbnmpc_stamps.so): lane 0 of
+// agent 0 accumulates s_memtime cycles per phase into a buffer nothing else reads.
+#ifdef SRB_STAMPS
+__device__ unsigned long long srb_stamp_buf[32];
+#define STAMP_DECL unsigned long long _st_t0 = 0; const bool _st_on = (blockIdx.x == 0 && threadIdx.x == 0);
+#define STAMP_BEGIN() do { __builtin_amdgcn_sched_barrier(0); _st_t0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define STAMP_END(slot) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); if (_st_on) srb_stamp_buf[slot] += _t - _st_t0; _st_t0 = _t; } while (0)
+#else
+#define STAMP_DECL
+#define STAMP_BEGIN() do {} while (0)
+#define STAMP_END(slot) do {} while (0)
+#endif
 
 // --------------------------------------------------------------------------- per-agent context
 struct Ctx {
@@ -54,8 +84,8 @@ struct Ctx {
     int rFm, rXp, rXm, rUp, rUm, rLlo, rLhi, rO, rV;
     // LDS arrays
     double *Z, *x, *q, *rx, *dx, *tv, *D, *ref, *foot, *offv;
-    double *s, *z, *rz, *dz, *dsv, *dsT, *om, *jc, *obs, *eps;
-    double *Hc, *L, *ZtZ, *ZtZL, *hvec;
+    double *s, *z, *rz, *dz, *dsv, *dsT, *om, *iz, *is, *l2, *jc, *obs, *eps;
+    double *Hc, *L, *dinv, *ZtZ, *ZtZL, *ZtZdinv, *hvec, *xiv;
     int tid;
 };
 
@@ -122,7 +152,7 @@ __device__ __forceinline__ double jt_gather(const Ctx &c, int v, const double *w
 }
 
 // out[v] = base[v] + sign*(J' w)[v] for all v (s row by reduction).  Collective.
-__device__ void jt_apply(const Ctx &c, const double *w, double *out, const double *base, double sign)
+__device__ __forceinline__ void jt_apply(const Ctx &c, const double *w, double *out, const double *base, double sign)
 {
     for (int v = c.tid; v < c.n - 1; v += WAVE) out[v] = (base ? base[v] : 0.0) + sign * jt_gather(c, v, w);
     double ps = 0.0;
@@ -154,7 +184,7 @@ __device__ __forceinline__ double hess_diag(const Ctx &c, int v)
 }
 
 // obstacle Jacobian coefficients at the current x: jc = -2 (p_k - o_kj)
-__device__ void obstacle_coefs(const Ctx &c)
+__device__ __forceinline__ void obstacle_coefs(const Ctx &c)
 {
     for (int o = c.tid; o < c.N * c.K; o += WAVE) {
         int k = o / c.K;
@@ -164,25 +194,21 @@ __device__ void obstacle_coefs(const Ctx &c)
     __syncthreads();
 }
 
-// g_r(x) for all rows -> rz = h - s - g  (collective)
-__device__ void residual_rows(const Ctx &c)
+// g_r(x) of row r (nonlinear for obstacle rows)
+__device__ __forceinline__ double row_val(const Ctx &c, int r)
 {
-    for (int r = c.tid; r < c.m; r += WAVE) {
-        double g;
-        if (r >= c.rO && r < c.rV) {
-            int o = r - c.rO, k = o / c.K;
-            double dx = c.x[4 * k] - c.obs[2 * o], dy = c.x[4 * k + 2] - c.obs[2 * o + 1];
-            g = -(dx * dx + dy * dy) - c.x[c.n - 1];
-        } else {
-            g = row_dot(c, r, c.x);
-        }
-        c.rz[r] = c.hvec[r] - c.s[r] - g;
+    if (r >= c.rO && r < c.rV) {
+        int o = r - c.rO, k = o / c.K;
+        double dx = c.x[4 * k] - c.obs[2 * o], dy = c.x[4 * k + 2] - c.obs[2 * o + 1];
+        return -(dx * dx + dy * dy) - c.x[c.n - 1];
     }
+    return row_dot(c, r, c.x);
 }
 
-// Build D (diag of H), offdiag values, then Hc = Z' H Z (+ delta ZtZ done by caller).
-// H = P + hess + delta I + J' diag(om) J.
-__device__ void build_H(const Ctx &c, double delta)
+// --------------------------------------------------------------------------- Z'HZ assembly
+// D (diag of H), friction couplings offv[0..2N-3], obstacle couplings per grid
+// (xy, xs, ys) at offv[2N-2 + 3k].  H = P + hess + delta I + J' diag(om) J.
+__device__ __forceinline__ void build_D(const Ctx &c, double delta)
 {
     const int N = c.N, n = c.n;
     for (int v = c.tid; v < n - 1; v += WAVE) {
@@ -214,7 +240,6 @@ __device__ void build_H(const Ctx &c, double delta)
         for (int o = c.tid; o < N * c.K; o += WAVE) ps += c.om[c.rO + o];
     ps = wsum(ps);
     if (c.tid == 0) c.D[n - 1] = Pdiag(c, n - 1) + delta + ps;
-    // off-diagonals: friction (i,d) -> (4i+2d, 4N+2(i+1)+d); obstacle stage k -> (xk,yk),(xk,s),(yk,s)
     const int nf = 2 * (N - 1);
     for (int e = c.tid; e < nf; e += WAVE) c.offv[e] = -(c.om[e] + c.om[c.rFm + e]);
     if (c.nl)
@@ -228,242 +253,323 @@ __device__ void build_H(const Ctx &c, double delta)
             c.offv[nf + 3 * k] = xy; c.offv[nf + 3 * k + 1] = xs; c.offv[nf + 3 * k + 2] = ys;
         }
     __syncthreads();
-    // Hc[a][b], a <= b
-    const int nz = c.nz, npair = nz * (nz + 1) / 2;
+}
+
+// out[a][b] = (Z' H Z)[a][b] from the structurally nonzero terms only:
+//   lambda columns of grid j touch X rows of grids >= j, the U/lambda rows of grid j;
+//   a friction coupling (X_i pos, U_{i+1}) links columns of grids <= i and i+1;
+//   the s column touches only s and (NLP) the obstacle couplings.
+// unit != 0: H = I (gives Z'Z).
+__device__ __forceinline__ void build_Hc(const Ctx &c, double *out, int unit)
+{
+    const int N = c.N, n = c.n, nz = c.nz, C = c.C, nf = 2 * (N - 1);
+    const double *Z = c.Z, *D = c.D, *off = c.offv;
+    const int npair = nz * (nz + 1) / 2;
     for (int pidx = c.tid; pidx < npair; pidx += WAVE) {
-        // decode pidx -> (a, b) with a <= b, row-major over b
         int b = (int)((sqrt(8.0 * pidx + 1.0) - 1.0) * 0.5);
         while (b * (b + 1) / 2 > pidx) b--;
         while ((b + 1) * (b + 2) / 2 <= pidx) b++;
-        int a = pidx - b * (b + 1) / 2;
-        int ja = col_stage(c, a), jb = col_stage(c, b);
-        int k0 = ja > jb ? ja : jb;
-        double acc = 0.0;
-        // X rows of grids >= max stage (Z_X is block lower triangular)
-        for (int v = 4 * k0; v < 4 * N; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
-        if (ja == jb && ja < N) {
-            for (int v = 4 * N + 2 * ja; v < 4 * N + 2 * ja + 2; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
-            for (int v = 6 * N + c.C * ja; v < 6 * N + c.C * ja + c.C; v++) acc += c.D[v] * c.Z[v * nz + a] * c.Z[v * nz + b];
-        }
-        if (ja == N && jb == N) acc += c.D[n - 1];
-        for (int e = 0; e < nf; e++) {
-            int i = e >> 1, d = e & 1, u = 4 * i + 2 * d, w = 4 * N + 2 * (i + 1) + d;
-            acc += c.offv[e] * (c.Z[u * nz + a] * c.Z[w * nz + b] + c.Z[w * nz + a] * c.Z[u * nz + b]);
-        }
-        if (c.nl)
-            for (int k = 0; k < N; k++) {
-                double xa = c.Z[(4 * k) * nz + a], ya = c.Z[(4 * k + 2) * nz + a], sa = c.Z[(n - 1) * nz + a];
-                double xb = c.Z[(4 * k) * nz + b], yb = c.Z[(4 * k + 2) * nz + b], sb = c.Z[(n - 1) * nz + b];
-                acc += c.offv[nf + 3 * k] * (xa * yb + ya * xb) + c.offv[nf + 3 * k + 1] * (xa * sb + sa * xb) +
-                       c.offv[nf + 3 * k + 2] * (ya * sb + sa * yb);
+        const int a = pidx - b * (b + 1) / 2;          // a <= b, so stage(a) <= stage(b)
+        const int ja = col_stage(c, a), jb = col_stage(c, b);
+        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
+        if (jb < N) {
+            // X rows of grids >= jb: 4 independent accumulators (one per state component)
+            for (int k = jb; k < N; k++) {
+                const int v = 4 * k;
+                const double d0 = unit ? 1.0 : D[v], d1 = unit ? 1.0 : D[v + 1];
+                const double d2 = unit ? 1.0 : D[v + 2], d3 = unit ? 1.0 : D[v + 3];
+                acc0 += d0 * Z[v * nz + a] * Z[v * nz + b];
+                acc1 += d1 * Z[(v + 1) * nz + a] * Z[(v + 1) * nz + b];
+                acc2 += d2 * Z[(v + 2) * nz + a] * Z[(v + 2) * nz + b];
+                acc3 += d3 * Z[(v + 3) * nz + a] * Z[(v + 3) * nz + b];
+                if (c.nl && !unit) {
+                    const double xa = Z[v * nz + a], ya = Z[(v + 2) * nz + a];
+                    const double xb = Z[v * nz + b], yb = Z[(v + 2) * nz + b];
+                    acc1 += off[nf + 3 * k] * (xa * yb + ya * xb);
+                }
             }
-        c.Hc[a * nz + b] = acc;
-        c.Hc[b * nz + a] = acc;
-    }
-    __syncthreads();
-}
-
-// In-place Cholesky of L (nz x nz, lower). Returns 0 on success (uniform).
-// regularise != 0 mirrors iSWIFT's dynamic pivot regularisation (ldl.c:320-321:
-// |D_kk| <= 1e-14 -> 1e-7) for the QP stage, where the reduced Hessian is PD in exact
-// arithmetic but can lose a pivot to round-off along a lambda direction whose bound
-// rows have gone inactive (4 contacts: u = F lambda leaves one lambda direction free).
-__device__ int chol_lds(const Ctx &c, double *L, int nz, int regularise = 0)
-{
-    for (int k = 0; k < nz; k++) {
-        __syncthreads();
-        double d = L[k * nz + k];
-        if (regularise && d <= 1e-14 && d == d) d = 1e-7;
-        if (!(d > 0.0)) return -1;
-        d = sqrt(d);
-        __syncthreads();
-        if (c.tid == 0) L[k * nz + k] = d;
-        for (int i = k + 1 + c.tid; i < nz; i += WAVE) L[i * nz + k] /= d;
-        __syncthreads();
-        for (int i = k + 1 + c.tid; i < nz; i += WAVE) {
-            double lik = L[i * nz + k];
-            for (int j = k + 1; j <= i; j++) L[i * nz + j] -= lik * L[j * nz + k];
+            if (ja == jb) {
+                for (int v = 4 * N + 2 * ja; v < 4 * N + 2 * ja + 2; v++)
+                    acc2 += (unit ? 1.0 : D[v]) * Z[v * nz + a] * Z[v * nz + b];
+                for (int v = 6 * N + C * ja; v < 6 * N + C * ja + C; v++)
+                    acc3 += (unit ? 1.0 : D[v]) * Z[v * nz + a] * Z[v * nz + b];
+            } else if (!unit) {
+                const int i = jb - 1;                 // friction rows between grid i pos and grid jb CoP
+                for (int d = 0; d < 2; d++)
+                    acc0 += off[2 * i + d] * Z[(4 * i + 2 * d) * nz + a] * Z[(4 * N + 2 * jb + d) * nz + b];
+            }
+        } else if (ja < N) {
+            if (c.nl && !unit)
+                for (int k = ja; k < N; k++)
+                    acc0 += off[nf + 3 * k + 1] * Z[(4 * k) * nz + a] + off[nf + 3 * k + 2] * Z[(4 * k + 2) * nz + a];
+        } else {
+            acc0 = unit ? 1.0 : D[n - 1];
         }
+        const double acc = (acc0 + acc1) + (acc2 + acc3);
+        out[a * nz + b] = acc;
+        out[b * nz + a] = acc;
     }
     __syncthreads();
-    return 0;
 }
 
-// Solve (L L') y = b with b held one entry per lane (lane i < nz). Returns y in the same form.
-__device__ double chol_solve_reg(const Ctx &c, const double *L, int nz, double bi)
+// --------------------------------------------------------------------------- register Cholesky
+// Lane i holds row i of the trailing matrix in a register window row[0..NZM-1] that
+// shifts left by one column per elimination step, so the pivot column is always row[0]
+// and every register index is a compile-time constant while the step loop over k stays
+// a runtime loop (small code: one copy of an NZM-wide body).  Cross-lane operands move
+// by v_readlane with a wave-uniform lane index.  Writes L (lower, LDS) and 1/L_kk.
+// regularise != 0 mirrors iSWIFT's dynamic pivot regularisation (ldl.c:320-321:
+// |D_kk| <= 1e-14 -> 1e-7) for the QP stage.  Returns 0 on success (wave-uniform).
+template <int NZM>
+__device__ __forceinline__ int chol_reg(const Ctx &c, const double *H, double *L, double *dinv, int nz, int regularise)
 {
+    const int i = c.tid;
+    double row[NZM];
+#pragma unroll
+    for (int j = 0; j < NZM; j++) row[j] = (i < nz && j < nz) ? H[i * nz + j] : 0.0;
+    int fail = 0;
+#pragma clang loop unroll(disable)
     for (int k = 0; k < nz; k++) {
-        double yk = __shfl(bi, k, WAVE) / L[k * nz + k];
-        if (c.tid == k) bi = yk;
-        else if (c.tid > k && c.tid < nz) bi -= L[c.tid * nz + k] * yk;
+        double piv = readlane_d(row[0], k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        if (!(piv > 0.0)) { fail = 1; break; }
+        const double d = sqrt(piv), inv = 1.0 / d;
+        const double l = (i > k && i < nz) ? row[0] * inv : 0.0;
+        if (i > k && i < nz) L[i * nz + k] = l;
+        if (i == k) { L[k * nz + k] = d; dinv[k] = inv; }
+#pragma unroll
+        for (int t = 1; t < NZM; t++) {
+            const double lj = readlane_d(l, (k + t) & (WAVE - 1));   // lanes <= k hold l = 0
+            row[t - 1] = row[t] - l * lj;
+        }
+        row[NZM - 1] = 0.0;
     }
-    for (int k = nz - 1; k >= 0; k--) {
-        double xk = __shfl(bi, k, WAVE) / L[k * nz + k];
-        if (c.tid == k) bi = xk;
-        else if (c.tid < k) bi -= L[k * nz + c.tid] * xk;
-    }
-    return bi;
+    __syncthreads();
+    return fail;
 }
 
-// xi-vector (one entry per lane) = Z' v
+// (L L') x = b with b one entry per lane (lane i < nz); returns x in the same layout.
+// Runtime loops; the L operand of step k+1 is loaded while step k completes.
+__device__ __forceinline__ double chol_solve_reg(const Ctx &c, const double *L, const double *dinv, int nz, double b)
+{
+    const int i = c.tid;
+    double lnext = (i > 0 && i < nz) ? L[i * nz] : 0.0;
+#pragma clang loop unroll(disable)
+    for (int k = 0; k < nz; k++) {
+        const double lik = lnext;
+        lnext = (k + 1 < nz && i > k + 1 && i < nz) ? L[i * nz + k + 1] : 0.0;
+        const double yk = readlane_d(b, k) * dinv[k];
+        b = (i == k) ? yk : b - lik * yk;
+    }
+    lnext = (nz - 1 > i) ? L[(nz - 1) * nz + i] : 0.0;
+#pragma clang loop unroll(disable)
+    for (int k = nz - 1; k >= 0; k--) {
+        const double lki = lnext;
+        lnext = (k >= 1 && k - 1 > i) ? L[(k - 1) * nz + i] : 0.0;
+        const double xk = readlane_d(b, k) * dinv[k];
+        b = (i == k) ? xk : b - lki * xk;
+    }
+    return b;
+}
+
+// xi-vector (one entry per lane) = Z' v.  Lanes (a, d) = (4a + d) sum the X rows of state
+// component d over grids >= stage(a); the quad is reduced by xor-shuffles; the U/lambda
+// rows of the column's own grid are added by the d == 0 lane.
+template <int NZM>
 __device__ __forceinline__ double zt_mul(const Ctx &c, const double *v)
 {
-    double acc = 0.0;
-    if (c.tid < c.nz) {
-        int a = c.tid, ja = col_stage(c, a);
-        if (ja < c.N) {
-            for (int r = 4 * ja; r < 4 * c.N; r++) acc += c.Z[r * c.nz + a] * v[r];
-            for (int r = 4 * c.N + 2 * ja; r < 4 * c.N + 2 * ja + 2; r++) acc += c.Z[r * c.nz + a] * v[r];
-            for (int r = 6 * c.N + c.C * ja; r < 6 * c.N + c.C * ja + c.C; r++) acc += c.Z[r * c.nz + a] * v[r];
-        } else {
-            acc = v[c.n - 1];
+    const int N = c.N, nz = c.nz, C = c.C, d = c.tid & 3;
+    double res = 0.0;
+#pragma unroll
+    for (int round = 0; round < (NZM + 15) / 16; round++) {
+        const int a = round * 16 + (c.tid >> 2);
+        double acc = 0.0;
+        if (a < nz) {
+            const int ja = col_stage(c, a);
+            if (ja < N) {
+                double a0 = 0.0, a1 = 0.0;
+                int k = ja;
+                for (; k + 1 < N; k += 2) {
+                    a0 += c.Z[(4 * k + d) * nz + a] * v[4 * k + d];
+                    a1 += c.Z[(4 * (k + 1) + d) * nz + a] * v[4 * (k + 1) + d];
+                }
+                if (k < N) a0 += c.Z[(4 * k + d) * nz + a] * v[4 * k + d];
+                acc = a0 + a1;
+                if (d == 0) {
+                    for (int r = 4 * N + 2 * ja; r < 4 * N + 2 * ja + 2; r++) acc += c.Z[r * nz + a] * v[r];
+                } else if (d == 1) {
+                    for (int r = 6 * N + C * ja; r < 6 * N + C * ja + C; r++) acc += c.Z[r * nz + a] * v[r];
+                }
+            } else if (d == 0) {
+                acc = v[c.n - 1];
+            }
         }
+        acc += __shfl_xor(acc, 1, WAVE);
+        acc += __shfl_xor(acc, 2, WAVE);
+        // lane a' takes column a' of this round from lane 4 (a' - 16 round)
+        const int src = 4 * ((c.tid - round * 16) & 15);
+        const double got = __shfl(acc, src, WAVE);
+        if (c.tid >= round * 16 && c.tid < round * 16 + 16) res = got;
     }
-    return acc;
+    return (c.tid < nz) ? res : 0.0;
 }
 
-// out = Z xi  (xi one entry per lane)
-__device__ void z_mul(const Ctx &c, double xi, double *out)
+// out = Z xi  (xi one entry per lane); columns of grid j reach X rows of grids >= j and
+// the U/lambda rows of grid j only.
+template <int NZM>
+__device__ __forceinline__ void z_mul(const Ctx &c, double xi, double *out)
 {
-    for (int v = c.tid; v < c.n; v += WAVE) out[v] = 0.0;
-    // every lane needs every xi_a: loop a with shuffles (uniform)
-    double accs[4] = {0, 0, 0, 0};
-    for (int a = 0; a < c.nz; a++) {
-        double xa = __shfl(xi, a, WAVE);
-#pragma unroll
-        for (int t = 0; t < 4; t++) {
-            int v = c.tid + t * WAVE;
-            if (v < c.n) accs[t] += c.Z[v * c.nz + a] * xa;
+    const int N = c.N, nz = c.nz, C = c.C, n = c.n;
+    if (c.tid < nz) c.xiv[c.tid] = xi;
+    __syncthreads();
+    const double *xs = c.xiv;                       // LDS broadcast reads
+    for (int v = c.tid; v < n; v += WAVE) {
+        double a0 = 0.0, a1 = 0.0;
+        if (v < 4 * N) {
+            const int lim = ((v >> 2) + 1) * (C - 1);     // columns of grids <= k
+            int a = 0;
+            for (; a + 1 < lim; a += 2) {
+                a0 += c.Z[v * nz + a] * xs[a];
+                a1 += c.Z[v * nz + a + 1] * xs[a + 1];
+            }
+            if (a < lim) a0 += c.Z[v * nz + a] * xs[a];
+        } else if (v < n - 1) {
+            const int j = (v < 6 * N) ? (v - 4 * N) >> 1 : (v - 6 * N) / C;
+            for (int a = j * (C - 1); a < (j + 1) * (C - 1); a++) a0 += c.Z[v * nz + a] * xs[a];
+        } else {
+            a0 = xs[nz - 1];
         }
+        out[v] = a0 + a1;
     }
-#pragma unroll
-    for (int t = 0; t < 4; t++) { int v = c.tid + t * WAVE; if (v < c.n) out[v] = accs[t]; }
     __syncthreads();
 }
 
 // Newton solve with the current factor L and weights om:
 //   [H A' J'; A 0 0; J 0 -W][dx;dy;dz] = [r1; 0; r3], W^-1 = om
-// r1 (n) given, r3 in dz on entry (overwritten with dz).  dx -> c.dx.  Uses c.tv.
-__device__ void newton_solve(const Ctx &c, const double *r1, double *r3dz)
+// r1 (n) given, r3 in r3dz on entry (overwritten with dz).  dx -> c.dx.  Uses c.tv, c.dsv.
+template <int NZM>
+__device__ __forceinline__ void newton_solve(const Ctx &c, const double *r1, double *r3dz)
 {
-    // tv = r1 + J' (om .* r3); om .* r3 staged in the dsv scratch (callers recompute dsv)
-    double *w = c.dsv;                      // scratch m-vector (caller recomputes dsv after)
+    double *w = c.dsv;                      // scratch m-vector (callers recompute dsv after)
     for (int r = c.tid; r < c.m; r += WAVE) w[r] = c.om[r] * r3dz[r];
     __syncthreads();
     jt_apply(c, w, c.tv, r1, 1.0);
-    double g = zt_mul(c, c.tv);
-    double xi = chol_solve_reg(c, c.L, c.nz, g);
-    z_mul(c, xi, c.dx);
+    const double g = zt_mul<NZM>(c, c.tv);
+    const double xi = chol_solve_reg(c, c.L, c.dinv, c.nz, g);
+    z_mul<NZM>(c, xi, c.dx);
     for (int r = c.tid; r < c.m; r += WAVE) r3dz[r] = c.om[r] * (row_dot(c, r, c.dx) - r3dz[r]);
     __syncthreads();
 }
 
-// findsteplength (Auxilary.c:271-294): uniform result
-__device__ __forceinline__ double steplen(const Ctx &c, const double *v, const double *dv)
+// findsteplength (Auxilary.c:271-294): min over dv_r < 0 of -v_r/dv_r, 1 when no dv_r < 0.
+// Evaluated as 1 / max_r(-dv_r * (1/v_r)) with the per-iteration reciprocals of s and z,
+// so one division per call instead of one per row (equal up to rounding).  Uniform.
+__device__ __forceinline__ double steplen(const Ctx &c, const double *inv_v, const double *dv)
 {
-    double a = 1e10; int f = 0;
-    for (int r = c.tid; r < c.m; r += WAVE)
-        if (dv[r] < 0.0) { double t = -(v[r] / dv[r]); if (t < a) a = t; f = 1; }
-    a = wmin(a); f = wor(f);
-    return f ? a : 1.0;
+    double mx = 0.0;
+    for (int r = c.tid; r < c.m; r += WAVE) mx = fmax(mx, -dv[r] * inv_v[r]);
+    mx = wmax(mx);
+    return (mx > 0.0) ? 1.0 / mx : 1.0;
 }
 
 // One interior-point solve (QP stage: nl = 0, iSWIFT; NLP stage: nl = 1).
 // Returns exit code; *iters gets the number of steps taken.
-__device__ int ipm(Ctx &c, int maxit, int *iters)
+template <int NZM>
+__device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
 {
     const double tol = c.P->tol, th = tol / sqrt(3.0);
     double sigma = 100.0;               // options->sigma = SIGMA
     const double sigma_d = 0.0;
     int flag = 2, it = 0;
     double delta = 0.0;
+    STAMP_DECL
+    const int sb = c.nl ? 16 : 0;       // stamp slots: QP 0..15, NLP 16..31
     for (int iter = 0; iter < maxit; iter++) {
+        STAMP_BEGIN();
         if (c.nl) obstacle_coefs(c);
-        residual_rows(c);
-        // rx = -(P x + c) - q - J' z
-        __syncthreads();
+        // rz = h - s - g(x); tv = -(P x + c) - q
+        for (int r = c.tid; r < c.m; r += WAVE) c.rz[r] = c.hvec[r] - c.s[r] - row_val(c, r);
         for (int v = c.tid; v < c.n; v += WAVE) c.tv[v] = -(Pdiag(c, v) * c.x[v] + cvec(c, v)) - c.q[v];
         __syncthreads();
-        jt_apply(c, c.z, c.rx, c.tv, -1.0);
-        double nrx = 0, nrz = 0, sz = 0;
-        for (int v = c.tid; v < c.n; v += WAVE) nrx += c.rx[v] * c.rx[v];
-        for (int r = c.tid; r < c.m; r += WAVE) { nrz += c.rz[r] * c.rz[r]; sz += c.s[r] * c.z[r]; }
-        nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz);
+        jt_apply(c, c.z, c.rx, c.tv, -1.0);     // rx = -(P x + c) - q - J'z
+        double nrx = 0, nrz = 0, sz = 0, mu = 0, gm = 1.0;
+        for (int v = c.tid; v < c.n; v += WAVE) {
+            nrx += c.rx[v] * c.rx[v];
+            if (c.nl) gm = fmax(gm, fabs(Pdiag(c, v) * c.x[v] + cvec(c, v)));
+        }
+        for (int r = c.tid; r < c.m; r += WAVE) {
+            const double sr = c.s[r], zr = c.z[r];
+            nrz += c.rz[r] * c.rz[r]; sz += sr * zr;
+            const double l = sqrt(sr * zr), l2 = l * l;     // formlambda, lambda.*lambda
+            c.l2[r] = l2; mu += l2;
+            c.iz[r] = 1.0 / zr; c.is[r] = 1.0 / sr;
+        }
+        nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz); mu = wsum(mu) / c.m;
+        if (c.nl) gm = wmax(gm);
+        STAMP_END(sb + 0);
         if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
         // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
-        double thx = th;
-        if (c.nl) {
-            double gm = 1.0;
-            for (int v = c.tid; v < c.n; v += WAVE) gm = fmax(gm, fabs(Pdiag(c, v) * c.x[v] + cvec(c, v)));
-            thx = th * -wmin(-gm);
-        }
+        const double thx = c.nl ? th * gm : th;
         if (nrx < thx && nrz < th && sz / c.m < tol) { flag = 0; break; }
-        double mu = 0;
-        for (int r = c.tid; r < c.m; r += WAVE) { double l = sqrt(c.s[r] * c.z[r]); mu += l * l; }
-        mu = wsum(mu) / c.m;
         const int pc = c.nl || (sigma > sigma_d);
         if (pc) {
             // weights W^-1 = 1/(s/z) (updatekktmatrix, Auxilary.c:197-205) and factor
             for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0 / (c.s[r] / c.z[r]);
             __syncthreads();
+            STAMP_END(sb + 1);
             delta = 0.0;
             double dstart = 0.0;
             int ok = 0;
             for (int tries = 0; tries < (c.nl ? 14 : 1); tries++) {
-                build_H(c, delta);
+                build_D(c, delta);
+                build_Hc(c, c.Hc, 0);
+                STAMP_END(sb + 2);
                 if (tries == 0) {       // scale-aware first shift: 1e-10 * max(1, max diag of Z'HZ)
                     double dm = 1.0;
                     for (int a = c.tid; a < c.nz; a += WAVE) dm = fmax(dm, c.Hc[a * c.nz + a]);
-                    dstart = 1e-10 * -wmin(-dm);
+                    dstart = 1e-10 * wmax(dm);
                 }
-                for (int i = c.tid; i < c.nz * c.nz; i += WAVE) c.L[i] = c.Hc[i];
-                __syncthreads();
-                if (chol_lds(c, c.L, c.nz, !c.nl) == 0) { ok = 1; break; }
+                int cf = chol_reg<NZM>(c, c.Hc, c.L, c.dinv, c.nz, !c.nl);
+                STAMP_END(sb + 3);
+                if (cf == 0) { ok = 1; break; }
                 delta = (delta == 0.0) ? dstart : delta * 10.0;
             }
             if (!ok) { flag = 1; break; }
             // predictor: ds = -lambda.*lambda
             for (int r = c.tid; r < c.m; r += WAVE) {
-                double l = sqrt(c.s[r] * c.z[r]);
-                c.dsT[r] = -l * l;
-                c.dz[r] = c.rz[r] - c.dsT[r] / c.z[r];
+                c.dsT[r] = -c.l2[r];
+                c.dz[r] = c.rz[r] - c.dsT[r] * c.iz[r];
             }
             __syncthreads();
-            newton_solve(c, c.rx, c.dz);
-            for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) / c.z[r];
+            STAMP_END(sb + 4);
+            newton_solve<NZM>(c, c.rx, c.dz);
+            STAMP_END(sb + 5);
+            for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) * c.iz[r];
             __syncthreads();
-            double ap = steplen(c, c.s, c.dsv), ad = steplen(c, c.z, c.dz);
-            double num = 0, den = 0;
-            for (int r = c.tid; r < c.m; r += WAVE) {
-                num += (c.s[r] + ap * c.dsv[r]) * (c.z[r] + ad * c.dz[r]);
-                den += c.s[r] * c.z[r];
-            }
-            num = wsum(num); den = wsum(den);
-            double rho = num / den, mr = rho < 1.0 ? rho : 1.0;
+            double ap = steplen(c, c.is, c.dsv), ad = steplen(c, c.iz, c.dz);
+            double num = 0;
+            for (int r = c.tid; r < c.m; r += WAVE) num += (c.s[r] + ap * c.dsv[r]) * (c.z[r] + ad * c.dz[r]);
+            num = wsum(num);
+            double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
             sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
-            for (int r = c.tid; r < c.m; r += WAVE) {
-                double l = sqrt(c.s[r] * c.z[r]);
-                c.dsT[r] = -(l * l) - (c.dsv[r] * c.dz[r]) + sigma * mu;
-            }
+            for (int r = c.tid; r < c.m; r += WAVE) c.dsT[r] = -c.l2[r] - (c.dsv[r] * c.dz[r]) + sigma * mu;
         } else {
             // Prime.c:193-196: centring step with the previous factor
             sigma = sigma_d;
-            for (int r = c.tid; r < c.m; r += WAVE) {
-                double l = sqrt(c.s[r] * c.z[r]);
-                c.dsT[r] = -(l * l) + sigma * mu;
-            }
+            for (int r = c.tid; r < c.m; r += WAVE) c.dsT[r] = -c.l2[r] + sigma * mu;
         }
         __syncthreads();
-        for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.rz[r] - c.dsT[r] / c.z[r];
+        for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.rz[r] - c.dsT[r] * c.iz[r];
         __syncthreads();
-        newton_solve(c, c.rx, c.dz);
-        for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) / c.z[r];
-        __syncthreads();
+        STAMP_END(sb + 6);
+        newton_solve<NZM>(c, c.rx, c.dz);
+        STAMP_END(sb + 7);
+        for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) * c.iz[r];
         // dq = A'dy = rx - (P + hess + delta) dx - J' dz
         for (int v = c.tid; v < c.n; v += WAVE)
             c.tv[v] = c.rx[v] - (Pdiag(c, v) + hess_diag(c, v) + (c.nl ? delta : 0.0)) * c.dx[v];
         __syncthreads();
-        double ap = steplen(c, c.s, c.dsv), ad = steplen(c, c.z, c.dz);
+        double ap = steplen(c, c.is, c.dsv), ad = steplen(c, c.iz, c.dz);
         ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
         ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
         // tv - J'dz needs the dz of this step: apply before updating z (hess uses old z)
@@ -471,6 +577,7 @@ __device__ int ipm(Ctx &c, int maxit, int *iters)
         for (int v = c.tid; v < c.n; v += WAVE) { c.x[v] += c.dx[v] * ap; c.q[v] += c.tv[v] * ad; }
         for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] += c.dsv[r] * ap; c.z[r] += c.dz[r] * ad; }
         __syncthreads();
+        STAMP_END(sb + 8);
         it++;
     }
     *iters = it;
@@ -506,18 +613,27 @@ __device__ __forceinline__ int lambda_basis(const double *F, int C, int t, doubl
     return 0;
 }
 
+// (d, index) lexicographic wave argmin; every lane gets the winner
+__device__ __forceinline__ void wargmin(double &d, int &idx)
+{
+#pragma unroll
+    for (int o = 32; o > 0; o >>= 1) {
+        const double od = __shfl_xor(d, o, WAVE);
+        const int oi = __shfl_xor(idx, o, WAVE);
+        if (od < d || (od == d && oi < idx)) { d = od; idx = oi; }
+    }
+}
+
 // --------------------------------------------------------------------------- main kernel
-extern "C" __global__ void __launch_bounds__(WAVE)
-srb_nmpc_kernel(SrbKParams prm, int n_agents,
+template <int NZM>
+__device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
-                const double *__restrict__ obstacles, int n_obs,
+                const double *__restrict__ obstacles, const int *__restrict__ obs_idx,
                 const double *__restrict__ nbr_state, const int *__restrict__ nbr_idx,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
-                double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out)
+                double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
+                double *lds)
 {
-    extern __shared__ __attribute__((aligned(16))) double lds[];
-    const int agent = blockIdx.x;
-    if (agent >= n_agents) return;
     Ctx c;
     c.P = &prm; c.tid = threadIdx.x;
     c.N = prm.N; c.C = prm.C; c.K = prm.K_obs + prm.K_nbr;
@@ -534,19 +650,21 @@ srb_nmpc_kernel(SrbKParams prm, int n_agents,
     c.ref = p; p += 4 * N; c.foot = p; p += 2 * C * N; c.offv = p; p += 2 * (N - 1) + 3 * N;
     c.s = p; p += mmax; c.z = p; p += mmax; c.rz = p; p += mmax; c.dz = p; p += mmax;
     c.dsv = p; p += mmax; c.dsT = p; p += mmax; c.om = p; p += mmax; c.hvec = p; p += mmax;
+    c.iz = p; p += mmax; c.is = p; p += mmax; c.l2 = p; p += mmax;
     c.jc = p; p += 2 * N * K + 2; c.obs = p; p += 2 * N * K + 2; c.eps = p; p += K + 1;
     c.Hc = p; p += nz * nz; c.L = p; p += nz * nz; c.ZtZ = p; p += nz * nz; c.ZtZL = p; p += nz * nz;
+    c.dinv = p; p += nz; c.ZtZdinv = p; p += nz; c.xiv = p; p += nz;
 
+    STAMP_DECL
+    STAMP_BEGIN();
     // ---- load inputs (a1/a2/a3: x0, reference window, footholds)
     const double *x0 = x0g + 4 * (size_t)agent;
     for (int i = c.tid; i < 4 * N; i += WAVE) c.ref[i] = refg[(size_t)agent * 4 * N + i];
     for (int i = c.tid; i < 2 * C * N; i += WAVE) c.foot[i] = footg[(size_t)agent * 2 * C * N + i];
-    __syncthreads();
-    const double px = x0[0], py = x0[2];
-
-    // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
     for (int i = c.tid; i < n * nz; i += WAVE) c.Z[i] = 0.0;
     __syncthreads();
+
+    // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
     if (c.tid == 0) {
         double X[4] = {x0[0], x0[1], x0[2], x0[3]};
         for (int k = 0; k < N; k++) {
@@ -583,131 +701,109 @@ srb_nmpc_kernel(SrbKParams prm, int n_agents,
     if (c.tid == 0) c.Z[(n - 1) * nz + nz - 1] = 1.0;
     __syncthreads();
 
-    // =========================== QP stage (iSWIFT, Prime.c:35-230) ===========================
-    c.m = c.mq; c.nl = 0;
-    for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
-    for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0;     // kkt_initialize: -I block
-    __syncthreads();
-    int qp_flag = 3, qp_it = 0;
-    build_H(c, 0.0);
-    for (int i = c.tid; i < nz * nz; i += WAVE) c.L[i] = c.Hc[i];
-    __syncthreads();
-    if (chol_lds(c, c.L, nz) != 0) {
-        qp_flag = 1;
-    } else {
-        // r1 = -c - P xbar ; r3 = h - G xbar   ->  dx ; x = xbar + dx
-        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
-        for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.hvec[r] - row_dot(c, r, c.x);
-        __syncthreads();
-        for (int v = c.tid; v < n; v += WAVE) c.rx[v] = c.tv[v];
-        __syncthreads();
-        newton_solve(c, c.rx, c.dz);   // dz <- G x - h (z of the init system)
-        for (int v = c.tid; v < n; v += WAVE) c.x[v] += c.dx[v];
-        __syncthreads();
-        // q = A'y = -c - P x - G'(G x - h)
-        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
-        __syncthreads();
-        jt_apply(c, c.dz, c.q, c.tv, -1.0);
-        // s, z from z_inter = h - G x (Auxilary.c:716-746)
-        double mn = 1e300, mx = -1e300;
-        for (int r = c.tid; r < c.m; r += WAVE) {
-            double zi = c.hvec[r] - row_dot(c, r, c.x);
-            c.rz[r] = zi;
-            mn = fmin(mn, zi); mx = fmax(mx, zi);
+    STAMP_END(10);
+    // One loop over the two stages so that the interior-point iteration exists once in
+    // the code object (the solve is latency-bound; keeping the hot loop small keeps it in
+    // the instruction cache).  stage 0: QP (iSWIFT, Prime.c:35-230); stage 1: NLP
+    // (replaces SnoptSolver::Solve, MPC_dist.cpp:402-427), warm-started from stage 0.
+    int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
+    const int nstage = prm.use_nlp ? 2 : 1;
+#pragma clang loop unroll(disable)
+    for (int stage = 0; stage < nstage; stage++) {
+        if (stage == 0) {
+            c.m = c.mq; c.nl = 0;
+            for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
+            for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0;     // kkt_initialize: -I block
+            __syncthreads();
+            build_D(c, 0.0);
+            build_Hc(c, c.Hc, 0);
+            if (chol_reg<NZM>(c, c.Hc, c.L, c.dinv, nz, 1) != 0) { qp_flag = 1; continue; }
+            // r1 = -c - P xbar ; r3 = h - G xbar   ->  dx ; x = xbar + dx
+            for (int v = c.tid; v < n; v += WAVE) c.rx[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
+            for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.hvec[r] - row_dot(c, r, c.x);
+            __syncthreads();
+            newton_solve<NZM>(c, c.rx, c.dz);   // dz <- G x - h (z of the init system)
+            for (int v = c.tid; v < n; v += WAVE) c.x[v] += c.dx[v];
+            __syncthreads();
+            // q = A'y = -c - P x - G'(G x - h)
+            for (int v = c.tid; v < n; v += WAVE) c.tv[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
+            __syncthreads();
+            jt_apply(c, c.dz, c.q, c.tv, -1.0);
+            // s, z from z_inter = h - G x (Auxilary.c:716-746)
+            double mn = 1e300, mx = -1e300;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                double zi = c.hvec[r] - row_dot(c, r, c.x);
+                c.rz[r] = zi;
+                mn = fmin(mn, zi); mx = fmax(mx, zi);
+            }
+            mn = wmin(mn); mx = wmax(mx);
+            double ap = -mn, ad = mx;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                double zi = c.rz[r];
+                c.s[r] = (ap < 0) ? zi : zi + (1 + ap);
+                c.z[r] = (ad < 0) ? -zi : -zi + (1 + ad);
+            }
+            __syncthreads();
+            STAMP_END(11);
+        } else {
+            if (x_qp_out)
+                for (int v = c.tid; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = c.x[v];
+            c.nl = 1; c.m = mmax;
+            // obstacles per grid: K_obs nearest static (MPC_dist.cpp:371-396; srb_knn_kernel over
+            // the obstacle table) + K_nbr nearest agents predicted at constant velocity
+            for (int j = 0; j < K; j++) {
+                const bool st = j < prm.K_obs;
+                const int bi = st ? obs_idx[(size_t)agent * prm.K_obs + j] : nbr_idx[(size_t)agent * prm.K_nbr + (j - prm.K_obs)];
+                if (c.tid < N && bi >= 0) {
+                    const int k = c.tid;
+                    const double t = st ? 0.0 : prm.Ts * (k + 1);
+                    const double *srcp = st ? obstacles + 2 * (size_t)bi : nbr_state + 4 * (size_t)bi;
+                    c.obs[2 * (k * K + j)] = srcp[0] + (st ? 0.0 : srcp[2] * t);
+                    c.obs[2 * (k * K + j) + 1] = srcp[1] + (st ? 0.0 : srcp[3] * t);
+                }
+                if (c.tid == 0) c.eps[j] = st ? prm.eps_obs : prm.eps_nbr;
+            }
+            __syncthreads();
+            for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
+            __syncthreads();
+            obstacle_coefs(c);
+            // slacks: shifted h - g(x); duals 1
+            double mn = 1e300;
+            for (int r = c.tid; r < c.m; r += WAVE) {
+                c.rz[r] = c.hvec[r] - row_val(c, r);
+                mn = fmin(mn, c.rz[r]);
+            }
+            mn = wmin(mn);
+            double ap = -mn;
+            for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] = (ap < 0) ? c.rz[r] : c.rz[r] + (1 + ap); c.z[r] = 1.0; }
+            // Z'Z and its factor: projection for q0
+            build_Hc(c, c.ZtZ, 1);
+            chol_reg<NZM>(c, c.ZtZ, c.ZtZL, c.ZtZdinv, nz, 0);
+            // v = P x + c + J'z ; rx0 = -Z (Z'Z)^-1 Z' v ; q = -v - rx0
+            for (int v = c.tid; v < n; v += WAVE) c.tv[v] = Pdiag(c, v) * c.x[v] + cvec(c, v);
+            __syncthreads();
+            jt_apply(c, c.z, c.rx, c.tv, 1.0);
+            const double g = zt_mul<NZM>(c, c.rx);
+            const double t = chol_solve_reg(c, c.ZtZL, c.ZtZdinv, nz, g);
+            z_mul<NZM>(c, t, c.dx);
+            for (int v = c.tid; v < n; v += WAVE) c.q[v] = -c.rx[v] + c.dx[v];
+            __syncthreads();
+            STAMP_END(12);
         }
-        mn = wmin(mn); mx = -wmin(-mx);
-        double ap = -mn, ad = mx;
-        for (int r = c.tid; r < c.m; r += WAVE) {
-            double zi = c.rz[r];
-            c.s[r] = (ap < 0) ? zi : zi + (1 + ap);
-            c.z[r] = (ad < 0) ? -zi : -zi + (1 + ad);
-        }
-        __syncthreads();
-        qp_flag = ipm(c, prm.qp_maxit, &qp_it);
+        int it = 0;
+        const int f = ipm<NZM>(c, stage == 0 ? prm.qp_maxit : prm.nlp_maxit, &it);
+        if (stage == 0) { qp_flag = f; qp_it = it; } else { nlp_flag = f; nlp_it = it; }
+        STAMP_BEGIN();
     }
-    if (x_qp_out)
+    if (x_qp_out && nstage == 1)
         for (int v = c.tid; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = c.x[v];
-
-    // =========================== NLP stage (replaces SnoptSolver::Solve) ===========================
-    int nlp_flag = 0, nlp_it = 0;
-    if (prm.use_nlp) {
-        c.nl = 1; c.m = mmax;
-        // obstacle list per grid: K_obs nearest static (MPC_dist.cpp:371-396) + K_nbr neighbours
-        if (c.tid == 0) {
-            int chosen[SRB_MAX_K];
-            for (int j = 0; j < prm.K_obs; j++) {
-                double best = 1e300; int bi = -1;
-                for (int i = 0; i < n_obs; i++) {
-                    int used = 0;
-                    for (int t = 0; t < j; t++) used |= (chosen[t] == i);
-                    if (used) continue;
-                    double dx = px - obstacles[2 * i], dy = py - obstacles[2 * i + 1];
-                    double d = dx * dx + dy * dy;
-                    if (d < best) { best = d; bi = i; }
-                }
-                chosen[j] = bi;
-                c.eps[j] = prm.eps_obs;
-                for (int k = 0; k < N; k++) {
-                    c.obs[2 * (k * K + j)] = bi >= 0 ? obstacles[2 * bi] : 1e6;
-                    c.obs[2 * (k * K + j) + 1] = bi >= 0 ? obstacles[2 * bi + 1] : 1e6;
-                }
-            }
-            for (int j = 0; j < prm.K_nbr; j++) {
-                int bi = nbr_idx ? nbr_idx[(size_t)agent * prm.K_nbr + j] : -1;
-                c.eps[prm.K_obs + j] = prm.eps_nbr;
-                for (int k = 0; k < N; k++) {
-                    double t = prm.Ts * (k + 1);
-                    c.obs[2 * (k * K + prm.K_obs + j)] = bi >= 0 ? nbr_state[4 * (size_t)bi] + nbr_state[4 * (size_t)bi + 2] * t : 1e6;
-                    c.obs[2 * (k * K + prm.K_obs + j) + 1] = bi >= 0 ? nbr_state[4 * (size_t)bi + 1] + nbr_state[4 * (size_t)bi + 3] * t : 1e6;
-                }
-            }
-        }
-        __syncthreads();
-        for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
-        __syncthreads();
-        obstacle_coefs(c);
-        // slacks: shifted h - g(x); duals 1
-        double mn = 1e300;
-        for (int r = c.tid; r < c.m; r += WAVE) {
-            double g;
-            if (r >= c.rO && r < c.rV) {
-                int o = r - c.rO, k = o / K;
-                double dx = c.x[4 * k] - c.obs[2 * o], dy = c.x[4 * k + 2] - c.obs[2 * o + 1];
-                g = -(dx * dx + dy * dy) - c.x[n - 1];
-            } else g = row_dot(c, r, c.x);
-            c.rz[r] = c.hvec[r] - g;
-            mn = fmin(mn, c.rz[r]);
-        }
-        mn = wmin(mn);
-        double ap = -mn;
-        for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] = (ap < 0) ? c.rz[r] : c.rz[r] + (1 + ap); c.z[r] = 1.0; }
-        // Z'Z and its factor (projection for q0; inertia correction metric)
-        for (int pidx = c.tid; pidx < nz * nz; pidx += WAVE) {
-            int a = pidx / nz, b = pidx % nz;
-            double acc = 0;
-            for (int v = 0; v < n; v++) acc += c.Z[v * nz + a] * c.Z[v * nz + b];
-            c.ZtZ[pidx] = acc; c.ZtZL[pidx] = acc;
-        }
-        __syncthreads();
-        chol_lds(c, c.ZtZL, nz);
-        // v = P x + c + J'z ; rx0 = -Z (Z'Z)^-1 Z' v ; q = -v - rx0
-        for (int v = c.tid; v < n; v += WAVE) c.tv[v] = Pdiag(c, v) * c.x[v] + cvec(c, v);
-        __syncthreads();
-        jt_apply(c, c.z, c.rx, c.tv, 1.0);
-        double g = zt_mul(c, c.rx);
-        double t = chol_solve_reg(c, c.ZtZL, nz, g);
-        z_mul(c, t, c.dx);
-        for (int v = c.tid; v < n; v += WAVE) c.q[v] = -c.rx[v] + c.dx[v];
-        __syncthreads();
-        // the inertia-correction term delta*Z'Z is added inside build_H's caller via D (full-space delta I)
-        nlp_flag = ipm(c, prm.nlp_maxit, &nlp_it);
-    }
 
     // ---- outputs
     for (int v = c.tid; v < n; v += WAVE) x_out[(size_t)agent * n + v] = c.x[v];
     double f = 0;
     for (int v = c.tid; v < n; v += WAVE) f += 0.5 * Pdiag(c, v) * c.x[v] * c.x[v] + cvec(c, v) * c.x[v];
     f = wsum(f);
+    STAMP_END(13);
     if (c.tid == 0) {
         obj_out[agent] = f;
         status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
@@ -715,43 +811,75 @@ srb_nmpc_kernel(SrbKParams prm, int n_agents,
     }
 }
 
+#define SRB_NMPC_KERNEL(NAME, NZM)                                                                            \
+    extern "C" __global__ void __launch_bounds__(WAVE) NAME(                                                   \
+        SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
+        const double *__restrict__ footg, const double *__restrict__ obstacles, const int *__restrict__ obs_idx, \
+        const double *__restrict__ nbr_state, const int *__restrict__ nbr_idx, double *__restrict__ x_qp_out,   \
+        double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
+        int *__restrict__ iters_out)                                                                           \
+    {                                                                                                          \
+        extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
+        const int agent = blockIdx.x;                                                                          \
+        if (agent >= n_agents) return;                                                                         \
+        nmpc_agent<NZM>(prm, agent, x0g, refg, footg, obstacles, obs_idx, nbr_state, nbr_idx, x_qp_out, x_out, \
+                        obj_out, status_out, iters_out, lds);                                                  \
+    }
+
+SRB_NMPC_KERNEL(srb_nmpc_kernel_nz16, 16)
+SRB_NMPC_KERNEL(srb_nmpc_kernel_nz32, 32)
+SRB_NMPC_KERNEL(srb_nmpc_kernel_nz64, 64)
+
 // --------------------------------------------------------------------------- k nearest neighbours
-// One thread per agent; neighbour states streamed through LDS tiles.  Order: (d^2, index)
+// One thread per agent; table rows streamed through LDS tiles.  Order: (d^2, index)
 // ascending -- the order the reference's strict-'<' argmin scan produces (MPC_dist.cpp:373-382).
+// Used twice: static obstacles (table = Pobs_real columns, stride 2, no self) and other
+// agents (table = get_lastState() rows, stride 4, self = agent_offset + a excluded).
 // The query point is the agent's own current CoM from x0 (q[0], q[1] -- what the
-// reference's scan uses, MPC_dist.cpp:366), not its row of the neighbour table.
+// reference's scan uses, MPC_dist.cpp:366).
 extern "C" __global__ void __launch_bounds__(256)
 srb_knn_kernel(int n_agents, int agent_offset, const double *__restrict__ x0g, const double *__restrict__ state,
-               int n_all, int K, int *__restrict__ nbr_idx)
+               int stride, int n_all, int K, int *__restrict__ nbr_idx)
 {
     __shared__ double tile[1024 * 2];
     const int a = blockIdx.x * blockDim.x + threadIdx.x;
-    const int self = agent_offset + a;
+    const int self = (agent_offset >= 0) ? agent_offset + a : -1;
     double px = 0, py = 0;
     if (a < n_agents) { px = x0g[4 * (size_t)a]; py = x0g[4 * (size_t)a + 2]; }
-    double bd[SRB_MAX_K]; int bi[SRB_MAX_K];
-    for (int j = 0; j < SRB_MAX_K; j++) { bd[j] = 1e300; bi[j] = -1; }
+    // sorted top-K in registers: fixed-size compare-swap insertion chain (no dynamic indexing)
+    double bd[SRB_KNN_MAX]; int bi[SRB_KNN_MAX];
+#pragma unroll
+    for (int j = 0; j < SRB_KNN_MAX; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
+    double wd = 1e300; int wi = 0x7fffffff;        // current K-th best (admission threshold)
     for (int base = 0; base < n_all; base += 1024) {
         int cnt = n_all - base < 1024 ? n_all - base : 1024;
         __syncthreads();
         for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-            tile[2 * i] = state[4 * (size_t)(base + i)];
-            tile[2 * i + 1] = state[4 * (size_t)(base + i) + 1];
+            tile[2 * i] = state[(size_t)stride * (base + i)];
+            tile[2 * i + 1] = state[(size_t)stride * (base + i) + 1];
         }
         __syncthreads();
         if (a < n_agents)
             for (int i = 0; i < cnt; i++) {
                 int gi = base + i;
-                if (gi == self) continue;
                 double dx = px - tile[2 * i], dy = py - tile[2 * i + 1];
-                double d = dx * dx + dy * dy;
-                if (d < bd[K - 1] || (d == bd[K - 1] && gi < bi[K - 1])) {
-                    int j = K - 1;
-                    while (j > 0 && (d < bd[j - 1] || (d == bd[j - 1] && gi < bi[j - 1]))) { bd[j] = bd[j - 1]; bi[j] = bi[j - 1]; j--; }
-                    bd[j] = d; bi[j] = gi;
+                double d = (gi == self) ? 1e300 : dx * dx + dy * dy;
+                if (gi == self || !(d < wd || (d == wd && gi < wi))) continue;
+                double cd = d; int ci = gi;
+#pragma unroll
+                for (int j = 0; j < SRB_KNN_MAX; j++) {
+                    bool lt = (j < K) && (cd < bd[j] || (cd == bd[j] && ci < bi[j]));
+                    double td = bd[j]; int ti = bi[j];
+                    bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
+                    cd = lt ? td : cd; ci = lt ? ti : ci;
                 }
+#pragma unroll
+                for (int j = 0; j < SRB_KNN_MAX; j++)
+                    if (j == K - 1) { wd = bd[j]; wi = bi[j]; }
             }
     }
     if (a < n_agents)
-        for (int j = 0; j < K; j++) nbr_idx[(size_t)a * K + j] = bi[j];
+#pragma unroll
+        for (int j = 0; j < SRB_KNN_MAX; j++)
+            if (j < K) nbr_idx[(size_t)a * K + j] = (bi[j] == 0x7fffffff) ? -1 : bi[j];
 }
