@@ -100,7 +100,8 @@ int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, 
 int srb_sync(srb_ctx *ctx);
 
 /* Per-launch timing of the last srb_solve_batch_device call, measured with HIP events on
- * the stream the kernels ran on (ms): knn kernel, solve kernel. */
+ * the stream the kernel ran on (ms).  The nearest-obstacle selection is fused into the
+ * solve kernel, so knn_ms is always 0 (kept for ABI stability). */
 int srb_last_kernel_ms(srb_ctx *ctx, float *knn_ms, float *solve_ms);
 
 /* Dynamic LDS bytes one agent's workgroup uses (for occupancy reports). */

@@ -14,14 +14,12 @@
 
 #define DECL_NMPC(NAME)                                                                                       \
     extern "C" __global__ void NAME(SrbKParams prm, int n_agents, const double *x0g, const double *refg,      \
-                                    const double *footg, const double *obstacles, const int *obs_idx,          \
-                                    const double *nbr_state, const int *nbr_idx, double *x_qp_out,             \
+                                    const double *footg, const double *obstacles, int n_obs,                   \
+                                    const double *nbr_state, int n_all, int agent_offset, double *x_qp_out,    \
                                     double *x_out, double *obj_out, int *status_out, int *iters_out);
 DECL_NMPC(srb_nmpc_kernel_nz16)
 DECL_NMPC(srb_nmpc_kernel_nz32)
 DECL_NMPC(srb_nmpc_kernel_nz64)
-extern "C" __global__ void srb_knn_kernel(int n_agents, int agent_offset, const double *x0g, const double *state,
-                                          int stride, int n_all, int K, int *nbr_idx);
 
 static thread_local std::string g_err;
 
@@ -44,7 +42,7 @@ struct srb_ctx {
     hipEvent_t ev[4];
     // device staging
     double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj;
-    int *status, *iters, *nbr_idx, *obs_idx;
+    int *status, *iters;
     size_t cap_obs, cap_nbr;
     float knn_ms, solve_ms;
     bool timed;
@@ -110,8 +108,8 @@ static int validate(const srb_params *p)
 {
     if (!p) return fail(SRB_ERR_ARG, "null params");
     if (p->N < 2 || p->C < 2 || p->C > 4) return fail(SRB_ERR_ARG, "need N >= 2 and 2 <= C <= 4");
-    if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs + p->K_nbr > SRB_MAX_K || p->K_nbr > SRB_KNN_MAX)
-        return fail(SRB_ERR_ARG, "K_obs + K_nbr out of range (K_nbr <= 16, K_obs + K_nbr <= 32)");
+    if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs > SRB_KNN_MAX || p->K_nbr > SRB_KNN_MAX)
+        return fail(SRB_ERR_ARG, "K_obs, K_nbr out of range (each <= 16)");
     if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 64 (one xi entry per lane)");
     if ((6 + p->C) * p->N + 1 > SRB_MAX_NV) return fail(SRB_ERR_SIZE, "nv exceeds 256");
     SrbKParams k = make_kparams(p, p->use_nlp);
@@ -137,7 +135,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     srb_ctx *c = new srb_ctx();
     c->p = *p; c->max_agents = max_agents; c->device = device;
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false;
-    const int N = p->N, C = p->C, nv = srb_nv(p), Kn = p->K_nbr > 0 ? p->K_nbr : 1;
+    const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
@@ -149,8 +147,6 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->obj, A * sizeof(double)));
     HIPCHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
-    HIPCHK(hipMalloc(&c->nbr_idx, A * Kn * sizeof(int)));
-    HIPCHK(hipMalloc(&c->obs_idx, A * (p->K_obs > 0 ? p->K_obs : 1) * sizeof(int)));
     *out = c;
     return SRB_OK;
 }
@@ -160,7 +156,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->nbr_idx, c->obs_idx, c->obstacles, c->nbr};
+    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -187,34 +183,20 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
     const size_t lds = (size_t)srb_lds_doubles(k) * sizeof(double);
     HIPCHK(hipSetDevice(c->device));
-    const int *nbr_idx = nullptr;
+    const int n_obs = k.K_obs > 0 ? d->n_obs : 0, n_all = k.K_nbr > 0 ? d->n_all : 0;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
-    dim3 kblk(256), kgrd((n_agents + 255) / 256);
-    if (use_nlp && k.K_obs > 0) {       // K_obs nearest static obstacles (MPC_dist.cpp:371-396)
-        hipLaunchKernelGGL(srb_knn_kernel, kgrd, kblk, 0, s, n_agents, -1, d->x0, d->obstacles, 2, d->n_obs,
-                           k.K_obs, c->obs_idx);
-        HIPCHK(hipGetLastError());
-    }
-    if (use_nlp && k.K_nbr > 0) {       // K_nbr nearest other agents
-        hipLaunchKernelGGL(srb_knn_kernel, kgrd, kblk, 0, s, n_agents, d->agent_offset, d->x0, d->nbr_state, 4,
-                           d->n_all, k.K_nbr, c->nbr_idx);
-        HIPCHK(hipGetLastError());
-        nbr_idx = c->nbr_idx;
-    }
-    HIPCHK(hipEventRecord(c->ev[1], s));
-    // kernel instance by the register-resident bound on nz (one row of Z'HZ per lane)
-    if (k.nz <= 16)
-        hipLaunchKernelGGL(srb_nmpc_kernel_nz16, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
-                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
-    else if (k.nz <= 32)
-        hipLaunchKernelGGL(srb_nmpc_kernel_nz32, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
-                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
-    else
-        hipLaunchKernelGGL(srb_nmpc_kernel_nz64, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot,
-                           d->obstacles, c->obs_idx, d->nbr_state, nbr_idx, d->x_qp, d->x, d->obj, d->status, d->iters);
+    // one launch: nearest-obstacle selection, QP stage and NLP stage per agent; kernel
+    // instance by the register-resident bound on nz (one row of Z'HZ per lane)
+#define SRB_LAUNCH(KERN)                                                                                        \
+    hipLaunchKernelGGL(KERN, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,  \
+                       n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters)
+    if (k.nz <= 16) SRB_LAUNCH(srb_nmpc_kernel_nz16);
+    else if (k.nz <= 32) SRB_LAUNCH(srb_nmpc_kernel_nz32);
+    else SRB_LAUNCH(srb_nmpc_kernel_nz64);
+#undef SRB_LAUNCH
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[2], s));
+    HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
 }
 
@@ -236,11 +218,10 @@ extern "C" int srb_sync(srb_ctx *c)
 extern "C" int srb_last_kernel_ms(srb_ctx *c, float *knn_ms, float *solve_ms)
 {
     if (!c || !c->timed) return fail(SRB_ERR_ARG, "no timed launch");
-    HIPCHK(hipEventSynchronize(c->ev[2]));
-    float a = 0, b = 0;
-    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[1]));
-    HIPCHK(hipEventElapsedTime(&b, c->ev[1], c->ev[2]));
-    if (knn_ms) *knn_ms = a;
+    HIPCHK(hipEventSynchronize(c->ev[1]));
+    float b = 0;
+    HIPCHK(hipEventElapsedTime(&b, c->ev[0], c->ev[1]));
+    if (knn_ms) *knn_ms = 0.0f;         // selection is fused into the solve kernel
     if (solve_ms) *solve_ms = b;
     return SRB_OK;
 }
@@ -339,13 +320,13 @@ extern "C" void srb_fit_bezier(const double buf[4], const double *X, double alph
 extern "C" const char *srb_last_error(void) { return g_err.c_str(); }
 
 #ifdef SRB_STAMPS
-extern __device__ unsigned long long srb_stamp_buf[32];
+extern __device__ unsigned long long srb_stamp_buf[64];
 extern "C" int srb_debug_stamps(unsigned long long *out, int reset)
 {
     HIPCHK(hipDeviceSynchronize());
-    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_stamp_buf), sizeof(unsigned long long) * 32));
+    HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_stamp_buf), sizeof(unsigned long long) * 64));
     if (reset) {
-        unsigned long long z[32] = {0};
+        unsigned long long z[64] = {0};
         HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(srb_stamp_buf), z, sizeof z));
     }
     return SRB_OK;

@@ -16,11 +16,22 @@ struct SrbKParams {
     double eps_obs, eps_nbr, vsat, tol, Ts;
 };
 
+// Z'HZ layout helpers: Z is n8 x ldz (rows to a multiple of 8, columns to a multiple of
+// 16, zero padded); SRB_NCPL2 = both orientations of every off-diagonal coupling of H.
+#define SRB_R8(x) ((((x) + 7) / 8) * 8)
+#define SRB_LDZ(nz) ((((nz) + 15) / 16) * 16)
+#define SRB_NCPL2(N) (2 * (2 * ((N) - 1) + 3 * (N)))
+
 // doubles of dynamic LDS one agent needs; must match the carve in srb_nmpc_kernel
 static inline int srb_lds_doubles(const SrbKParams &p)
 {
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n = p.n, nz = p.nz;
     const int mmax = p.use_nlp ? (p.mq + N * K + 4 * N) : p.mq;
-    return n * nz + 6 * n + 4 * N + 2 * C * N + (2 * (N - 1) + 3 * N) + 11 * mmax +
-           (2 * N * K + 2) * 2 + (K + 1) + 4 * nz * nz + 3 * nz;
+    const int cpl8 = SRB_R8(SRB_NCPL2(N));
+    return SRB_R8(n) * SRB_LDZ(nz) + 5 * n + SRB_R8(n) + 2 * cpl8 + 4 * N + 2 * C * N + 11 * mmax +
+           (2 * N * K + 2) * 2 + (K + 1) + 2 * nz * nz + 3 * nz + 64
+#ifdef SRB_STAMPS
+           + 64
+#endif
+        ;
 }

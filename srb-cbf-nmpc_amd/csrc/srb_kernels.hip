@@ -34,25 +34,44 @@
 #define WAVE 64
 
 // --------------------------------------------------------------------------- wave helpers
-__device__ __forceinline__ double wsum(double v)
+// Cross-lane traffic stays in the VALU: DPP row permutations for the 16-lane rows and
+// gfx950's v_permlane16/32_swap across rows (no LDS round trips, unlike __shfl_xor, which
+// lowers to ds_bpermute).  Every lane ends with the bit-identical result (each stage
+// combines a pair with a commutative op), so branches on it stay wave-uniform.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v += __shfl_xor(v, o, WAVE);
-    return v;
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
-__device__ __forceinline__ double wmin(double v)
+// the two halves of a permlane swap of v with itself: {v, partner} in some order
+template <int W>
+__device__ __forceinline__ void swap_d(double v, double &a, double &b)
 {
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v = fmin(v, __shfl_xor(v, o, WAVE));
-    return v;
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto l = (W == 16) ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false) : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h = (W == 16) ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false) : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0]));
+    b = __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]));
 }
-__device__ __forceinline__ double wmax(double v) { return -wmin(-v); }
-__device__ __forceinline__ int wor(int v)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) v |= __shfl_xor(v, o, WAVE);
-    return v;
-}
+#define SRB_WAVE_REDUCE(NAME, OP)                                                  \
+    __device__ __forceinline__ double NAME(double v)                               \
+    {                                                                              \
+        v = OP(v, dpp_d<0xB1>(v));   /* quad_perm [1,0,3,2] */                     \
+        v = OP(v, dpp_d<0x4E>(v));   /* quad_perm [2,3,0,1] */                     \
+        v = OP(v, dpp_d<0x141>(v));  /* row_half_mirror     */                     \
+        v = OP(v, dpp_d<0x140>(v));  /* row_mirror          */                     \
+        double a, b;                                                               \
+        swap_d<16>(v, a, b); v = OP(a, b);                                         \
+        swap_d<32>(v, a, b); return OP(a, b);                                      \
+    }
+__device__ __forceinline__ double op_add(double a, double b) { return a + b; }
+SRB_WAVE_REDUCE(wsum, op_add)
+SRB_WAVE_REDUCE(wmin, fmin)
+SRB_WAVE_REDUCE(wmax, fmax)
 // value of lane `lane` (wave-uniform index, SGPR) -> wave-uniform value
 __device__ __forceinline__ double readlane_d(double v, int lane)
 {
@@ -62,31 +81,56 @@ __device__ __forceinline__ double readlane_d(double v, int lane)
     return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
 }
 
+// 1/x and 1/sqrt(x) from the hardware estimates (v_rcp_f64 / v_rsq_f64) refined by two
+// Newton steps: within an ulp or two of the IEEE results, a handful of FMAs instead of
+// the ~12-instruction division / square-root sequences.
+__device__ __forceinline__ double rcp_d(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+}
+__device__ __forceinline__ double rsq_d(double x)
+{
+    double r = __builtin_amdgcn_rsq(x);
+    r = fma(0.5 * r, fma(-x * r, r, 1.0), r);
+    r = fma(0.5 * r, fma(-x * r, r, 1.0), r);
+    return r;
+}
+
 // --------------------------------------------------------------------------- diagnostic stamps
 // Built only with -DSRB_STAMPS (make stamps -> srbnmpc/libsrbnmpc_stamps.so): lane 0 of
-// agent 0 accumulates s_memtime cycles per phase into a buffer nothing else reads.
+// every agent accumulates s_memtime cycles per phase into LDS (fire-and-forget
+// ds_add_u64); agent 0 adds them to a device buffer nothing else reads at the end.
 #ifdef SRB_STAMPS
-__device__ unsigned long long srb_stamp_buf[32];
-#define STAMP_DECL unsigned long long _st_t0 = 0; const bool _st_on = (blockIdx.x == 0 && threadIdx.x == 0);
-#define STAMP_BEGIN() do { __builtin_amdgcn_sched_barrier(0); _st_t0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
-#define STAMP_END(slot) do { __builtin_amdgcn_sched_barrier(0); unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0); if (_st_on) srb_stamp_buf[slot] += _t - _st_t0; _st_t0 = _t; } while (0)
+#define SRB_NSTAMP 64
+__device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
+#define STAMP_BEGIN(c) do { __builtin_amdgcn_sched_barrier(0); (c).st_t0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
+#define STAMP_END(c, slot) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
+    __builtin_amdgcn_sched_barrier(0); if ((c).tid == 0) atomicAdd(&(c).stamps[slot], _t - (c).st_t0); (c).st_t0 = _t; } while (0)
 #else
-#define STAMP_DECL
-#define STAMP_BEGIN() do {} while (0)
-#define STAMP_END(slot) do {} while (0)
+#define STAMP_BEGIN(c) do {} while (0)
+#define STAMP_END(c, slot) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- per-agent context
 struct Ctx {
     const SrbKParams *P;
     int N, C, K, n, nz, mq, m, nl;          // nl: NLP rows/terms active
+    int ldz, n8;                            // Z: n8 rows (zero beyond n) x ldz columns (zero beyond nz)
     int rFm, rXp, rXm, rUp, rUm, rLlo, rLhi, rO, rV;
     // LDS arrays
-    double *Z, *x, *q, *rx, *dx, *tv, *D, *ref, *foot, *offv;
+    double *Z, *x, *q, *rx, *dx, *tv, *D, *ref, *foot;
     double *s, *z, *rz, *dz, *dsv, *dsT, *om, *iz, *is, *l2, *jc, *obs, *eps;
     double *Hc, *L, *dinv, *ZtZ, *ZtZL, *ZtZdinv, *hvec, *xiv;
+    double *bc;                             // 64-entry broadcast scratch (chol_reg)
+    int2 *term;                             // Z'HZ term table: (u*nz, w*nz) per term (see build_Hc)
     int tid;
+#ifdef SRB_STAMPS
+    unsigned long long *stamps;
+    mutable unsigned long long st_t0;
+#endif
 };
 
 __device__ __forceinline__ int col_stage(const Ctx &c, int a) { return (a == c.nz - 1) ? c.N : a / (c.C - 1); }
@@ -206,8 +250,9 @@ __device__ __forceinline__ double row_val(const Ctx &c, int r)
 }
 
 // --------------------------------------------------------------------------- Z'HZ assembly
-// D (diag of H), friction couplings offv[0..2N-3], obstacle couplings per grid
-// (xy, xs, ys) at offv[2N-2 + 3k].  H = P + hess + delta I + J' diag(om) J.
+// Values of the Z'HZ terms (term_table order): D[0..n) = diag of H, then both orientations
+// of the friction couplings and (NLP) the per-grid obstacle couplings (xy, xs, ys).
+// H = P + hess + delta I + J' diag(om) J.
 __device__ __forceinline__ void build_D(const Ctx &c, double delta)
 {
     const int N = c.N, n = c.n;
@@ -240,8 +285,10 @@ __device__ __forceinline__ void build_D(const Ctx &c, double delta)
         for (int o = c.tid; o < N * c.K; o += WAVE) ps += c.om[c.rO + o];
     ps = wsum(ps);
     if (c.tid == 0) c.D[n - 1] = Pdiag(c, n - 1) + delta + ps;
+    // off-diagonal terms: both orientations of each coupling (see term_table)
+    double *hc = c.D + c.n8;
     const int nf = 2 * (N - 1);
-    for (int e = c.tid; e < nf; e += WAVE) c.offv[e] = -(c.om[e] + c.om[c.rFm + e]);
+    for (int e = c.tid; e < nf; e += WAVE) { const double v = -(c.om[e] + c.om[c.rFm + e]); hc[2 * e] = v; hc[2 * e + 1] = v; }
     if (c.nl)
         for (int k = c.tid; k < N; k += WAVE) {
             double xy = 0, xs = 0, ys = 0;
@@ -250,126 +297,186 @@ __device__ __forceinline__ void build_D(const Ctx &c, double delta)
                 double w = c.om[c.rO + o], jx = c.jc[2 * o], jy = c.jc[2 * o + 1];
                 xy += w * jx * jy; xs -= w * jx; ys -= w * jy;
             }
-            c.offv[nf + 3 * k] = xy; c.offv[nf + 3 * k + 1] = xs; c.offv[nf + 3 * k + 2] = ys;
+            double *t = hc + 2 * (nf + 3 * k);
+            t[0] = xy; t[1] = xy; t[2] = xs; t[3] = xs; t[4] = ys; t[5] = ys;
         }
     __syncthreads();
 }
 
-// out[a][b] = (Z' H Z)[a][b] from the structurally nonzero terms only:
-//   lambda columns of grid j touch X rows of grids >= j, the U/lambda rows of grid j;
-//   a friction coupling (X_i pos, U_{i+1}) links columns of grids <= i and i+1;
-//   the s column touches only s and (NLP) the obstacle couplings.
-// unit != 0: H = I (gives Z'Z).
+// Z'HZ as a sum of rank-1 terms  sum_t h_t Z[u_t,:]' Z[w_t,:]  over the nonzeros of H:
+//   diagonal terms       (u, w) = (v, v),  h = D[v]            (v < n8; Z rows >= n are 0)
+//   coupling terms       each coupling (u, w) of H twice, (u, w) and (w, u), h = H_uw:
+//                          friction row e = 2i+d: X_i pos d  <->  U_{i+1} d
+//                          (NLP) grid k: x_k <-> y_k, x_k <-> s, y_k <-> s
+// The coupling table holds the Z row offsets (u*ldz, w*ldz), padded to a multiple of 8
+// with (0, 0); h lives in D[n8 + e] (build_D; padding stays 0).  Built once.
+__device__ __forceinline__ void term_table(const Ctx &c)
+{
+    const int N = c.N, n = c.n, ldz = c.ldz, nf = 2 * (N - 1);
+    const int ncpl2 = SRB_NCPL2(N), cpl8 = SRB_R8(ncpl2);
+    for (int t = c.tid; t < cpl8; t += WAVE) {
+        int u = 0, w = 0;
+        if (t < ncpl2) {
+            const int e = t >> 1;
+            if (e < nf) { const int i = e >> 1, d = e & 1; u = 4 * i + 2 * d; w = 4 * N + 2 * (i + 1) + d; }
+            else {
+                const int o = e - nf, k = o / 3, r = o - 3 * k;
+                u = (r == 2) ? 4 * k + 2 : 4 * k;
+                w = (r == 0) ? 4 * k + 2 : n - 1;
+            }
+            if (t & 1) { const int tmp = u; u = w; w = tmp; }
+        }
+        c.term[t] = make_int2(u * ldz, w * ldz);
+    }
+    __syncthreads();
+}
+
+typedef double srb_d4 __attribute__((ext_vector_type(4)));
+
+// out = Z' H Z (nz x nz, row-major in LDS) on the matrix cores: v_mfma_f64_16x16x4_f64
+// with A[a][t] = h_t Z[u_t][a], B[t][b] = Z[w_t][b], four terms per instruction
+// (lane l supplies term t0 + (l >> 4), column l & 15).  Z and the term lists are
+// zero-padded (rows to n8, columns to ldz, couplings to a multiple of 8), so the loops
+// are branch-free with unconditional LDS loads; two accumulator chains per tile keep
+// consecutive MFMAs independent.  16x16 output tiles, upper triangle of tiles computed
+// and mirrored.  unit != 0: H = I (gives Z'Z).
+template <int NZM>
 __device__ __forceinline__ void build_Hc(const Ctx &c, double *out, int unit)
 {
-    const int N = c.N, n = c.n, nz = c.nz, C = c.C, nf = 2 * (N - 1);
-    const double *Z = c.Z, *D = c.D, *off = c.offv;
-    const int npair = nz * (nz + 1) / 2;
-    for (int pidx = c.tid; pidx < npair; pidx += WAVE) {
-        int b = (int)((sqrt(8.0 * pidx + 1.0) - 1.0) * 0.5);
-        while (b * (b + 1) / 2 > pidx) b--;
-        while ((b + 1) * (b + 2) / 2 <= pidx) b++;
-        const int a = pidx - b * (b + 1) / 2;          // a <= b, so stage(a) <= stage(b)
-        const int ja = col_stage(c, a), jb = col_stage(c, b);
-        double acc0 = 0.0, acc1 = 0.0, acc2 = 0.0, acc3 = 0.0;
-        if (jb < N) {
-            // X rows of grids >= jb: 4 independent accumulators (one per state component)
-            for (int k = jb; k < N; k++) {
-                const int v = 4 * k;
-                const double d0 = unit ? 1.0 : D[v], d1 = unit ? 1.0 : D[v + 1];
-                const double d2 = unit ? 1.0 : D[v + 2], d3 = unit ? 1.0 : D[v + 3];
-                acc0 += d0 * Z[v * nz + a] * Z[v * nz + b];
-                acc1 += d1 * Z[(v + 1) * nz + a] * Z[(v + 1) * nz + b];
-                acc2 += d2 * Z[(v + 2) * nz + a] * Z[(v + 2) * nz + b];
-                acc3 += d3 * Z[(v + 3) * nz + a] * Z[(v + 3) * nz + b];
-                if (c.nl && !unit) {
-                    const double xa = Z[v * nz + a], ya = Z[(v + 2) * nz + a];
-                    const double xb = Z[v * nz + b], yb = Z[(v + 2) * nz + b];
-                    acc1 += off[nf + 3 * k] * (xa * yb + ya * xb);
+    constexpr int T = NZM / 16;
+    const int nz = c.nz, ldz = c.ldz, n8 = c.n8, li = c.tid & 15, kq = c.tid >> 4;
+    const int cpl8 = unit ? 0 : SRB_R8(2 * (2 * (c.N - 1) + (c.nl ? 3 * c.N : 0)));
+    const int Tn = ldz >> 4;
+    const double *Z = c.Z, *D = c.D, *Dc = c.D + n8;
+#pragma unroll
+    for (int ta = 0; ta < T; ta++) {
+        if (ta >= Tn) break;
+        srb_d4 acc0[T], acc1[T];
+#pragma unroll
+        for (int tb = 0; tb < T; tb++) { acc0[tb] = srb_d4{0.0, 0.0, 0.0, 0.0}; acc1[tb] = acc0[tb]; }
+        const int ca = 16 * ta + li;
+#pragma unroll 2
+        for (int t0 = 0; t0 < n8; t0 += 8) {                 // diagonal terms
+            const int v0 = t0 + kq, v1 = t0 + 4 + kq;
+            const double h0 = unit ? 1.0 : D[v0], h1 = unit ? 1.0 : D[v1];
+            const double a0 = h0 * Z[v0 * ldz + ca], a1 = h1 * Z[v1 * ldz + ca];
+#pragma unroll
+            for (int tb = 0; tb < T; tb++)
+                if (tb >= ta && tb < Tn) {
+                    const int cb = 16 * tb + li;
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, Z[v0 * ldz + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, Z[v1 * ldz + cb], acc1[tb], 0, 0, 0);
+                }
+        }
+#pragma unroll 2
+        for (int e0 = 0; e0 < cpl8; e0 += 8) {               // coupling terms
+            const int2 uw0 = c.term[e0 + kq], uw1 = c.term[e0 + 4 + kq];
+            const double a0 = Dc[e0 + kq] * Z[uw0.x + ca], a1 = Dc[e0 + 4 + kq] * Z[uw1.x + ca];
+#pragma unroll
+            for (int tb = 0; tb < T; tb++)
+                if (tb >= ta && tb < Tn) {
+                    const int cb = 16 * tb + li;
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, Z[uw0.y + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, Z[uw1.y + cb], acc1[tb], 0, 0, 0);
+                }
+        }
+        // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
+#pragma unroll
+        for (int tb = 0; tb < T; tb++)
+            if (tb >= ta && tb < Tn) {
+                const int col = 16 * tb + li;
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = 16 * ta + kq + 4 * r;
+                    const double v = acc0[tb][r] + acc1[tb][r];
+                    if (row < nz && col < nz) { out[row * nz + col] = v; out[col * nz + row] = v; }
                 }
             }
-            if (ja == jb) {
-                for (int v = 4 * N + 2 * ja; v < 4 * N + 2 * ja + 2; v++)
-                    acc2 += (unit ? 1.0 : D[v]) * Z[v * nz + a] * Z[v * nz + b];
-                for (int v = 6 * N + C * ja; v < 6 * N + C * ja + C; v++)
-                    acc3 += (unit ? 1.0 : D[v]) * Z[v * nz + a] * Z[v * nz + b];
-            } else if (!unit) {
-                const int i = jb - 1;                 // friction rows between grid i pos and grid jb CoP
-                for (int d = 0; d < 2; d++)
-                    acc0 += off[2 * i + d] * Z[(4 * i + 2 * d) * nz + a] * Z[(4 * N + 2 * jb + d) * nz + b];
-            }
-        } else if (ja < N) {
-            if (c.nl && !unit)
-                for (int k = ja; k < N; k++)
-                    acc0 += off[nf + 3 * k + 1] * Z[(4 * k) * nz + a] + off[nf + 3 * k + 2] * Z[(4 * k + 2) * nz + a];
-        } else {
-            acc0 = unit ? 1.0 : D[n - 1];
-        }
-        const double acc = (acc0 + acc1) + (acc2 + acc3);
-        out[a * nz + b] = acc;
-        out[b * nz + a] = acc;
     }
     __syncthreads();
 }
 
 // --------------------------------------------------------------------------- register Cholesky
-// Lane i holds row i of the trailing matrix in a register window row[0..NZM-1] that
-// shifts left by one column per elimination step, so the pivot column is always row[0]
-// and every register index is a compile-time constant while the step loop over k stays
-// a runtime loop (small code: one copy of an NZM-wide body).  Cross-lane operands move
-// by v_readlane with a wave-uniform lane index.  Writes L (lower, LDS) and 1/L_kk.
-// regularise != 0 mirrors iSWIFT's dynamic pivot regularisation (ldl.c:320-321:
-// |D_kk| <= 1e-14 -> 1e-7) for the QP stage.  Returns 0 on success (wave-uniform).
+// Right-looking Cholesky of the nz x nz SPD matrix H, lane i = row i held in registers
+// row[0..NZM) (the k loop is unrolled, so every register index is static).  Step k: the
+// pivot comes from lane k by v_readlane, each lane forms its multiplier l_i = L[i][k],
+// the column is broadcast through LDS (bc: one write per lane, same-address reads), and
+// the trailing rows are updated in place.  The eliminated column k of lane i > k keeps
+// l_i.  At the end lane i holds, in row[]:
+//     row[k] = L[i][k]            for k < i
+//     row[k] = A_i[i][k]          for k > i  (row i of the step-i Schur complement,
+//                                             = L[k][i] / inv_i, i.e. column i of L)
+// so both triangular solves run from the lane's own registers.  row[] goes to LDS
+// (Lr, row-major, stride nz) with inv_i = 1/L_ii in dinv.  regularise != 0 mirrors
+// iSWIFT's dynamic pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7) for
+// the QP stage.  Returns 0 on success (wave-uniform).  Lr may alias H.
 template <int NZM>
-__device__ __forceinline__ int chol_reg(const Ctx &c, const double *H, double *L, double *dinv, int nz, int regularise)
+__device__ __forceinline__ int chol_reg(const Ctx &c, const double *H, double *Lr, double *dinv, int nz, int regularise)
 {
     const int i = c.tid;
     double row[NZM];
 #pragma unroll
     for (int j = 0; j < NZM; j++) row[j] = (i < nz && j < nz) ? H[i * nz + j] : 0.0;
+    __syncthreads();
+    double myinv = 0.0;
     int fail = 0;
-#pragma clang loop unroll(disable)
-    for (int k = 0; k < nz; k++) {
-        double piv = readlane_d(row[0], k);
-        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
-        if (!(piv > 0.0)) { fail = 1; break; }
-        const double d = sqrt(piv), inv = 1.0 / d;
-        const double l = (i > k && i < nz) ? row[0] * inv : 0.0;
-        if (i > k && i < nz) L[i * nz + k] = l;
-        if (i == k) { L[k * nz + k] = d; dinv[k] = inv; }
 #pragma unroll
-        for (int t = 1; t < NZM; t++) {
-            const double lj = readlane_d(l, (k + t) & (WAVE - 1));   // lanes <= k hold l = 0
-            row[t - 1] = row[t] - l * lj;
-        }
-        row[NZM - 1] = 0.0;
+    for (int k = 0; k < NZM; k++) {
+        if (k >= nz || fail) continue;  // (no break: it would block the full unroll)
+        double piv = readlane_d(row[k], k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        if (!(piv > 0.0)) { fail = 1; continue; }
+        const double inv = rsq_d(piv);
+        const double l = (i > k && i < nz) ? row[k] * inv : 0.0;
+        if (i == k) myinv = inv;
+        c.bc[i] = l;
+        __syncthreads();
+#pragma unroll
+        for (int j = k + 1; j < NZM; j++) row[j] = fma(-l, c.bc[j], row[j]);
+        if (i > k) row[k] = l;
+        __syncthreads();                // bc is rewritten next step
+    }
+    if (i < nz) {
+#pragma unroll
+        for (int j = 0; j < NZM; j++)
+            if (j < nz) Lr[i * nz + j] = row[j];
+        dinv[i] = myinv;
     }
     __syncthreads();
     return fail;
 }
 
 // (L L') x = b with b one entry per lane (lane i < nz); returns x in the same layout.
-// Runtime loops; the L operand of step k+1 is loaded while step k completes.
-__device__ __forceinline__ double chol_solve_reg(const Ctx &c, const double *L, const double *dinv, int nz, double b)
+// Forward:  y_k = b_k inv_k after all updates of lanes < k, then b_i -= L[i][k] y_k.
+// Backward: x_k = inv_k (y_k - inv_k acc_k), acc_i += A_i[i][k] x_k  (L[k][i] = inv_i A_i[i][k]).
+// Lanes that already hold their final value keep it via the select.
+template <int NZM>
+__device__ __forceinline__ double chol_solve_reg(const Ctx &c, const double *Lr, const double *dinv, int nz, double b)
 {
     const int i = c.tid;
-    double lnext = (i > 0 && i < nz) ? L[i * nz] : 0.0;
-#pragma clang loop unroll(disable)
-    for (int k = 0; k < nz; k++) {
-        const double lik = lnext;
-        lnext = (k + 1 < nz && i > k + 1 && i < nz) ? L[i * nz + k + 1] : 0.0;
-        const double yk = readlane_d(b, k) * dinv[k];
-        b = (i == k) ? yk : b - lik * yk;
+    double row[NZM];
+#pragma unroll
+    for (int j = 0; j < NZM; j++) row[j] = (i < nz && j < nz) ? Lr[i * nz + j] : 0.0;
+    const double inv = (i < nz) ? dinv[i] : 0.0;
+    double y = 0.0;
+#pragma unroll
+    for (int k = 0; k < NZM; k++) {
+        if (k >= nz) continue;
+        const double t = b * inv;
+        const double yk = readlane_d(t, k);
+        if (i == k) y = t;
+        b = fma(-row[k], yk, b);         // lanes > k: L[i][k]; lanes <= k: final already
     }
-    lnext = (nz - 1 > i) ? L[(nz - 1) * nz + i] : 0.0;
-#pragma clang loop unroll(disable)
-    for (int k = nz - 1; k >= 0; k--) {
-        const double lki = lnext;
-        lnext = (k >= 1 && k - 1 > i) ? L[(k - 1) * nz + i] : 0.0;
-        const double xk = readlane_d(b, k) * dinv[k];
-        b = (i == k) ? xk : b - lki * xk;
+    double acc = 0.0, x = 0.0;
+#pragma unroll
+    for (int k = NZM - 1; k >= 0; k--) {
+        if (k >= nz) continue;
+        const double t = inv * fma(-inv, acc, y);
+        const double xk = readlane_d(t, k);
+        if (i == k) x = t;
+        acc = fma(row[k], xk, acc);      // lanes < k: A_i[i][k]; lanes >= k: final already
     }
-    return b;
+    return x;
 }
 
 // xi-vector (one entry per lane) = Z' v.  Lanes (a, d) = (4a + d) sum the X rows of state
@@ -390,15 +497,15 @@ __device__ __forceinline__ double zt_mul(const Ctx &c, const double *v)
                 double a0 = 0.0, a1 = 0.0;
                 int k = ja;
                 for (; k + 1 < N; k += 2) {
-                    a0 += c.Z[(4 * k + d) * nz + a] * v[4 * k + d];
-                    a1 += c.Z[(4 * (k + 1) + d) * nz + a] * v[4 * (k + 1) + d];
+                    a0 += c.Z[(4 * k + d) * c.ldz + a] * v[4 * k + d];
+                    a1 += c.Z[(4 * (k + 1) + d) * c.ldz + a] * v[4 * (k + 1) + d];
                 }
-                if (k < N) a0 += c.Z[(4 * k + d) * nz + a] * v[4 * k + d];
+                if (k < N) a0 += c.Z[(4 * k + d) * c.ldz + a] * v[4 * k + d];
                 acc = a0 + a1;
                 if (d == 0) {
-                    for (int r = 4 * N + 2 * ja; r < 4 * N + 2 * ja + 2; r++) acc += c.Z[r * nz + a] * v[r];
+                    for (int r = 4 * N + 2 * ja; r < 4 * N + 2 * ja + 2; r++) acc += c.Z[r * c.ldz + a] * v[r];
                 } else if (d == 1) {
-                    for (int r = 6 * N + C * ja; r < 6 * N + C * ja + C; r++) acc += c.Z[r * nz + a] * v[r];
+                    for (int r = 6 * N + C * ja; r < 6 * N + C * ja + C; r++) acc += c.Z[r * c.ldz + a] * v[r];
                 }
             } else if (d == 0) {
                 acc = v[c.n - 1];
@@ -429,13 +536,13 @@ __device__ __forceinline__ void z_mul(const Ctx &c, double xi, double *out)
             const int lim = ((v >> 2) + 1) * (C - 1);     // columns of grids <= k
             int a = 0;
             for (; a + 1 < lim; a += 2) {
-                a0 += c.Z[v * nz + a] * xs[a];
-                a1 += c.Z[v * nz + a + 1] * xs[a + 1];
+                a0 += c.Z[v * c.ldz + a] * xs[a];
+                a1 += c.Z[v * c.ldz + a + 1] * xs[a + 1];
             }
-            if (a < lim) a0 += c.Z[v * nz + a] * xs[a];
+            if (a < lim) a0 += c.Z[v * c.ldz + a] * xs[a];
         } else if (v < n - 1) {
             const int j = (v < 6 * N) ? (v - 4 * N) >> 1 : (v - 6 * N) / C;
-            for (int a = j * (C - 1); a < (j + 1) * (C - 1); a++) a0 += c.Z[v * nz + a] * xs[a];
+            for (int a = j * (C - 1); a < (j + 1) * (C - 1); a++) a0 += c.Z[v * c.ldz + a] * xs[a];
         } else {
             a0 = xs[nz - 1];
         }
@@ -448,17 +555,22 @@ __device__ __forceinline__ void z_mul(const Ctx &c, double xi, double *out)
 //   [H A' J'; A 0 0; J 0 -W][dx;dy;dz] = [r1; 0; r3], W^-1 = om
 // r1 (n) given, r3 in r3dz on entry (overwritten with dz).  dx -> c.dx.  Uses c.tv, c.dsv.
 template <int NZM>
-__device__ __forceinline__ void newton_solve(const Ctx &c, const double *r1, double *r3dz)
+__device__ __forceinline__ void newton_solve(const Ctx &c, const double *r1, double *r3dz, int sslot)
 {
     double *w = c.dsv;                      // scratch m-vector (callers recompute dsv after)
     for (int r = c.tid; r < c.m; r += WAVE) w[r] = c.om[r] * r3dz[r];
     __syncthreads();
     jt_apply(c, w, c.tv, r1, 1.0);
+    STAMP_END(c, sslot + 0);
     const double g = zt_mul<NZM>(c, c.tv);
-    const double xi = chol_solve_reg(c, c.L, c.dinv, c.nz, g);
+    STAMP_END(c, sslot + 1);
+    const double xi = chol_solve_reg<NZM>(c, c.L, c.dinv, c.nz, g);
+    STAMP_END(c, sslot + 2);
     z_mul<NZM>(c, xi, c.dx);
+    STAMP_END(c, sslot + 3);
     for (int r = c.tid; r < c.m; r += WAVE) r3dz[r] = c.om[r] * (row_dot(c, r, c.dx) - r3dz[r]);
     __syncthreads();
+    STAMP_END(c, sslot + 4);
 }
 
 // findsteplength (Auxilary.c:271-294): min over dv_r < 0 of -v_r/dv_r, 1 when no dv_r < 0.
@@ -482,10 +594,12 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
     const double sigma_d = 0.0;
     int flag = 2, it = 0;
     double delta = 0.0;
-    STAMP_DECL
-    const int sb = c.nl ? 16 : 0;       // stamp slots: QP 0..15, NLP 16..31
+    const int sb = c.nl ? 32 : 0;       // stamp slots: QP 0..17, NLP 32..49 (tools/stamps.py)
     for (int iter = 0; iter < maxit; iter++) {
-        STAMP_BEGIN();
+        // Opaque lane id per iteration: per-lane addresses are recomputed inside the loop
+        // instead of being hoisted out of it and held in registers for its whole length.
+        asm volatile("" : "+v"(c.tid));
+        STAMP_BEGIN(c);
         if (c.nl) obstacle_coefs(c);
         // rz = h - s - g(x); tv = -(P x + c) - q
         for (int r = c.tid; r < c.m; r += WAVE) c.rz[r] = c.hvec[r] - c.s[r] - row_val(c, r);
@@ -500,37 +614,38 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
         for (int r = c.tid; r < c.m; r += WAVE) {
             const double sr = c.s[r], zr = c.z[r];
             nrz += c.rz[r] * c.rz[r]; sz += sr * zr;
-            const double l = sqrt(sr * zr), l2 = l * l;     // formlambda, lambda.*lambda
+            const double l2 = sr * zr;                        // formlambda then lambda.*lambda
             c.l2[r] = l2; mu += l2;
-            c.iz[r] = 1.0 / zr; c.is[r] = 1.0 / sr;
+            c.iz[r] = rcp_d(zr); c.is[r] = rcp_d(sr);
         }
         nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz); mu = wsum(mu) / c.m;
         if (c.nl) gm = wmax(gm);
-        STAMP_END(sb + 0);
+        STAMP_END(c, sb + 0);
         if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
         // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
         const double thx = c.nl ? th * gm : th;
         if (nrx < thx && nrz < th && sz / c.m < tol) { flag = 0; break; }
         const int pc = c.nl || (sigma > sigma_d);
         if (pc) {
-            // weights W^-1 = 1/(s/z) (updatekktmatrix, Auxilary.c:197-205) and factor
-            for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0 / (c.s[r] / c.z[r]);
+            // weights W^-1 = z/s (updatekktmatrix, Auxilary.c:197-205) and factor
+            for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = c.z[r] * c.is[r];
             __syncthreads();
-            STAMP_END(sb + 1);
+            STAMP_END(c, sb + 1);
             delta = 0.0;
             double dstart = 0.0;
             int ok = 0;
             for (int tries = 0; tries < (c.nl ? 14 : 1); tries++) {
                 build_D(c, delta);
-                build_Hc(c, c.Hc, 0);
-                STAMP_END(sb + 2);
+                STAMP_END(c, sb + 2);
+                build_Hc<NZM>(c, c.Hc, 0);
+                STAMP_END(c, sb + 3);
                 if (tries == 0) {       // scale-aware first shift: 1e-10 * max(1, max diag of Z'HZ)
                     double dm = 1.0;
                     for (int a = c.tid; a < c.nz; a += WAVE) dm = fmax(dm, c.Hc[a * c.nz + a]);
                     dstart = 1e-10 * wmax(dm);
                 }
                 int cf = chol_reg<NZM>(c, c.Hc, c.L, c.dinv, c.nz, !c.nl);
-                STAMP_END(sb + 3);
+                STAMP_END(c, sb + 4);
                 if (cf == 0) { ok = 1; break; }
                 delta = (delta == 0.0) ? dstart : delta * 10.0;
             }
@@ -541,9 +656,8 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
                 c.dz[r] = c.rz[r] - c.dsT[r] * c.iz[r];
             }
             __syncthreads();
-            STAMP_END(sb + 4);
-            newton_solve<NZM>(c, c.rx, c.dz);
-            STAMP_END(sb + 5);
+            STAMP_END(c, sb + 5);
+            newton_solve<NZM>(c, c.rx, c.dz, sb + 6);
             for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) * c.iz[r];
             __syncthreads();
             double ap = steplen(c, c.is, c.dsv), ad = steplen(c, c.iz, c.dz);
@@ -561,9 +675,8 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
         __syncthreads();
         for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.rz[r] - c.dsT[r] * c.iz[r];
         __syncthreads();
-        STAMP_END(sb + 6);
-        newton_solve<NZM>(c, c.rx, c.dz);
-        STAMP_END(sb + 7);
+        STAMP_END(c, sb + 11);
+        newton_solve<NZM>(c, c.rx, c.dz, sb + 12);
         for (int r = c.tid; r < c.m; r += WAVE) c.dsv[r] = (c.dsT[r] - c.s[r] * c.dz[r]) * c.iz[r];
         // dq = A'dy = rx - (P + hess + delta) dx - J' dz
         for (int v = c.tid; v < c.n; v += WAVE)
@@ -577,7 +690,7 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
         for (int v = c.tid; v < c.n; v += WAVE) { c.x[v] += c.dx[v] * ap; c.q[v] += c.tv[v] * ad; }
         for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] += c.dsv[r] * ap; c.z[r] += c.dz[r] * ad; }
         __syncthreads();
-        STAMP_END(sb + 8);
+        STAMP_END(c, sb + 17);
         it++;
     }
     *iters = it;
@@ -624,12 +737,54 @@ __device__ __forceinline__ void wargmin(double &d, int &idx)
     }
 }
 
+// K nearest rows of a table (row i at tab[stride*i], x at +0, y at +1) to (px, py),
+// ascending in (d^2, index) -- the order of the reference's strict-'<' scan
+// (MPC_dist.cpp:373-382) -- excluding row `self`; indices to sel[0..K).  The wave scans
+// the table once: every lane keeps a sorted top-K of its own rows (visited in increasing
+// index, so a strict '<' keeps the lower index on ties), then K rounds of a wave argmin
+// over the lane heads pop the global order.  Rows stream from L2 coalesced across lanes.
+__device__ __forceinline__ void knn_select(const Ctx &c, double px, double py, const double *__restrict__ tab,
+                                           int stride, int n_rows, int self, int K, int *sel)
+{
+    double bd[SRB_KNN_MAX]; int bi[SRB_KNN_MAX];
+#pragma unroll
+    for (int j = 0; j < SRB_KNN_MAX; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
+    double wd = 1e300;                                  // this lane's K-th best (admission threshold)
+    for (int i = c.tid; i < n_rows; i += WAVE) {
+        const double dx = tab[(size_t)stride * i] - px, dy = tab[(size_t)stride * i + 1] - py;
+        const double d = dx * dx + dy * dy;
+        if (i == self || !(d < wd)) continue;
+        double cd = d; int ci = i;
+#pragma unroll
+        for (int j = 0; j < SRB_KNN_MAX; j++) {
+            const bool lt = (j < K) && (cd < bd[j]);
+            const double td = bd[j]; const int ti = bi[j];
+            bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
+            cd = lt ? td : cd; ci = lt ? ti : ci;
+        }
+#pragma unroll
+        for (int j = 0; j < SRB_KNN_MAX; j++)
+            if (j == K - 1) wd = bd[j];
+    }
+#pragma clang loop unroll(disable)
+    for (int j = 0; j < K; j++) {
+        double d = bd[0]; int idx = bi[0];
+        wargmin(d, idx);
+        if (bi[0] == idx) {                             // the owning lane pops its head
+#pragma unroll
+            for (int t = 0; t + 1 < SRB_KNN_MAX; t++) { bd[t] = bd[t + 1]; bi[t] = bi[t + 1]; }
+            bd[SRB_KNN_MAX - 1] = 1e300; bi[SRB_KNN_MAX - 1] = 0x7fffffff;
+        }
+        if (c.tid == 0) sel[j] = (idx == 0x7fffffff) ? -1 : idx;
+    }
+}
+
 // --------------------------------------------------------------------------- main kernel
 template <int NZM>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
-                const double *__restrict__ obstacles, const int *__restrict__ obs_idx,
-                const double *__restrict__ nbr_state, const int *__restrict__ nbr_idx,
+                const double *__restrict__ obstacles, int n_obs,
+                const double *__restrict__ nbr_state, int n_all, int agent_offset,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
                 double *lds)
@@ -645,23 +800,33 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     const int mmax = prm.use_nlp ? (c.mq + N * K + 4 * N) : c.mq;
     // carve LDS (offsets must match srb_lds_doubles())
     double *p = lds;
-    c.Z = p; p += n * nz;
-    c.x = p; p += n; c.q = p; p += n; c.rx = p; p += n; c.dx = p; p += n; c.tv = p; p += n; c.D = p; p += n;
-    c.ref = p; p += 4 * N; c.foot = p; p += 2 * C * N; c.offv = p; p += 2 * (N - 1) + 3 * N;
+    c.ldz = SRB_LDZ(nz); c.n8 = SRB_R8(n);
+    const int cpl8 = SRB_R8(SRB_NCPL2(N));
+    c.Z = p; p += c.n8 * c.ldz;
+    c.x = p; p += n; c.q = p; p += n; c.rx = p; p += n; c.dx = p; p += n; c.tv = p; p += n;
+    c.D = p; p += c.n8 + cpl8; c.term = (int2 *)p; p += cpl8;
+    c.ref = p; p += 4 * N; c.foot = p; p += 2 * C * N;
     c.s = p; p += mmax; c.z = p; p += mmax; c.rz = p; p += mmax; c.dz = p; p += mmax;
     c.dsv = p; p += mmax; c.dsT = p; p += mmax; c.om = p; p += mmax; c.hvec = p; p += mmax;
     c.iz = p; p += mmax; c.is = p; p += mmax; c.l2 = p; p += mmax;
     c.jc = p; p += 2 * N * K + 2; c.obs = p; p += 2 * N * K + 2; c.eps = p; p += K + 1;
-    c.Hc = p; p += nz * nz; c.L = p; p += nz * nz; c.ZtZ = p; p += nz * nz; c.ZtZL = p; p += nz * nz;
+    // the factor overwrites the assembled matrix (chol_reg holds all rows in registers first)
+    c.Hc = p; c.L = p; p += nz * nz; c.ZtZ = p; c.ZtZL = p; p += nz * nz;
     c.dinv = p; p += nz; c.ZtZdinv = p; p += nz; c.xiv = p; p += nz;
+    c.bc = p; p += WAVE;
+#ifdef SRB_STAMPS
+    c.stamps = (unsigned long long *)p; p += SRB_NSTAMP;
+    c.stamps[c.tid] = 0;
+    __syncthreads();
+#endif
 
-    STAMP_DECL
-    STAMP_BEGIN();
+    STAMP_BEGIN(c);
     // ---- load inputs (a1/a2/a3: x0, reference window, footholds)
     const double *x0 = x0g + 4 * (size_t)agent;
     for (int i = c.tid; i < 4 * N; i += WAVE) c.ref[i] = refg[(size_t)agent * 4 * N + i];
     for (int i = c.tid; i < 2 * C * N; i += WAVE) c.foot[i] = footg[(size_t)agent * 2 * C * N + i];
-    for (int i = c.tid; i < n * nz; i += WAVE) c.Z[i] = 0.0;
+    for (int i = c.tid; i < c.n8 * c.ldz; i += WAVE) c.Z[i] = 0.0;
+    for (int i = c.tid; i < c.n8 + cpl8; i += WAVE) c.D[i] = 0.0;      // padding terms stay 0
     __syncthreads();
 
     // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
@@ -686,22 +851,23 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         double g0 = 0.0, g1 = 0.0;
         if (!is_null)
             for (int i = 0; i < C; i++) { g0 += c.foot[(j * 2 + 0) * C + i] * lam[i]; g1 += c.foot[(j * 2 + 1) * C + i] * lam[i]; }
-        for (int i = 0; i < C; i++) c.Z[(6 * N + C * j + i) * nz + col] = lam[i];
-        c.Z[(4 * N + 2 * j) * nz + col] = g0;
-        c.Z[(4 * N + 2 * j + 1) * nz + col] = g1;
+        for (int i = 0; i < C; i++) c.Z[(6 * N + C * j + i) * c.ldz + col] = lam[i];
+        c.Z[(4 * N + 2 * j) * c.ldz + col] = g0;
+        c.Z[(4 * N + 2 * j + 1) * c.ldz + col] = g1;
         double v[4];
         for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1;
         for (int k = j; k < N; k++) {
-            for (int d = 0; d < 4; d++) c.Z[(4 * k + d) * nz + col] = v[d];
+            for (int d = 0; d < 4; d++) c.Z[(4 * k + d) * c.ldz + col] = v[d];
             double tt[4];
             for (int d = 0; d < 4; d++) tt[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3];
             for (int d = 0; d < 4; d++) v[d] = tt[d];
         }
     }
-    if (c.tid == 0) c.Z[(n - 1) * nz + nz - 1] = 1.0;
+    if (c.tid == 0) c.Z[(n - 1) * c.ldz + nz - 1] = 1.0;
     __syncthreads();
+    term_table(c);
 
-    STAMP_END(10);
+    STAMP_END(c, 28);
     // One loop over the two stages so that the interior-point iteration exists once in
     // the code object (the solve is latency-bound; keeping the hot loop small keeps it in
     // the instruction cache).  stage 0: QP (iSWIFT, Prime.c:35-230); stage 1: NLP
@@ -710,19 +876,20 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     const int nstage = prm.use_nlp ? 2 : 1;
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
+        asm volatile("" : "+v"(c.tid));     // see ipm()
         if (stage == 0) {
             c.m = c.mq; c.nl = 0;
             for (int r = c.tid; r < c.m; r += WAVE) c.hvec[r] = row_h(c, r);
             for (int r = c.tid; r < c.m; r += WAVE) c.om[r] = 1.0;     // kkt_initialize: -I block
             __syncthreads();
             build_D(c, 0.0);
-            build_Hc(c, c.Hc, 0);
+            build_Hc<NZM>(c, c.Hc, 0);
             if (chol_reg<NZM>(c, c.Hc, c.L, c.dinv, nz, 1) != 0) { qp_flag = 1; continue; }
             // r1 = -c - P xbar ; r3 = h - G xbar   ->  dx ; x = xbar + dx
             for (int v = c.tid; v < n; v += WAVE) c.rx[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
             for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.hvec[r] - row_dot(c, r, c.x);
             __syncthreads();
-            newton_solve<NZM>(c, c.rx, c.dz);   // dz <- G x - h (z of the init system)
+            newton_solve<NZM>(c, c.rx, c.dz, 20);   // dz <- G x - h (z of the init system)
             for (int v = c.tid; v < n; v += WAVE) c.x[v] += c.dx[v];
             __syncthreads();
             // q = A'y = -c - P x - G'(G x - h)
@@ -744,16 +911,26 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 c.z[r] = (ad < 0) ? -zi : -zi + (1 + ad);
             }
             __syncthreads();
-            STAMP_END(11);
+            STAMP_END(c, 29);
         } else {
             if (x_qp_out)
                 for (int v = c.tid; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = c.x[v];
             c.nl = 1; c.m = mmax;
-            // obstacles per grid: K_obs nearest static (MPC_dist.cpp:371-396; srb_knn_kernel over
-            // the obstacle table) + K_nbr nearest agents predicted at constant velocity
+            // obstacles per grid: the K_obs nearest static obstacles (MPC_dist.cpp:371-396,
+            // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
+            // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
+            int *sel = (int *)c.jc;                     // scratch until obstacle_coefs
+#pragma clang loop unroll(disable)
+            for (int tsel = 0; tsel < 2; tsel++) {
+                const int Kt = tsel ? prm.K_nbr : prm.K_obs;
+                if (Kt > 0)
+                    knn_select(c, x0[0], x0[2], tsel ? nbr_state : obstacles, tsel ? 4 : 2, tsel ? n_all : n_obs,
+                               tsel ? agent_offset + agent : -1, Kt, sel + (tsel ? prm.K_obs : 0));
+            }
+            __syncthreads();
             for (int j = 0; j < K; j++) {
                 const bool st = j < prm.K_obs;
-                const int bi = st ? obs_idx[(size_t)agent * prm.K_obs + j] : nbr_idx[(size_t)agent * prm.K_nbr + (j - prm.K_obs)];
+                const int bi = sel[j];
                 if (c.tid < N && bi >= 0) {
                     const int k = c.tid;
                     const double t = st ? 0.0 : prm.Ts * (k + 1);
@@ -777,23 +954,23 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             double ap = -mn;
             for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] = (ap < 0) ? c.rz[r] : c.rz[r] + (1 + ap); c.z[r] = 1.0; }
             // Z'Z and its factor: projection for q0
-            build_Hc(c, c.ZtZ, 1);
+            build_Hc<NZM>(c, c.ZtZ, 1);
             chol_reg<NZM>(c, c.ZtZ, c.ZtZL, c.ZtZdinv, nz, 0);
             // v = P x + c + J'z ; rx0 = -Z (Z'Z)^-1 Z' v ; q = -v - rx0
             for (int v = c.tid; v < n; v += WAVE) c.tv[v] = Pdiag(c, v) * c.x[v] + cvec(c, v);
             __syncthreads();
             jt_apply(c, c.z, c.rx, c.tv, 1.0);
             const double g = zt_mul<NZM>(c, c.rx);
-            const double t = chol_solve_reg(c, c.ZtZL, c.ZtZdinv, nz, g);
+            const double t = chol_solve_reg<NZM>(c, c.ZtZL, c.ZtZdinv, nz, g);
             z_mul<NZM>(c, t, c.dx);
             for (int v = c.tid; v < n; v += WAVE) c.q[v] = -c.rx[v] + c.dx[v];
             __syncthreads();
-            STAMP_END(12);
+            STAMP_END(c, 30);
         }
         int it = 0;
         const int f = ipm<NZM>(c, stage == 0 ? prm.qp_maxit : prm.nlp_maxit, &it);
         if (stage == 0) { qp_flag = f; qp_it = it; } else { nlp_flag = f; nlp_it = it; }
-        STAMP_BEGIN();
+        STAMP_BEGIN(c);
     }
     if (x_qp_out && nstage == 1)
         for (int v = c.tid; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = c.x[v];
@@ -803,7 +980,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double f = 0;
     for (int v = c.tid; v < n; v += WAVE) f += 0.5 * Pdiag(c, v) * c.x[v] * c.x[v] + cvec(c, v) * c.x[v];
     f = wsum(f);
-    STAMP_END(13);
+    STAMP_END(c, 31);
+#ifdef SRB_STAMPS
+    if (agent == 0) atomicAdd(&srb_stamp_buf[c.tid], c.stamps[c.tid]);
+#endif
     if (c.tid == 0) {
         obj_out[agent] = f;
         status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
@@ -814,72 +994,19 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 #define SRB_NMPC_KERNEL(NAME, NZM)                                                                            \
     extern "C" __global__ void __launch_bounds__(WAVE) NAME(                                                   \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
-        const double *__restrict__ footg, const double *__restrict__ obstacles, const int *__restrict__ obs_idx, \
-        const double *__restrict__ nbr_state, const int *__restrict__ nbr_idx, double *__restrict__ x_qp_out,   \
+        const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
+        const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
         int *__restrict__ iters_out)                                                                           \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        nmpc_agent<NZM>(prm, agent, x0g, refg, footg, obstacles, obs_idx, nbr_state, nbr_idx, x_qp_out, x_out, \
+        nmpc_agent<NZM>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset,       \
+                        x_qp_out, x_out,                                                                       \
                         obj_out, status_out, iters_out, lds);                                                  \
     }
 
 SRB_NMPC_KERNEL(srb_nmpc_kernel_nz16, 16)
 SRB_NMPC_KERNEL(srb_nmpc_kernel_nz32, 32)
 SRB_NMPC_KERNEL(srb_nmpc_kernel_nz64, 64)
-
-// --------------------------------------------------------------------------- k nearest neighbours
-// One thread per agent; table rows streamed through LDS tiles.  Order: (d^2, index)
-// ascending -- the order the reference's strict-'<' argmin scan produces (MPC_dist.cpp:373-382).
-// Used twice: static obstacles (table = Pobs_real columns, stride 2, no self) and other
-// agents (table = get_lastState() rows, stride 4, self = agent_offset + a excluded).
-// The query point is the agent's own current CoM from x0 (q[0], q[1] -- what the
-// reference's scan uses, MPC_dist.cpp:366).
-extern "C" __global__ void __launch_bounds__(256)
-srb_knn_kernel(int n_agents, int agent_offset, const double *__restrict__ x0g, const double *__restrict__ state,
-               int stride, int n_all, int K, int *__restrict__ nbr_idx)
-{
-    __shared__ double tile[1024 * 2];
-    const int a = blockIdx.x * blockDim.x + threadIdx.x;
-    const int self = (agent_offset >= 0) ? agent_offset + a : -1;
-    double px = 0, py = 0;
-    if (a < n_agents) { px = x0g[4 * (size_t)a]; py = x0g[4 * (size_t)a + 2]; }
-    // sorted top-K in registers: fixed-size compare-swap insertion chain (no dynamic indexing)
-    double bd[SRB_KNN_MAX]; int bi[SRB_KNN_MAX];
-#pragma unroll
-    for (int j = 0; j < SRB_KNN_MAX; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
-    double wd = 1e300; int wi = 0x7fffffff;        // current K-th best (admission threshold)
-    for (int base = 0; base < n_all; base += 1024) {
-        int cnt = n_all - base < 1024 ? n_all - base : 1024;
-        __syncthreads();
-        for (int i = threadIdx.x; i < cnt; i += blockDim.x) {
-            tile[2 * i] = state[(size_t)stride * (base + i)];
-            tile[2 * i + 1] = state[(size_t)stride * (base + i) + 1];
-        }
-        __syncthreads();
-        if (a < n_agents)
-            for (int i = 0; i < cnt; i++) {
-                int gi = base + i;
-                double dx = px - tile[2 * i], dy = py - tile[2 * i + 1];
-                double d = (gi == self) ? 1e300 : dx * dx + dy * dy;
-                if (gi == self || !(d < wd || (d == wd && gi < wi))) continue;
-                double cd = d; int ci = gi;
-#pragma unroll
-                for (int j = 0; j < SRB_KNN_MAX; j++) {
-                    bool lt = (j < K) && (cd < bd[j] || (cd == bd[j] && ci < bi[j]));
-                    double td = bd[j]; int ti = bi[j];
-                    bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
-                    cd = lt ? td : cd; ci = lt ? ti : ci;
-                }
-#pragma unroll
-                for (int j = 0; j < SRB_KNN_MAX; j++)
-                    if (j == K - 1) { wd = bd[j]; wi = bi[j]; }
-            }
-    }
-    if (a < n_agents)
-#pragma unroll
-        for (int j = 0; j < SRB_KNN_MAX; j++)
-            if (j < K) nbr_idx[(size_t)a * K + j] = (bi[j] == 0x7fffffff) ? -1 : bi[j];
-}
