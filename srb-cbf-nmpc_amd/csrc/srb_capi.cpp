@@ -19,7 +19,6 @@
                                     double *x_out, double *obj_out, int *status_out, int *iters_out);
 DECL_NMPC(srb_nmpc_kernel_nz16)
 DECL_NMPC(srb_nmpc_kernel_nz32)
-DECL_NMPC(srb_nmpc_kernel_nz64)
 
 static thread_local std::string g_err;
 
@@ -110,7 +109,7 @@ static int validate(const srb_params *p)
     if (p->N < 2 || p->C < 2 || p->C > 4) return fail(SRB_ERR_ARG, "need N >= 2 and 2 <= C <= 4");
     if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs > SRB_KNN_MAX || p->K_nbr > SRB_KNN_MAX)
         return fail(SRB_ERR_ARG, "K_obs, K_nbr out of range (each <= 16)");
-    if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 64 (one xi entry per lane)");
+    if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 32 (reduced Newton system bound)");
     if ((6 + p->C) * p->N + 1 > SRB_MAX_NV) return fail(SRB_ERR_SIZE, "nv exceeds 256");
     SrbKParams k = make_kparams(p, p->use_nlp);
     if ((size_t)srb_lds_doubles(k) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
@@ -192,8 +191,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     hipLaunchKernelGGL(KERN, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,  \
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters)
     if (k.nz <= 16) SRB_LAUNCH(srb_nmpc_kernel_nz16);
-    else if (k.nz <= 32) SRB_LAUNCH(srb_nmpc_kernel_nz32);
-    else SRB_LAUNCH(srb_nmpc_kernel_nz64);
+    else SRB_LAUNCH(srb_nmpc_kernel_nz32);
 #undef SRB_LAUNCH
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));

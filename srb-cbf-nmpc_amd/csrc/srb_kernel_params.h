@@ -3,7 +3,7 @@
 
 #define SRB_MAX_K 32      // obstacle rows per grid (K_obs + K_nbr)
 #define SRB_KNN_MAX 16    // neighbours per agent (K_nbr)
-#define SRB_MAX_N 64      // lanes of one wave hold one xi entry each: nz = N(C-1)+1 <= 64
+#define SRB_MAX_N 32      // reduced Newton system size bound: nz = N(C-1)+1 <= 32
 #define SRB_MAX_OBS 4096  // static obstacles (64 lanes x 64-bit chosen mask)
 #define SRB_MAX_NV 256    // z_mul keeps 4 variables per lane
 
@@ -16,9 +16,9 @@ struct SrbKParams {
     double eps_obs, eps_nbr, vsat, tol, Ts;
 };
 
-// Z'HZ layout helpers: Z is n8 x ldz (rows to a multiple of 8, columns to a multiple of
+// Z'HZ layout helpers: Z is n16 x ldz (rows to a multiple of 16, columns to a multiple of
 // 16, zero padded); SRB_NCPL2 = both orientations of every off-diagonal coupling of H.
-#define SRB_R8(x) ((((x) + 7) / 8) * 8)
+#define SRB_R16(x) ((((x) + 15) / 16) * 16)     /* term lists: whole 16-term MFMA trips */
 #define SRB_LDZ(nz) ((((nz) + 15) / 16) * 16)
 #define SRB_NCPL2(N) (2 * (2 * ((N) - 1) + 3 * (N)))
 
@@ -27,9 +27,9 @@ static inline int srb_lds_doubles(const SrbKParams &p)
 {
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n = p.n, nz = p.nz;
     const int mmax = p.use_nlp ? (p.mq + N * K + 4 * N) : p.mq;
-    const int cpl8 = SRB_R8(SRB_NCPL2(N));
-    return SRB_R8(n) * SRB_LDZ(nz) + 5 * n + SRB_R8(n) + 2 * cpl8 + 4 * N + 2 * C * N + 11 * mmax +
-           (2 * N * K + 2) * 2 + (K + 1) + 2 * nz * nz + 3 * nz + 64
+    const int cpl16 = SRB_R16(SRB_NCPL2(N));
+    return SRB_R16(n) * SRB_LDZ(nz) + 5 * n + SRB_R16(n) + 2 * cpl16 + 4 * N + 2 * C * N + 11 * mmax +
+           (2 * N * K + 2) * 2 + (K + 1) + 4 * nz * nz + 6 * 64
 #ifdef SRB_STAMPS
            + 64
 #endif

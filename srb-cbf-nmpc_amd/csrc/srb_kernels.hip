@@ -118,13 +118,13 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 struct Ctx {
     const SrbKParams *P;
     int N, C, K, n, nz, mq, m, nl;          // nl: NLP rows/terms active
-    int ldz, n8;                            // Z: n8 rows (zero beyond n) x ldz columns (zero beyond nz)
+    int ldz, n16;                            // Z: n16 rows (zero beyond n) x ldz columns (zero beyond nz)
     int rFm, rXp, rXm, rUp, rUm, rLlo, rLhi, rO, rV;
     // LDS arrays
     double *Z, *x, *q, *rx, *dx, *tv, *D, *ref, *foot;
     double *s, *z, *rz, *dz, *dsv, *dsT, *om, *iz, *is, *l2, *jc, *obs, *eps;
-    double *Hc, *L, *dinv, *ZtZ, *ZtZL, *ZtZdinv, *hvec, *xiv;
-    double *bc;                             // 64-entry broadcast scratch (chol_reg)
+    double *Hc, *L, *ZtZ, *ZtZL, *hvec, *xiv, *gbuf;   // L, ZtZL: inverses of Hc, ZtZ
+    double *bc;                             // 4 x 64 broadcast scratch (gj_inverse)
     int2 *term;                             // Z'HZ term table: (u*nz, w*nz) per term (see build_Hc)
     int tid;
 #ifdef SRB_STAMPS
@@ -286,7 +286,7 @@ __device__ __forceinline__ void build_D(const Ctx &c, double delta)
     ps = wsum(ps);
     if (c.tid == 0) c.D[n - 1] = Pdiag(c, n - 1) + delta + ps;
     // off-diagonal terms: both orientations of each coupling (see term_table)
-    double *hc = c.D + c.n8;
+    double *hc = c.D + c.n16;
     const int nf = 2 * (N - 1);
     for (int e = c.tid; e < nf; e += WAVE) { const double v = -(c.om[e] + c.om[c.rFm + e]); hc[2 * e] = v; hc[2 * e + 1] = v; }
     if (c.nl)
@@ -304,17 +304,17 @@ __device__ __forceinline__ void build_D(const Ctx &c, double delta)
 }
 
 // Z'HZ as a sum of rank-1 terms  sum_t h_t Z[u_t,:]' Z[w_t,:]  over the nonzeros of H:
-//   diagonal terms       (u, w) = (v, v),  h = D[v]            (v < n8; Z rows >= n are 0)
+//   diagonal terms       (u, w) = (v, v),  h = D[v]            (v < n16; Z rows >= n are 0)
 //   coupling terms       each coupling (u, w) of H twice, (u, w) and (w, u), h = H_uw:
 //                          friction row e = 2i+d: X_i pos d  <->  U_{i+1} d
 //                          (NLP) grid k: x_k <-> y_k, x_k <-> s, y_k <-> s
-// The coupling table holds the Z row offsets (u*ldz, w*ldz), padded to a multiple of 8
-// with (0, 0); h lives in D[n8 + e] (build_D; padding stays 0).  Built once.
+// The coupling table holds the Z row offsets (u*ldz, w*ldz), padded to a multiple of 16
+// with (0, 0); h lives in D[n16 + e] (build_D; padding stays 0).  Built once.
 __device__ __forceinline__ void term_table(const Ctx &c)
 {
     const int N = c.N, n = c.n, ldz = c.ldz, nf = 2 * (N - 1);
-    const int ncpl2 = SRB_NCPL2(N), cpl8 = SRB_R8(ncpl2);
-    for (int t = c.tid; t < cpl8; t += WAVE) {
+    const int ncpl2 = SRB_NCPL2(N), cpl16 = SRB_R16(ncpl2);
+    for (int t = c.tid; t < cpl16; t += WAVE) {
         int u = 0, w = 0;
         if (t < ncpl2) {
             const int e = t >> 1;
@@ -336,7 +336,7 @@ typedef double srb_d4 __attribute__((ext_vector_type(4)));
 // out = Z' H Z (nz x nz, row-major in LDS) on the matrix cores: v_mfma_f64_16x16x4_f64
 // with A[a][t] = h_t Z[u_t][a], B[t][b] = Z[w_t][b], four terms per instruction
 // (lane l supplies term t0 + (l >> 4), column l & 15).  Z and the term lists are
-// zero-padded (rows to n8, columns to ldz, couplings to a multiple of 8), so the loops
+// zero-padded (rows to n16, columns to ldz, couplings to a multiple of 16), so the loops
 // are branch-free with unconditional LDS loads; two accumulator chains per tile keep
 // consecutive MFMAs independent.  16x16 output tiles, upper triangle of tiles computed
 // and mirrored.  unit != 0: H = I (gives Z'Z).
@@ -344,10 +344,10 @@ template <int NZM>
 __device__ __forceinline__ void build_Hc(const Ctx &c, double *out, int unit)
 {
     constexpr int T = NZM / 16;
-    const int nz = c.nz, ldz = c.ldz, n8 = c.n8, li = c.tid & 15, kq = c.tid >> 4;
-    const int cpl8 = unit ? 0 : SRB_R8(2 * (2 * (c.N - 1) + (c.nl ? 3 * c.N : 0)));
+    const int nz = c.nz, ldz = c.ldz, n16 = c.n16, li = c.tid & 15, kq = c.tid >> 4;
+    const int cpl16 = unit ? 0 : SRB_R16(2 * (2 * (c.N - 1) + (c.nl ? 3 * c.N : 0)));
     const int Tn = ldz >> 4;
-    const double *Z = c.Z, *D = c.D, *Dc = c.D + n8;
+    const double *Z = c.Z, *D = c.D, *Dc = c.D + n16;
 #pragma unroll
     for (int ta = 0; ta < T; ta++) {
         if (ta >= Tn) break;
@@ -355,29 +355,39 @@ __device__ __forceinline__ void build_Hc(const Ctx &c, double *out, int unit)
 #pragma unroll
         for (int tb = 0; tb < T; tb++) { acc0[tb] = srb_d4{0.0, 0.0, 0.0, 0.0}; acc1[tb] = acc0[tb]; }
         const int ca = 16 * ta + li;
-#pragma unroll 2
-        for (int t0 = 0; t0 < n8; t0 += 8) {                 // diagonal terms
-            const int v0 = t0 + kq, v1 = t0 + 4 + kq;
-            const double h0 = unit ? 1.0 : D[v0], h1 = unit ? 1.0 : D[v1];
-            const double a0 = h0 * Z[v0 * ldz + ca], a1 = h1 * Z[v1 * ldz + ca];
+        for (int t0 = 0; t0 < n16; t0 += 16) {                // diagonal terms, 16 per trip
+            double a[4]; int r[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                const int v = t0 + 4 * u + kq;
+                r[u] = v * ldz;
+                a[u] = (unit ? 1.0 : D[v]) * Z[r[u] + ca];
+            }
 #pragma unroll
             for (int tb = 0; tb < T; tb++)
                 if (tb >= ta && tb < Tn) {
                     const int cb = 16 * tb + li;
-                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, Z[v0 * ldz + cb], acc0[tb], 0, 0, 0);
-                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, Z[v1 * ldz + cb], acc1[tb], 0, 0, 0);
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], Z[r[0] + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], Z[r[1] + cb], acc1[tb], 0, 0, 0);
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[2], Z[r[2] + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[3], Z[r[3] + cb], acc1[tb], 0, 0, 0);
                 }
         }
-#pragma unroll 2
-        for (int e0 = 0; e0 < cpl8; e0 += 8) {               // coupling terms
-            const int2 uw0 = c.term[e0 + kq], uw1 = c.term[e0 + 4 + kq];
-            const double a0 = Dc[e0 + kq] * Z[uw0.x + ca], a1 = Dc[e0 + 4 + kq] * Z[uw1.x + ca];
+        for (int e0 = 0; e0 < cpl16; e0 += 16) {              // coupling terms, 16 per trip
+            double a[4]; int2 uw[4];
+#pragma unroll
+            for (int u = 0; u < 4; u++) {
+                uw[u] = c.term[e0 + 4 * u + kq];
+                a[u] = Dc[e0 + 4 * u + kq] * Z[uw[u].x + ca];
+            }
 #pragma unroll
             for (int tb = 0; tb < T; tb++)
                 if (tb >= ta && tb < Tn) {
                     const int cb = 16 * tb + li;
-                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, Z[uw0.y + cb], acc0[tb], 0, 0, 0);
-                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, Z[uw1.y + cb], acc1[tb], 0, 0, 0);
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[0], Z[uw[0].y + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[1], Z[uw[1].y + cb], acc1[tb], 0, 0, 0);
+                    acc0[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[2], Z[uw[2].y + cb], acc0[tb], 0, 0, 0);
+                    acc1[tb] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[3], Z[uw[3].y + cb], acc1[tb], 0, 0, 0);
                 }
         }
         // D layout of v_mfma_f64_16x16x4: col = lane & 15, row = (lane >> 4) + 4 * reg
@@ -396,97 +406,112 @@ __device__ __forceinline__ void build_Hc(const Ctx &c, double *out, int unit)
     __syncthreads();
 }
 
-// --------------------------------------------------------------------------- register Cholesky
-// Right-looking Cholesky of the nz x nz SPD matrix H, lane i = row i held in registers
-// row[0..NZM) (the k loop is unrolled, so every register index is static).  Step k: the
-// pivot comes from lane k by v_readlane, each lane forms its multiplier l_i = L[i][k],
-// the column is broadcast through LDS (bc: one write per lane, same-address reads), and
-// the trailing rows are updated in place.  The eliminated column k of lane i > k keeps
-// l_i.  At the end lane i holds, in row[]:
-//     row[k] = L[i][k]            for k < i
-//     row[k] = A_i[i][k]          for k > i  (row i of the step-i Schur complement,
-//                                             = L[k][i] / inv_i, i.e. column i of L)
-// so both triangular solves run from the lane's own registers.  row[] goes to LDS
-// (Lr, row-major, stride nz) with inv_i = 1/L_ii in dinv.  regularise != 0 mirrors
-// iSWIFT's dynamic pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7) for
-// the QP stage.  Returns 0 on success (wave-uniform).  Lr may alias H.
+// --------------------------------------------------------------------------- Gauss-Jordan inverse
+// The reduced Newton matrix (nz x nz SPD) is inverted in place by Gauss-Jordan without
+// pivoting; each Newton solve is then one matvec.  Layout: G = 64/NZM lanes per row,
+// lane = G*i + g holds A[i][CW*g .. CW*g+CW-1] (CW = NZM/G: 4 entries at NZM = 16), so a
+// step costs each lane CW FMAs.  Step k: the pivot comes from its lane by v_readlane;
+// lanes of row k publish the scaled row, lanes of column k the multipliers, through a
+// double-buffered LDS broadcast; every lane updates its entries.  The pivots are those
+// of L D L' in natural order, so pivot <= 0 <=> not positive definite, and regularise
+// != 0 applies iSWIFT's dynamic pivot regularisation to them (ldl.c:320-321:
+// |D_kk| <= 1e-14 -> 1e-7) for the QP stage.  Padding rows/columns (>= nz) are the
+// identity, so the steps of the last 4-step chunk beyond nz are no-ops.  Steps run in
+// straight-line chunks of 4 (one uniform branch per chunk).  Minv (row-major, stride
+// nz) may alias H.  Returns 0 on success (wave-uniform).
 template <int NZM>
-__device__ __forceinline__ int chol_reg(const Ctx &c, const double *H, double *Lr, double *dinv, int nz, int regularise)
+__device__ __forceinline__ int gj_inverse(const Ctx &c, const double *H, double *Minv, int nz, int regularise)
 {
-    const int i = c.tid;
-    double row[NZM];
+    constexpr int G = WAVE / NZM, CW = NZM / G;
+    const int i = c.tid / G, g = c.tid % G;
+    double A[CW];
 #pragma unroll
-    for (int j = 0; j < NZM; j++) row[j] = (i < nz && j < nz) ? H[i * nz + j] : 0.0;
+    for (int q = 0; q < CW; q++) {
+        const int j = CW * g + q;
+        A[q] = (i < nz && j < nz) ? H[i * nz + j] : (i == j ? 1.0 : 0.0);
+    }
     __syncthreads();
-    double myinv = 0.0;
     int fail = 0;
 #pragma unroll
-    for (int k = 0; k < NZM; k++) {
-        if (k >= nz || fail) continue;  // (no break: it would block the full unroll)
-        double piv = readlane_d(row[k], k);
-        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
-        if (!(piv > 0.0)) { fail = 1; continue; }
-        const double inv = rsq_d(piv);
-        const double l = (i > k && i < nz) ? row[k] * inv : 0.0;
-        if (i == k) myinv = inv;
-        c.bc[i] = l;
-        __syncthreads();
+    for (int k0 = 0; k0 < NZM; k0 += 4) {
+        if (k0 >= nz) continue;
 #pragma unroll
-        for (int j = k + 1; j < NZM; j++) row[j] = fma(-l, c.bc[j], row[j]);
-        if (i > k) row[k] = l;
-        __syncthreads();                // bc is rewritten next step
+        for (int k = k0; k < k0 + 4; k++) {
+            const int gk = k / CW, qk = k % CW;
+            double piv = readlane_d(A[qk], G * k + gk);
+            if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+            fail |= !(piv > 0.0);
+            const double inv = rcp_d(piv);
+            double *rb = c.bc + 2 * WAVE * (k & 1), *cb = rb + WAVE;
+            if (i == k) {
+#pragma unroll
+                for (int q = 0; q < CW; q++) rb[CW * g + q] = (q == qk && g == gk) ? inv : A[q] * inv;
+            }
+            if (g == gk) cb[i] = A[qk];
+            __builtin_amdgcn_wave_barrier();
+            const double f = cb[i];
+            if (g == gk) A[qk] = 0.0;                       // column k becomes -f * inv
+#pragma unroll
+            for (int q = 0; q < CW; q++) {
+                const double r = rb[CW * g + q];
+                A[q] = (i == k) ? r : fma(-f, r, A[q]);
+            }
+        }
     }
     if (i < nz) {
 #pragma unroll
-        for (int j = 0; j < NZM; j++)
-            if (j < nz) Lr[i * nz + j] = row[j];
-        dinv[i] = myinv;
+        for (int q = 0; q < CW; q++)
+            if (CW * g + q < nz) Minv[i * nz + CW * g + q] = A[q];
     }
     __syncthreads();
     return fail;
 }
 
-// (L L') x = b with b one entry per lane (lane i < nz); returns x in the same layout.
-// Forward:  y_k = b_k inv_k after all updates of lanes < k, then b_i -= L[i][k] y_k.
-// Backward: x_k = inv_k (y_k - inv_k acc_k), acc_i += A_i[i][k] x_k  (L[k][i] = inv_i A_i[i][k]).
-// Lanes that already hold their final value keep it via the select.
+// y = M x for an nz x nz row-major LDS matrix and an LDS vector: lane (i, g) sums its CW
+// columns, the G lanes of row i (adjacent) combine by DPP; every lane of row i holds y_i.
 template <int NZM>
-__device__ __forceinline__ double chol_solve_reg(const Ctx &c, const double *Lr, const double *dinv, int nz, double b)
+__device__ __forceinline__ double gj_matvec(const Ctx &c, const double *M, const double *x)
 {
-    const int i = c.tid;
-    double row[NZM];
+    constexpr int G = WAVE / NZM, CW = NZM / G;
+    const int nz = c.nz, i = c.tid / G, g = c.tid % G;
+    double acc = 0.0;
 #pragma unroll
-    for (int j = 0; j < NZM; j++) row[j] = (i < nz && j < nz) ? Lr[i * nz + j] : 0.0;
-    const double inv = (i < nz) ? dinv[i] : 0.0;
-    double y = 0.0;
-#pragma unroll
-    for (int k = 0; k < NZM; k++) {
-        if (k >= nz) continue;
-        const double t = b * inv;
-        const double yk = readlane_d(t, k);
-        if (i == k) y = t;
-        b = fma(-row[k], yk, b);         // lanes > k: L[i][k]; lanes <= k: final already
+    for (int q = 0; q < CW; q++) {
+        const int j = CW * g + q;
+        if (i < nz && j < nz) acc = fma(M[i * nz + j], x[j], acc);
     }
-    double acc = 0.0, x = 0.0;
-#pragma unroll
-    for (int k = NZM - 1; k >= 0; k--) {
-        if (k >= nz) continue;
-        const double t = inv * fma(-inv, acc, y);
-        const double xk = readlane_d(t, k);
-        if (i == k) x = t;
-        acc = fma(row[k], xk, acc);      // lanes < k: A_i[i][k]; lanes >= k: final already
-    }
-    return x;
+    if (G >= 2) acc += dpp_d<0xB1>(acc);
+    if (G >= 4) acc += dpp_d<0x4E>(acc);
+    return acc;
 }
 
-// xi-vector (one entry per lane) = Z' v.  Lanes (a, d) = (4a + d) sum the X rows of state
-// component d over grids >= stage(a); the quad is reduced by xor-shuffles; the U/lambda
-// rows of the column's own grid are added by the d == 0 lane.
+// out = H^-1 gin with one step of iterative refinement (x = M g; x += M (g - H x)):
+// the explicit inverse alone is not backward stable, and near the end of an interior-
+// point solve H carries barrier weights of 1e8..1e12.  gin, out, c.bc scratch in LDS.
 template <int NZM>
-__device__ __forceinline__ double zt_mul(const Ctx &c, const double *v)
+__device__ __forceinline__ void gj_solve(const Ctx &c, const double *H, const double *Minv, const double *gin, double *out)
+{
+    constexpr int G = WAVE / NZM;
+    const int nz = c.nz, i = c.tid / G, g = c.tid % G;
+    double *xs = c.bc, *rs = c.bc + WAVE;
+    const double x0 = gj_matvec<NZM>(c, Minv, gin);
+    if (g == 0 && i < nz) xs[i] = x0;
+    __syncthreads();
+    const double r = (i < nz ? gin[i] : 0.0) - gj_matvec<NZM>(c, H, xs);
+    if (g == 0 && i < nz) rs[i] = r;
+    __syncthreads();
+    const double x1 = x0 + gj_matvec<NZM>(c, Minv, rs);
+    if (g == 0 && i < nz) out[i] = x1;
+    __syncthreads();
+}
+
+// out[0..nz) = Z' v (LDS).  Lanes (a, d) = (4a + d) sum the X rows of state component d
+// over grids >= stage(a); the quad is reduced by DPP; the U/lambda rows of the column's
+// own grid are added by the d == 0 / d == 1 lanes.
+template <int NZM>
+__device__ __forceinline__ void zt_mul(const Ctx &c, const double *v, double *out)
 {
     const int N = c.N, nz = c.nz, C = c.C, d = c.tid & 3;
-    double res = 0.0;
 #pragma unroll
     for (int round = 0; round < (NZM + 15) / 16; round++) {
         const int a = round * 16 + (c.tid >> 2);
@@ -511,25 +536,19 @@ __device__ __forceinline__ double zt_mul(const Ctx &c, const double *v)
                 acc = v[c.n - 1];
             }
         }
-        acc += __shfl_xor(acc, 1, WAVE);
-        acc += __shfl_xor(acc, 2, WAVE);
-        // lane a' takes column a' of this round from lane 4 (a' - 16 round)
-        const int src = 4 * ((c.tid - round * 16) & 15);
-        const double got = __shfl(acc, src, WAVE);
-        if (c.tid >= round * 16 && c.tid < round * 16 + 16) res = got;
+        acc += dpp_d<0xB1>(acc);
+        acc += dpp_d<0x4E>(acc);
+        if (d == 0 && a < nz) out[a] = acc;
     }
-    return (c.tid < nz) ? res : 0.0;
+    __syncthreads();
 }
 
-// out = Z xi  (xi one entry per lane); columns of grid j reach X rows of grids >= j and
+// out = Z xi  (xi in LDS); columns of grid j reach X rows of grids >= j and
 // the U/lambda rows of grid j only.
 template <int NZM>
-__device__ __forceinline__ void z_mul(const Ctx &c, double xi, double *out)
+__device__ __forceinline__ void z_mul(const Ctx &c, const double *xs, double *out)
 {
     const int N = c.N, nz = c.nz, C = c.C, n = c.n;
-    if (c.tid < nz) c.xiv[c.tid] = xi;
-    __syncthreads();
-    const double *xs = c.xiv;                       // LDS broadcast reads
     for (int v = c.tid; v < n; v += WAVE) {
         double a0 = 0.0, a1 = 0.0;
         if (v < 4 * N) {
@@ -562,11 +581,11 @@ __device__ __forceinline__ void newton_solve(const Ctx &c, const double *r1, dou
     __syncthreads();
     jt_apply(c, w, c.tv, r1, 1.0);
     STAMP_END(c, sslot + 0);
-    const double g = zt_mul<NZM>(c, c.tv);
+    zt_mul<NZM>(c, c.tv, c.gbuf);
     STAMP_END(c, sslot + 1);
-    const double xi = chol_solve_reg<NZM>(c, c.L, c.dinv, c.nz, g);
+    gj_solve<NZM>(c, c.Hc, c.L, c.gbuf, c.xiv);
     STAMP_END(c, sslot + 2);
-    z_mul<NZM>(c, xi, c.dx);
+    z_mul<NZM>(c, c.xiv, c.dx);
     STAMP_END(c, sslot + 3);
     for (int r = c.tid; r < c.m; r += WAVE) r3dz[r] = c.om[r] * (row_dot(c, r, c.dx) - r3dz[r]);
     __syncthreads();
@@ -644,7 +663,7 @@ __device__ __forceinline__ int ipm(Ctx &c, int maxit, int *iters)
                     for (int a = c.tid; a < c.nz; a += WAVE) dm = fmax(dm, c.Hc[a * c.nz + a]);
                     dstart = 1e-10 * wmax(dm);
                 }
-                int cf = chol_reg<NZM>(c, c.Hc, c.L, c.dinv, c.nz, !c.nl);
+                int cf = gj_inverse<NZM>(c, c.Hc, c.L, c.nz, !c.nl);
                 STAMP_END(c, sb + 4);
                 if (cf == 0) { ok = 1; break; }
                 delta = (delta == 0.0) ? dstart : delta * 10.0;
@@ -800,20 +819,20 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     const int mmax = prm.use_nlp ? (c.mq + N * K + 4 * N) : c.mq;
     // carve LDS (offsets must match srb_lds_doubles())
     double *p = lds;
-    c.ldz = SRB_LDZ(nz); c.n8 = SRB_R8(n);
-    const int cpl8 = SRB_R8(SRB_NCPL2(N));
-    c.Z = p; p += c.n8 * c.ldz;
+    c.ldz = SRB_LDZ(nz); c.n16 = SRB_R16(n);
+    const int cpl16 = SRB_R16(SRB_NCPL2(N));
+    c.Z = p; p += c.n16 * c.ldz;
     c.x = p; p += n; c.q = p; p += n; c.rx = p; p += n; c.dx = p; p += n; c.tv = p; p += n;
-    c.D = p; p += c.n8 + cpl8; c.term = (int2 *)p; p += cpl8;
+    c.D = p; p += c.n16 + cpl16; c.term = (int2 *)p; p += cpl16;
     c.ref = p; p += 4 * N; c.foot = p; p += 2 * C * N;
     c.s = p; p += mmax; c.z = p; p += mmax; c.rz = p; p += mmax; c.dz = p; p += mmax;
     c.dsv = p; p += mmax; c.dsT = p; p += mmax; c.om = p; p += mmax; c.hvec = p; p += mmax;
     c.iz = p; p += mmax; c.is = p; p += mmax; c.l2 = p; p += mmax;
     c.jc = p; p += 2 * N * K + 2; c.obs = p; p += 2 * N * K + 2; c.eps = p; p += K + 1;
-    // the factor overwrites the assembled matrix (chol_reg holds all rows in registers first)
-    c.Hc = p; c.L = p; p += nz * nz; c.ZtZ = p; c.ZtZL = p; p += nz * nz;
-    c.dinv = p; p += nz; c.ZtZdinv = p; p += nz; c.xiv = p; p += nz;
-    c.bc = p; p += WAVE;
+    // assembled matrices and their inverses (the solves refine against the originals)
+    c.Hc = p; p += nz * nz; c.L = p; p += nz * nz; c.ZtZ = p; p += nz * nz; c.ZtZL = p; p += nz * nz;
+    c.xiv = p; p += WAVE; c.gbuf = p; p += WAVE;
+    c.bc = p; p += 4 * WAVE;
 #ifdef SRB_STAMPS
     c.stamps = (unsigned long long *)p; p += SRB_NSTAMP;
     c.stamps[c.tid] = 0;
@@ -825,8 +844,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     const double *x0 = x0g + 4 * (size_t)agent;
     for (int i = c.tid; i < 4 * N; i += WAVE) c.ref[i] = refg[(size_t)agent * 4 * N + i];
     for (int i = c.tid; i < 2 * C * N; i += WAVE) c.foot[i] = footg[(size_t)agent * 2 * C * N + i];
-    for (int i = c.tid; i < c.n8 * c.ldz; i += WAVE) c.Z[i] = 0.0;
-    for (int i = c.tid; i < c.n8 + cpl8; i += WAVE) c.D[i] = 0.0;      // padding terms stay 0
+    for (int i = c.tid; i < c.n16 * c.ldz; i += WAVE) c.Z[i] = 0.0;
+    for (int i = c.tid; i < c.n16 + cpl16; i += WAVE) c.D[i] = 0.0;      // padding terms stay 0
     __syncthreads();
 
     // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
@@ -884,7 +903,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             __syncthreads();
             build_D(c, 0.0);
             build_Hc<NZM>(c, c.Hc, 0);
-            if (chol_reg<NZM>(c, c.Hc, c.L, c.dinv, nz, 1) != 0) { qp_flag = 1; continue; }
+            if (gj_inverse<NZM>(c, c.Hc, c.L, nz, 1) != 0) { qp_flag = 1; continue; }
             // r1 = -c - P xbar ; r3 = h - G xbar   ->  dx ; x = xbar + dx
             for (int v = c.tid; v < n; v += WAVE) c.rx[v] = -cvec(c, v) - Pdiag(c, v) * c.x[v];
             for (int r = c.tid; r < c.m; r += WAVE) c.dz[r] = c.hvec[r] - row_dot(c, r, c.x);
@@ -955,14 +974,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int r = c.tid; r < c.m; r += WAVE) { c.s[r] = (ap < 0) ? c.rz[r] : c.rz[r] + (1 + ap); c.z[r] = 1.0; }
             // Z'Z and its factor: projection for q0
             build_Hc<NZM>(c, c.ZtZ, 1);
-            chol_reg<NZM>(c, c.ZtZ, c.ZtZL, c.ZtZdinv, nz, 0);
+            gj_inverse<NZM>(c, c.ZtZ, c.ZtZL, nz, 0);
             // v = P x + c + J'z ; rx0 = -Z (Z'Z)^-1 Z' v ; q = -v - rx0
             for (int v = c.tid; v < n; v += WAVE) c.tv[v] = Pdiag(c, v) * c.x[v] + cvec(c, v);
             __syncthreads();
             jt_apply(c, c.z, c.rx, c.tv, 1.0);
-            const double g = zt_mul<NZM>(c, c.rx);
-            const double t = chol_solve_reg<NZM>(c, c.ZtZL, c.ZtZdinv, nz, g);
-            z_mul<NZM>(c, t, c.dx);
+            zt_mul<NZM>(c, c.rx, c.gbuf);
+            gj_solve<NZM>(c, c.ZtZ, c.ZtZL, c.gbuf, c.xiv);
+            z_mul<NZM>(c, c.xiv, c.dx);
             for (int v = c.tid; v < n; v += WAVE) c.q[v] = -c.rx[v] + c.dx[v];
             __syncthreads();
             STAMP_END(c, 30);
@@ -1009,4 +1028,3 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 
 SRB_NMPC_KERNEL(srb_nmpc_kernel_nz16, 16)
 SRB_NMPC_KERNEL(srb_nmpc_kernel_nz32, 32)
-SRB_NMPC_KERNEL(srb_nmpc_kernel_nz64, 64)
