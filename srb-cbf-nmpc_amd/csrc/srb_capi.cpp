@@ -12,13 +12,30 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
-#define DECL_NMPC(NAME)                                                                                       \
-    extern "C" __global__ void NAME(SrbKParams prm, int n_agents, const double *x0g, const double *refg,      \
-                                    const double *footg, const double *obstacles, int n_obs,                   \
-                                    const double *nbr_state, int n_all, int agent_offset, double *x_qp_out,    \
-                                    double *x_out, double *obj_out, int *status_out, int *iters_out);
-DECL_NMPC(srb_nmpc_kernel_nz16)
-DECL_NMPC(srb_nmpc_kernel_nz32)
+#define DECL_NMPC(NZL, TV, TO)                                                                                \
+    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TV##_##TO(                                           \
+        SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
+        const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
+        double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out);
+SRB_KERNEL_INSTANCES(DECL_NMPC)
+#undef DECL_NMPC
+
+typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
+                              const double *, int, int, double *, double *, double *, int *, int *);
+struct srb_instance { int nzl, tv, to; srb_kernel_fn fn; };
+#define ENTRY_NMPC(NZL, TV, TO) {NZL, TV, TO, srb_nmpc_kernel_##NZL##_##TV##_##TO},
+static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
+#undef ENTRY_NMPC
+
+// first instance whose register bounds cover the problem (nz rows, n variable slots,
+// N*K obstacle slots); NULL when none does
+static const srb_instance *pick_instance(const SrbKParams &k)
+{
+    const int nk = k.N * (k.K_obs + k.K_nbr);
+    for (const srb_instance &in : g_instances)
+        if (in.nzl >= k.nz && 64 * in.tv >= k.n && 64 * in.to >= (nk > 0 ? nk : 1)) return &in;
+    return nullptr;
+}
 
 static thread_local std::string g_err;
 
@@ -107,19 +124,22 @@ static int validate(const srb_params *p)
 {
     if (!p) return fail(SRB_ERR_ARG, "null params");
     if (p->N < 2 || p->C < 2 || p->C > 4) return fail(SRB_ERR_ARG, "need N >= 2 and 2 <= C <= 4");
+    if (p->N > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N exceeds 33 (CoM-CoP slots in one 64-lane trip)");
     if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs > SRB_KNN_MAX || p->K_nbr > SRB_KNN_MAX)
         return fail(SRB_ERR_ARG, "K_obs, K_nbr out of range (each <= 16)");
-    if (p->N * (p->C - 1) + 1 > SRB_MAX_N) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 32 (reduced Newton system bound)");
-    if ((6 + p->C) * p->N + 1 > SRB_MAX_NV) return fail(SRB_ERR_SIZE, "nv exceeds 256");
+    if (p->N * (p->C - 1) + 1 > SRB_MAX_NZ) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 32 (reduced Newton system bound)");
     SrbKParams k = make_kparams(p, p->use_nlp);
-    if ((size_t)srb_lds_doubles(k) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
+    const srb_instance *in = pick_instance(k);
+    if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers nv / N*K (nv <= 256, N*K <= 256)");
+    if ((size_t)srb_lds_doubles(k, in->nzl) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
     return SRB_OK;
 }
 
 extern "C" int srb_lds_bytes(const srb_params *p)
 {
     SrbKParams k = make_kparams(p, p->use_nlp);
-    return srb_lds_doubles(k) * (int)sizeof(double);
+    const srb_instance *in = pick_instance(k);
+    return in ? srb_lds_doubles(k, in->nzl) * (int)sizeof(double) : -1;
 }
 
 extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out)
@@ -180,19 +200,16 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
     if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
-    const size_t lds = (size_t)srb_lds_doubles(k) * sizeof(double);
+    const srb_instance *in = pick_instance(k);
+    if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers this problem");
+    const size_t lds = (size_t)srb_lds_doubles(k, in->nzl) * sizeof(double);
     HIPCHK(hipSetDevice(c->device));
     const int n_obs = k.K_obs > 0 ? d->n_obs : 0, n_all = k.K_nbr > 0 ? d->n_all : 0;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
-    // one launch: nearest-obstacle selection, QP stage and NLP stage per agent; kernel
-    // instance by the register-resident bound on nz (one row of Z'HZ per lane)
-#define SRB_LAUNCH(KERN)                                                                                        \
-    hipLaunchKernelGGL(KERN, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,  \
-                       n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters)
-    if (k.nz <= 16) SRB_LAUNCH(srb_nmpc_kernel_nz16);
-    else SRB_LAUNCH(srb_nmpc_kernel_nz32);
-#undef SRB_LAUNCH
+    // one launch: nearest-obstacle selection, QP stage and NLP stage per agent
+    hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
+                       n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;

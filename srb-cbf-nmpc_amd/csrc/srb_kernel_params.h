@@ -1,11 +1,10 @@
-// Kernel-side parameter block (host fills it from srb_params, see srb_capi.cpp).
+// Kernel-side parameter block (host fills it from srb_params, see srb_capi.cpp) and the
+// per-instance LDS budget.
 #pragma once
 
-#define SRB_MAX_K 32      // obstacle rows per grid (K_obs + K_nbr)
-#define SRB_KNN_MAX 16    // neighbours per agent (K_nbr)
-#define SRB_MAX_N 32      // reduced Newton system size bound: nz = N(C-1)+1 <= 32
-#define SRB_MAX_OBS 4096  // static obstacles (64 lanes x 64-bit chosen mask)
-#define SRB_MAX_NV 256    // z_mul keeps 4 variables per lane
+#define SRB_KNN_MAX 16    // nearest static obstacles / neighbours per agent (each)
+#define SRB_MAX_NZ 32     // reduced Newton system size bound: nz = N(C-1)+1 <= 32
+#define SRB_MAX_N 33      // CoM-CoP slots 2(N-1) fit one 64-lane trip
 
 struct SrbKParams {
     int N, C, K_obs, K_nbr;
@@ -16,22 +15,21 @@ struct SrbKParams {
     double eps_obs, eps_nbr, vsat, tol, Ts;
 };
 
-// Z'HZ layout helpers: Z is n16 x ldz (rows to a multiple of 16, columns to a multiple of
-// 16, zero padded); SRB_NCPL2 = both orientations of every off-diagonal coupling of H.
-#define SRB_R16(x) ((((x) + 15) / 16) * 16)     /* term lists: whole 16-term MFMA trips */
-#define SRB_LDZ(nz) ((((nz) + 15) / 16) * 16)
-#define SRB_NCPL2(N) (2 * (2 * ((N) - 1) + 3 * (N)))
+// Kernel instances (NZL, TV, TO): register bound on nz (one reduced-matrix row per lane),
+// trips of 64 variable slots, trips of 64 obstacle slots.  The host launches the first
+// instance of this list that fits (srb_capi.cpp).
+#define SRB_KERNEL_INSTANCES(X) \
+    X(8, 1, 1) X(16, 1, 1) X(12, 2, 1) X(12, 2, 2) X(16, 2, 2) X(24, 3, 1) X(24, 3, 4) X(32, 2, 2) X(32, 4, 4)
 
-// doubles of dynamic LDS one agent needs; must match the carve in srb_nmpc_kernel
-static inline int srb_lds_doubles(const SrbKParams &p)
+static inline int srb_r4(int x) { return (x + 3) & ~3; }
+
+// doubles of dynamic LDS one agent needs for instance bound NZL; must match the carve in
+// nmpc_agent (srb_kernels.hip)
+static inline int srb_lds_doubles(const SrbKParams &p, int NZL)
 {
-    const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n = p.n, nz = p.nz;
-    const int mmax = p.use_nlp ? (p.mq + N * K + 4 * N) : p.mq;
-    const int cpl16 = SRB_R16(SRB_NCPL2(N));
-    return SRB_R16(n) * SRB_LDZ(nz) + 5 * n + SRB_R16(n) + 2 * cpl16 + 4 * N + 2 * C * N + 11 * mmax +
-           (2 * N * K + 2) * 2 + (K + 1) + 4 * nz * nz + 6 * 64
-#ifdef SRB_STAMPS
-           + 64
-#endif
-        ;
+    const int NZM = ((NZL + 15) / 16) * 16, LDR = NZM + 1, LDH = NZM + 1;
+    const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
+    const int TT = n4 + srb_r4(2 * (N - 1)) + srb_r4(NK);
+    return TT * LDR + 2 * TT + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
+           srb_r4(NK) + (K + 1);
 }
