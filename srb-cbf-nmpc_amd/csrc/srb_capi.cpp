@@ -12,8 +12,8 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
-#define DECL_NMPC(NZL, TV, TO)                                                                                \
-    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TV##_##TO(                                           \
+#define DECL_NMPC(NZL, TS)                                                                                    \
+    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS(                                                  \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out);
@@ -22,18 +22,18 @@ SRB_KERNEL_INSTANCES(DECL_NMPC)
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *);
-struct srb_instance { int nzl, tv, to; srb_kernel_fn fn; };
-#define ENTRY_NMPC(NZL, TV, TO) {NZL, TV, TO, srb_nmpc_kernel_##NZL##_##TV##_##TO},
+struct srb_instance { int nzl, ts; srb_kernel_fn fn; };
+#define ENTRY_NMPC(NZL, TS) {NZL, TS, srb_nmpc_kernel_##NZL##_##TS},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 #undef ENTRY_NMPC
 
-// first instance whose register bounds cover the problem (nz rows, n variable slots,
-// N*K obstacle slots); NULL when none does
+// first instance whose register bounds cover the problem (nz reduced rows, all row slots);
+// NULL when none does
 static const srb_instance *pick_instance(const SrbKParams &k)
 {
-    const int nk = k.N * (k.K_obs + k.K_nbr);
+    const int S = srb_slots(k.N, k.C, k.K_obs + k.K_nbr);
     for (const srb_instance &in : g_instances)
-        if (in.nzl >= k.nz && 64 * in.tv >= k.n && 64 * in.to >= (nk > 0 ? nk : 1)) return &in;
+        if (in.nzl >= k.nz && 64 * in.ts >= S) return &in;
     return nullptr;
 }
 
@@ -130,7 +130,7 @@ static int validate(const srb_params *p)
     if (p->N * (p->C - 1) + 1 > SRB_MAX_NZ) return fail(SRB_ERR_SIZE, "N(C-1)+1 exceeds 32 (reduced Newton system bound)");
     SrbKParams k = make_kparams(p, p->use_nlp);
     const srb_instance *in = pick_instance(k);
-    if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers nv / N*K (nv <= 256, N*K <= 256)");
+    if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers the row slots (n + 4N - 2 + N K <= 512)");
     if ((size_t)srb_lds_doubles(k, in->nzl) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
     return SRB_OK;
 }

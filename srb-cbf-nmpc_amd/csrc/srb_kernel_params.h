@@ -15,11 +15,12 @@ struct SrbKParams {
     double eps_obs, eps_nbr, vsat, tol, Ts;
 };
 
-// Kernel instances (NZL, TV, TO): register bound on nz (one reduced-matrix row per lane),
-// trips of 64 variable slots, trips of 64 obstacle slots.  The host launches the first
-// instance of this list that fits (srb_capi.cpp).
+// Kernel instances (NZL, TS): register bound on nz (one reduced-matrix row per lane) and
+// trips of 64 row slots (n + 2(N-1) + 2N + N K slots, see srb_kernels.hip).  The host
+// launches the first instance of this list that fits (srb_capi.cpp).
 #define SRB_KERNEL_INSTANCES(X) \
-    X(8, 1, 1) X(16, 1, 1) X(12, 2, 1) X(12, 2, 2) X(16, 2, 2) X(24, 3, 1) X(24, 3, 4) X(32, 2, 2) X(32, 4, 4)
+    X(8, 1) X(16, 1) X(12, 3) X(12, 4) X(16, 4) X(24, 5) X(24, 8) X(32, 4) X(32, 8)
+static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K; }
 
 static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
@@ -27,9 +28,13 @@ static inline int srb_r4(int x) { return (x + 3) & ~3; }
 // nmpc_agent (srb_kernels.hip)
 static inline int srb_lds_doubles(const SrbKParams &p, int NZL)
 {
-    const int NZM = ((NZL + 15) / 16) * 16, LDR = NZM + 1, LDH = NZM + 1;
+    const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZM + 1;
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
-    const int TT = n4 + srb_r4(2 * (N - 1)) + srb_r4(NK);
-    return TT * LDR + 2 * TT + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
-           srb_r4(NK) + (K + 1);
+    const int TT = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + srb_r4(NK) + 15) & ~15;
+    return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
+           srb_r4(NK) + (K + 1)
+#ifdef SRB_STAMPS
+           + 64
+#endif
+        ;
 }

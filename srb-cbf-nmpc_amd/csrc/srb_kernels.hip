@@ -84,6 +84,34 @@ __device__ __forceinline__ double op_add(double a, double b) { return a + b; }
 SRB_WAVE_REDUCE(wsum, op_add)
 SRB_WAVE_REDUCE(wmin, fmin)
 SRB_WAVE_REDUCE(wmax, fmax)
+// NV independent wave reductions interleaved stage by stage (one DPP/permlane latency per
+// stage for all of them); bit i of MX selects max (1) or sum (0) for v[i].
+template <int NV, unsigned MX>
+__device__ __forceinline__ void wred(double (&v)[NV])
+{
+#define SRB_RED_STAGE(GET)                                                                      \
+    _Pragma("unroll") for (int i = 0; i < NV; i++) {                                            \
+        const double t_ = GET;                                                                  \
+        v[i] = ((MX >> i) & 1u) ? fmax(v[i], t_) : v[i] + t_;                                   \
+    }
+    SRB_RED_STAGE(dpp_d<0xB1>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x4E>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x141>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x140>(v[i]))
+#undef SRB_RED_STAGE
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        double a, b;
+        swap_d<16>(v[i], a, b);
+        v[i] = ((MX >> i) & 1u) ? fmax(a, b) : a + b;
+    }
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        double a, b;
+        swap_d<32>(v[i], a, b);
+        v[i] = ((MX >> i) & 1u) ? fmax(a, b) : a + b;
+    }
+}
 // sum over the lanes that share (lane mod W), W = 16 or 32: permlane butterflies only
 __device__ __forceinline__ double chunk_sum16(double v)
 {
@@ -123,109 +151,136 @@ __device__ __forceinline__ int rnd4(int x) { return (x + 3) & ~3; }
 #ifdef SRB_STAMPS
 #define SRB_NSTAMP 64
 __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
-#define STAMP_DECL unsigned long long st_acc[SRB_NSTAMP / 4] = {0}; unsigned long long st_t0 = 0
+#define STAMP_DECL unsigned long long st_t0 = 0; int st_off = 0
 #define STAMP_BEGIN() do { __builtin_amdgcn_sched_barrier(0); st_t0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define STAMP_END(slot) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0); st_acc[(slot)] += _t - st_t0; st_t0 = _t; } while (0)
-#define STAMP_FLUSH(agent) do { if ((agent) == 0 && threadIdx.x == 0) for (int _i = 0; _i < SRB_NSTAMP / 4; _i++) atomicAdd(&srb_stamp_buf[_i], st_acc[_i]); } while (0)
+    __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0) atomicAdd(&stamp_lds[st_off + (slot)], _t - st_t0); st_t0 = _t; } while (0)
+#define STAMP_STAGE(s) (st_off = 32 * (s))
+#define STAMP_FLUSH(agent) do { SYNC(); if ((agent) == 0) atomicAdd(&srb_stamp_buf[threadIdx.x], stamp_lds[threadIdx.x]); } while (0)
 #else
 #define STAMP_DECL do {} while (0)
 #define STAMP_BEGIN() do {} while (0)
 #define STAMP_END(slot) do {} while (0)
+#define STAMP_STAGE(s) do {} while (0)
 #define STAMP_FLUSH(agent) do {} while (0)
 #endif
 
-// --------------------------------------------------------------------------- row state
-// One bound pair on a scalar function f = a'x (row+:  f <= hp, row-: -f <= hm), or a single
-// row (index 0 only).  s, z: slack and dual; the rest is per-iteration scratch.
-struct Pair {
-    double s[2], z[2], iz[2], is[2], dz[2], ds[2], dsT[2], r3[2];
+// --------------------------------------------------------------------------- term rows
+// Term row t (Z row of a variable, M_e, M_o) at R + t * LDR; LDR = NZL + 1 (odd: lane-
+// parallel row reads stay conflict-free).  Rows are zero beyond nz and beyond the count.
+// Row order: X rows (4N) | CoM-CoP rows | U, lambda, slack rows | obstacle rows.
+struct TermLayout {
+    int N, C, n, nz, E4;
+    __device__ __forceinline__ int zr(int v) const { return v < 4 * N ? v : v + E4; }
 };
 
-// rz_r = h_r - s_r - sg_r f
-__device__ __forceinline__ double rz_of(const Pair &p, int r, double f, double h)
+// GRAM: H = sum_t W_t r_t r_t' over the term rows [0, cnt): v_mfma_f64_16x16x4f64 with
+//   A[a][k] = r_{t0+k}[a], B[k][b] = W_{t0+k} r_{t0+k}[b]; lane l supplies term t0 + (l >> 4),
+//   column l & 15; D layout row (l >> 4) + 4 q, column l & 15; NZM = 32: tiles (0,0), (0,1),
+//   (1,1).  The next group's operands are loaded before the current MFMA issues, so the LDS
+//   latency hides under the 64-cycle f64 MFMA.
+// RHS: g[a] = sum_t CF_t r_t[a]: the very element lane l loads for the MFMA is the one its
+//   (column, term) pair needs, so the right-hand side costs one FMA per load; the four term
+//   chunks combine by permlane swaps.
+// cnt is a multiple of 16; rows / W / CF are zero beyond every real row.
+template <int NZL, bool RHS>
+__device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt,
+                                         double *H, double *g, int nz, int lane)
 {
-    return (r == 0) ? (h - p.s[0] - f) : (h - p.s[1] + f);
-}
-
-// --------------------------------------------------------------------------- term rows
-// Term row t (Z row of a variable, M_e, M_o) at rows + t * LDR; LDR = NZM + 1 (odd: lane-
-// parallel row reads stay conflict-free).  Rows are zero beyond nz and beyond the count.
-
-// out = sum_t w_t r_t r_t' (+ init): v_mfma_f64_16x16x4f64 with A[a][k] = r_{t0+k}[a],
-// B[k][b] = w_{t0+k} r_{t0+k}[b]; lane l supplies term t0 + (l >> 4), column l & 15.
-// D layout: row (l >> 4) + 4 q, column l & 15.  NZM = 32: tiles (0,0), (0,1), (1,1).
-template <int NZM>
-__device__ __forceinline__ void gram(const double *rows, const double *w, int cnt, double *out, int lane)
-{
-    constexpr int LDR = NZM + 1, LDH = NZM + 1;
-    constexpr int NT = (NZM == 16) ? 1 : 3;
+    constexpr int NZM = ((NZL + 15) / 16) * 16;
+    constexpr int LDR = NZL + 1, LDH = NZM + 1;
+    constexpr int NT = (NZM == 16) ? 1 : 3, NTC = NZM / 16;
     const int li = lane & 15, kq = lane >> 4;
-    d4 acc0[NT], acc1[NT];
+    d4 acc[NT];
+    double ps[NTC];
 #pragma unroll
-    for (int t = 0; t < NT; t++) { acc0[t] = d4{0.0, 0.0, 0.0, 0.0}; acc1[t] = acc0[t]; }
-    int t0 = 0;
-    for (; t0 + 8 <= cnt; t0 += 8) {
-        const double *r0 = rows + (t0 + kq) * LDR, *r1 = r0 + 4 * LDR;
-        const double w0 = w[t0 + kq], w1 = w[t0 + 4 + kq];
-        if constexpr (NZM == 16) {
-            const double a0 = r0[li], a1 = r1[li];
-            acc0[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * a0, acc0[0], 0, 0, 0);
-            acc1[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, w1 * a1, acc1[0], 0, 0, 0);
-        } else {
-            const double a0 = r0[li], b0 = r0[16 + li], a1 = r1[li], b1 = r1[16 + li];
-            acc0[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * a0, acc0[0], 0, 0, 0);
-            acc0[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * b0, acc0[1], 0, 0, 0);
-            acc0[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(b0, w0 * b0, acc0[2], 0, 0, 0);
-            acc1[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, w1 * a1, acc1[0], 0, 0, 0);
-            acc1[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a1, w1 * b1, acc1[1], 0, 0, 0);
-            acc1[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(b1, w1 * b1, acc1[2], 0, 0, 0);
+    for (int t = 0; t < NT; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+    for (int t = 0; t < NTC; t++) ps[t] = 0.0;
+    // four term groups per batch: every operand load of the batch issues before the first
+    // MFMA waits on one, and the next batch's loads issue while the MFMAs drain
+    for (int t0 = 0; t0 < cnt; t0 += 16) {
+        double a[4][NTC], w[4], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = t0 + 4 * u + kq;
+#pragma unroll
+            for (int tc = 0; tc < NTC; tc++) a[u][tc] = (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0;
+            w[u] = W[r];
+            c[u] = RHS ? CF[r] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);     // keep the batch's loads ahead of its MFMAs
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (RHS)
+#pragma unroll
+                for (int tc = 0; tc < NTC; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
+            if constexpr (NZM == 16) {
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
+            } else {
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][NTC - 1], acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][NTC - 1], w[u] * a[u][NTC - 1], acc[2], 0, 0, 0);
+            }
         }
     }
-    if (t0 < cnt) {                      // cnt is a multiple of 4
-        const double *r0 = rows + (t0 + kq) * LDR;
-        const double w0 = w[t0 + kq];
-        if constexpr (NZM == 16) {
-            const double a0 = r0[li];
-            acc0[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * a0, acc0[0], 0, 0, 0);
-        } else {
-            const double a0 = r0[li], b0 = r0[16 + li];
-            acc0[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * a0, acc0[0], 0, 0, 0);
-            acc0[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a0, w0 * b0, acc0[1], 0, 0, 0);
-            acc0[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(b0, w0 * b0, acc0[2], 0, 0, 0);
+    if (RHS) {
+#pragma unroll
+        for (int tc = 0; tc < NTC; tc++) {
+            const double sv = chunk_sum16(ps[tc]);
+            if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
         }
     }
 #pragma unroll
     for (int q = 0; q < 4; q++) {
         const int r = kq + 4 * q;
-        out[r * LDH + li] = acc0[0][q] + acc1[0][q];
+        H[r * LDH + li] = acc[0][q];
         if constexpr (NZM == 32) {
-            const double v01 = acc0[1][q] + acc1[1][q];
-            out[r * LDH + 16 + li] = v01;
-            out[(16 + li) * LDH + r] = v01;
-            out[(16 + r) * LDH + 16 + li] = acc0[2][q] + acc1[2][q];
+            H[r * LDH + 16 + li] = acc[1][q];
+            H[(16 + li) * LDH + r] = acc[1][q];
+            H[(16 + r) * LDH + 16 + li] = acc[2][q];
         }
     }
 }
 
-// out[a] = sum_t c_t r_t[a] for a < nz (VALU): lane (a, chunk) sums the terms of its chunk,
-// the chunks combine by permlane swaps.  cnt is a multiple of 4.
-template <int NZM>
-__device__ __forceinline__ void rmul(const double *rows, const double *cf, int cnt, double *out, int nz, int lane)
+// g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping as gram_rhs, eight term
+// groups per batch so that 16 LDS loads are in flight before the FMAs need them.
+template <int NZL>
+__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, double *g, int nz, int lane)
 {
-    constexpr int LDR = NZM + 1;
-    constexpr int NCH = 64 / NZM;            // term chunks (4 or 2)
-    const int a = lane % NZM, q = lane / NZM;
-    double s0 = 0.0, s1 = 0.0;
-    int t = q;
-    for (; t + NCH < cnt; t += 2 * NCH) {
-        s0 = fma(cf[t], rows[t * LDR + a], s0);
-        s1 = fma(cf[t + NCH], rows[(t + NCH) * LDR + a], s1);
+    constexpr int NZM = ((NZL + 15) / 16) * 16;
+    constexpr int LDR = NZL + 1, NTC = NZM / 16;
+    const int li = lane & 15, kq = lane >> 4;
+    double ps[2][NTC];
+#pragma unroll
+    for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
+    int t0 = 0;
+    for (; t0 + 32 <= cnt; t0 += 32) {
+        double a[8][NTC], c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int r = t0 + 4 * u + kq;
+            c[u] = CF[r];
+#pragma unroll
+            for (int tc = 0; tc < NTC; tc++) a[u][tc] = (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0;
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+            for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
     }
-    if (t < cnt) s0 = fma(cf[t], rows[t * LDR + a], s0);
-    double s = s0 + s1;
-    s = (NZM == 16) ? chunk_sum16(s) : chunk_sum32(s);
-    if (q == 0 && a < nz) out[a] = s;
+    for (; t0 < cnt; t0 += 4) {
+        const int r = t0 + kq;
+        const double cc = CF[r];
+#pragma unroll
+        for (int tc = 0; tc < NTC; tc++) ps[0][tc] = fma(cc, (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0, ps[0][tc]);
+    }
+#pragma unroll
+    for (int tc = 0; tc < NTC; tc++) {
+        const double sv = chunk_sum16(ps[0][tc] + ps[1][tc]);
+        if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
+    }
 }
 
 // dot of LDS term row (lane-parallel rows) with a wave-uniform vector held in registers
@@ -241,30 +296,38 @@ __device__ __forceinline__ double row_dot(const double *row, const double (&v)[N
 
 // --------------------------------------------------------------------------- Gauss-Jordan
 // In-place inverse of the nz x nz SPD matrix held one row per lane (lane i: A[0..NZL)),
-// rows/columns >= nz padded with the identity.  Step k: the pivot row is broadcast by
-// v_readlane; every lane updates its row.  The pivots are those of LDL' in natural order,
-// so pivot <= 0 <=> not positive definite; regularise != 0 applies iSWIFT's dynamic pivot
-// regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7).  Returns 0 on success (uniform).
+// rows/columns >= nz padded with the identity.  Step k broadcasts the pivot row by
+// v_readlane and every other lane eliminates column k from its row; the pivot row itself is
+// not scaled (each lane keeps 1 / its own pivot and scales its row once at the end), so a
+// step is one multiplier and one FMA per entry.  The pivots are those of LDL' in natural
+// order, so pivot <= 0 <=> not positive definite; regularise != 0 applies iSWIFT's dynamic
+// pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7).  Returns 0 on success.
 template <int NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
     int fail = 0;
+    double dinv = 1.0;
 #pragma unroll
     for (int k = 0; k < NZL; k++) {
-        if (k >= nz) break;
-        double piv = readlane_d(A[k], k);
-        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
-        fail |= !(piv > 0.0);
-        const double inv = rcp_d(piv);
-        double rk[NZL];
+        if (k < nz) {
+            double piv = readlane_d(A[k], k);
+            if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+            fail |= !(piv > 0.0);
+            const double inv = rcp_d(piv);
+            double rk[NZL];
 #pragma unroll
-        for (int j = 0; j < NZL; j++) rk[j] = readlane_d(A[j], k);
-        const double fi = A[k] * inv;
-        const bool me = lane == k;
+            for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
+            const bool me = lane == k;
+            const double f = me ? 0.0 : A[k] * inv;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) A[j] = me ? rk[j] * inv : fma(-fi, rk[j], A[j]);
-        A[k] = me ? inv : -fi;
+            for (int j = 0; j < NZL; j++)
+                if (j != k) A[j] = fma(-f, rk[j], A[j]);
+            A[k] = me ? 1.0 : -f;
+            dinv = me ? inv : dinv;
+        }
     }
+#pragma unroll
+    for (int j = 0; j < NZL; j++) A[j] *= dinv;
     return fail;
 }
 
@@ -397,10 +460,53 @@ __device__ __forceinline__ void knn_select(int lane, double px, double py, const
     }
 }
 
+// --------------------------------------------------------------------------- slots
+// Every inequality row of the problem belongs to a SLOT: a bound pair on one scalar
+// function f of x (row 0: f <= h0, row 1: -f <= h1; a single row has row 1 off) whose
+// Jacobian, reduced by Z, is one term row of R.  Slot s lives in registers of lane s % 64
+// (trip s / 64) for the whole solve.  Kinds, in slot order:
+//   VAR  s in [0, n):            f = x_v (v = s), box +-1e3 on X/U, [0, 1] on lambda, none on
+//                                the slack; also carries rx_v, P_v, c_v; term row v (Z row)
+//   COP  [n, n + 2(N-1)):        f = p_i - u_{i+1}, +-mu h / sqrt 2; term row M_e
+//   VEL  [.., + 2N) (NLP):       f = xdot_k / ydot_k, +-vsat; adds into term row v
+//   OBS  [.., + N K) (NLP):      f = -|p_k - o_kj|^2 - s, single row <= -eps_j; term row M_o
+// so residuals, Newton rows, step lengths and updates are one straight-line code path.
+enum { K_NONE = 0, K_VAR = 1, K_COP = 2, K_VEL = 3, K_OBS = 4 };
+
+struct Slot {
+    double s[2], z[2], iz[2], is[2], dz[2], ds[2], dsT[2], r3[2];
+    double h[2];        // row bounds
+    double a0, a1, rx;  // VAR: P_v, c_v ; OBS: o_x, o_y
+    double jd;          // J dx of the latest Newton solve (VAR: dx_v)
+    double m[2];        // 1.0 / 0.0: row active in the current stage (arithmetic masks keep
+                        // per-lane flags in VGPRs instead of long-lived SGPR lane masks)
+    int i0, i1, r;      // xs indices of f, term row
+    int wr;             // row this slot stores W / CF to (a scratch entry for VEL / unused slots)
+    int kind;
+};
+
+// kind read through an opaque copy: comparisons on it are recomputed at each use instead
+// of being hoisted into lane masks that stay live across the whole iteration
+__device__ __forceinline__ int kind_of(const Slot &q)
+{
+    int k = q.kind;
+    asm volatile("" : "+v"(k));
+    return k;
+}
+
+__device__ __forceinline__ double slot_f(const Slot &q, const double *xs, double s_var)
+{
+    const double x0 = xs[q.i0], x1 = xs[q.i1];
+    const int k = kind_of(q);
+    const double dx = x0 - q.a0, dy = x1 - q.a1;
+    return (k == K_OBS) ? -(dx * dx + dy * dy) - s_var : (k == K_COP) ? x0 - x1 : x0;
+}
+
+
+
 // --------------------------------------------------------------------------- main kernel
-// NZL: register bound on nz (rows of the reduced system, one per lane); TV / TO: trips of
-// 64 variable / obstacle slots.  CoM-CoP slots use one trip (N <= 33).
-template <int NZL, int TV, int TO>
+// NZL: register bound on nz (one reduced-matrix row per lane); TS: trips of 64 slots.
+template <int NZL, int TS>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
                 const double *__restrict__ obstacles, int n_obs,
@@ -410,20 +516,23 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 double *lds)
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
-    constexpr int LDR = NZM + 1, LDH = NZM + 1;
+    constexpr int LDR = NZL + 1, LDH = NZM + 1;
     const int lane = threadIdx.x;
     const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz;
     const int NK = N * K, NE = 2 * (N - 1);
-    const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK);
-    const int TT = n4 + E4 + NK4;                       // term rows: variables | CoM-CoP | obstacles
+    const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N);
+    // term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | obstacles (NK4) | 4 zero rows
+    const int rC = 4 * N, rU = rC + E4, rO = rU + UL4, TT = (rO + NK4 + 15) & ~15;
+    const TermLayout TL{N, C, n, nz, E4};
+    const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK;
     const double tol = prm.tol, th = tol / sqrt(3.0);
     STAMP_DECL;
 
     // ---- LDS carve (must match srb_lds_doubles)
     double *p = lds;
     double *R = p; p += TT * LDR;                       // term rows (Z rows first)
-    double *W = p; p += TT;                             // gram weights
-    double *CF = p; p += TT;                            // rhs coefficients
+    double *W = p; p += TT + 1;                         // gram weights (+ one scratch entry)
+    double *CF = p; p += TT + 1;                        // rhs coefficients (+ one scratch entry)
     double *H0 = p; p += NZM * LDH;                     // assembled Z'HZ (delta = 0)
     double *HS = p; p += NZM * LDH;                     // Z'HZ + delta Z'Z (when delta != 0)
     double *ZZ = p; p += NZM * LDH;                     // Z'Z (NLP)
@@ -436,8 +545,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double *eps = p; p += K + 1;
     double *zo = p; p += NK4;                           // obstacle duals (per-grid sums)
     int *sel = (int *)p; p += (K + 1);
-    double *Rt = R + n4 * LDR;                          // CoM-CoP rows, then obstacle rows
-    double *Ro = Rt + E4 * LDR;
+#ifdef SRB_STAMPS
+    unsigned long long *stamp_lds = (unsigned long long *)p; p += SRB_NSTAMP;
+    stamp_lds[lane] = 0;
+#endif
+    double *Rt = R + rC * LDR;                          // CoM-CoP rows
 
     STAMP_BEGIN();
     // ---- load inputs (a1/a2/a3: x0, reference window, footholds); zero the padded tables
@@ -470,9 +582,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         double g0 = 0.0, g1 = 0.0;
         if (!is_null)
             for (int i = 0; i < C; i++) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; }
-        for (int i = 0; i < C; i++) R[(6 * N + C * j + i) * LDR + col] = lam[i];
-        R[(4 * N + 2 * j) * LDR + col] = g0;
-        R[(4 * N + 2 * j + 1) * LDR + col] = g1;
+        for (int i = 0; i < C; i++) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i];
+        R[TL.zr(4 * N + 2 * j) * LDR + col] = g0;
+        R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = g1;
         double v[4];
         for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1;
         for (int k = j; k < N; k++) {
@@ -482,49 +594,44 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int d = 0; d < 4; d++) v[d] = tt[d];
         }
     }
-    if (lane == 0) R[(n - 1) * LDR + nz - 1] = 1.0;
+    if (lane == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0;
     SYNC();
-    // CoM-CoP term rows M_e = Z_p - Z_u (p = CoM position of grid i, u = CoP of grid i+1)
-    const int e_i = lane >> 1, e_d = lane & 1;
-    const int e_p = 4 * e_i + 2 * e_d, e_u = 4 * N + 2 * (e_i + 1) + e_d;
-    const bool e_on = lane < NE;
-    if (e_on)
-        for (int a = 0; a < NZM; a++) Rt[lane * LDR + a] = R[e_p * LDR + a] - R[e_u * LDR + a];
+    // CoM-CoP term rows M_e = Z_p - Z_u (p = CoM position of grid i, u = CoP of grid i+1); xs = xbar
+    if (lane < NE) {
+        const int i = lane >> 1, d = lane & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d;
+        for (int a = 0; a < NZL; a++) Rt[lane * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a];
+    }
+    for (int v = lane; v < n; v += WAVE) xs[v] = xb[v];
 
     // ---- slot constants
-    // variable slots: v = lane + 64 t
-    double xv[TV], rx[TV], Pv[TV], cv[TV], hAp[TV], hAm[TV];
-    bool vok[TV], aon[TV], vel[TV], pos[TV];
-    Pair A[TV], B[TV];
+    Slot Q[TS];
 #pragma unroll
-    for (int t = 0; t < TV; t++) {
-        const int v = lane + 64 * t;
-        vok[t] = v < n;
-        const bool isX = v < 4 * N, isU = !isX && v < 6 * N, isL = !isX && !isU && v < n - 1;
-        Pv[t] = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : isL ? 0.0 : (v == n - 1 ? prm.Sw : 0.0);
-        cv[t] = isX ? -Pv[t] * ref[v] : 0.0;
-        xv[t] = vok[t] ? xb[v] : 0.0;
-        rx[t] = 0.0;
-        aon[t] = vok[t] && v < n - 1;
-        hAp[t] = isL ? 1.0 : prm.box;
-        hAm[t] = isL ? 0.0 : prm.box;
-        vel[t] = isX && (v & 1);
-        pos[t] = isX && !(v & 1);
+    for (int t = 0; t < TS; t++) {
+        Slot &q = Q[t];
+        const int sl = lane + 64 * t;
+        q.kind = K_NONE; q.i0 = q.i1 = 0; q.r = 0; q.h[0] = q.h[1] = 0.0; q.a0 = q.a1 = 0.0; q.rx = 0.0; q.jd = 0.0;
+        q.m[0] = q.m[1] = 0.0; q.wr = TT;
+        if (sl < sE) {                                   // VAR
+            const int v = sl;
+            const bool isX = v < 4 * N, isU = !isX && v < 6 * N, isL = !isX && !isU && v < n - 1;
+            q.kind = K_VAR; q.i0 = q.i1 = v; q.r = TL.zr(v);
+            q.a0 = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : isL ? 0.0 : prm.Sw;
+            q.a1 = isX ? -q.a0 * ref[v] : 0.0;
+            q.h[0] = isL ? 1.0 : prm.box; q.h[1] = isL ? 0.0 : prm.box;
+        } else if (sl < sV) {                            // COP
+            const int e = sl - sE, i = e >> 1, d = e & 1;
+            q.kind = K_COP; q.i0 = 4 * i + 2 * d; q.i1 = 4 * N + 2 * (i + 1) + d; q.r = rC + e;
+            q.h[0] = q.h[1] = prm.fr;
+        } else if (sl < sO) {                            // VEL
+            const int tt = sl - sV, comp = (tt < N) ? 1 : 3, k = tt % N;
+            q.kind = K_VEL; q.i0 = q.i1 = 4 * k + comp; q.r = 4 * k + comp;
+            q.h[0] = q.h[1] = prm.vsat;
+        } else if (sl < S) {                             // OBS (positions filled at the NLP stage)
+            const int o = sl - sO, k = o / K;
+            q.kind = K_OBS; q.i0 = 4 * k; q.i1 = 4 * k + 2; q.r = rO + o;
+        }
 #pragma unroll
-        for (int r = 0; r < 2; r++) { A[t].s[r] = A[t].z[r] = B[t].s[r] = B[t].z[r] = 1.0; }
-    }
-    Pair E;                                                  // CoM-CoP slot (one trip)
-    E.s[0] = E.s[1] = E.z[0] = E.z[1] = 1.0;
-    const double fr = prm.fr;
-    // obstacle slots: o = lane + 64 t  (grid k = o / K, obstacle j = o % K)
-    Pair O[TO];
-    bool ook[TO];
-    int ok_[TO];
-    double ox[TO], oy[TO], oh[TO];
-#pragma unroll
-    for (int t = 0; t < TO; t++) {
-        O[t].s[0] = O[t].z[0] = 1.0;
-        ook[t] = false; ok_[t] = 0; ox[t] = oy[t] = 0.0; oh[t] = 0.0;
+        for (int r = 0; r < 2; r++) { q.s[r] = q.z[r] = 1.0; q.iz[r] = q.is[r] = 1.0; q.dz[r] = q.ds[r] = q.dsT[r] = q.r3[r] = 0.0; }
     }
     double Mi[NZL];                                          // inverse of the reduced Newton matrix (row = lane)
     double dxi[NZL];                                         // Newton direction in xi (uniform)
@@ -535,99 +642,81 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
-    const int nchunk_v = (n + 63) / 64, nchunk_o = (NK + 63) / 64;
     // One loop over the two stages so that the interior-point iteration exists once in the
     // code object (keeps the hot loop small for the instruction cache).
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
-        int mrows = 0;                                        // active rows (m)
-        int cnt = n4 + E4 + (nl ? NK4 : 0);                   // term rows in this stage
+        STAMP_STAGE(stage);
+        const int nts = ((nl ? S : sV) + 63) / 64;            // active slot trips
+        const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
+        const int cnt = ((nl ? rO + NK4 : rO) + 15) & ~15;     // term rows in this stage (zero-padded to 16)
         STAMP_BEGIN();
+        // stage activity of each row
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            Slot &q = Q[t];
+            const bool lin = (q.kind == K_VAR && q.i0 < n - 1) || q.kind == K_COP;
+            q.m[0] = (lin || (nl && (q.kind == K_VEL || q.kind == K_OBS))) ? 1.0 : 0.0;
+            q.m[1] = (lin || (nl && q.kind == K_VEL)) ? 1.0 : 0.0;
+            q.wr = (q.kind == K_VAR || q.kind == K_COP || q.kind == K_OBS) ? q.r : TT;
+        }
         if (!nl) {
             // ---------------- QP stage setup: kkt_initialize (Auxilary.c:680-755) ----------------
-            // [P A' G'; A 0 0; G 0 -I] [x; y; z] = [-c; b; h]  ->  reduced:  (Z'(P + G'G)Z) xi = -Z'(P xbar + c) + Z'G'(h - G xbar)
-            mrows = 2 * NE + 2 * (6 * N) + 2 * C * N;         // 4(N-1) + 12N + 2CN
+            // [P A' G'; A 0 0; G 0 -I] [x; y; z] = [-c; b; h]:  (Z'(P + G'G)Z) xi = -Z'(P xbar + c) + Z'G'(h - G xbar)
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    const int v = lane + 64 * t;
-                    const double wA = aon[t] ? 2.0 : 0.0;
-                    // w = r3 = h - G xbar on both rows of pair A
-                    const double wp = hAp[t] - xv[t], wm = hAm[t] + xv[t];
-                    if (v < n4) {
-                        W[v] = vok[t] ? Pv[t] + wA : 0.0;
-                        CF[v] = vok[t] ? (-cv[t] - Pv[t] * xv[t]) + (aon[t] ? (wp - wm) : 0.0) : 0.0;
-                    }
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    const double f = slot_f(q, xs, 0.0);
+                    const double w0 = q.m[0] * (q.h[0] - f), w1 = q.m[1] * (q.h[1] + f);
+                    const bool var = q.kind == K_VAR;
+                    const double wgt = (var ? q.a0 : 0.0) + q.m[0] + q.m[1];
+                    const double cfv = (var ? -q.a1 - q.a0 * f : 0.0) + (w0 - w1);
+                    if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
-            {
-                const double ge = e_on ? xb[e_p] - xb[e_u] : 0.0;
-                if (lane < E4) { W[n4 + lane] = e_on ? 2.0 : 0.0; CF[n4 + lane] = e_on ? ((fr - ge) - (fr + ge)) : 0.0; }
-            }
             SYNC();
-            gram<NZM>(R, W, cnt, H0, lane);
-            rmul<NZM>(R, CF, cnt, vg, nz, lane);
+            gram_rhs<NZL, true>(R, W, CF, cnt, H0, vg, nz, lane);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
             if (gj_invert<NZL>(Mi, nz, lane, 1) != 0) {
-                qp_flag = 1;
-                // x stays xbar (as the reference, the last iterate is returned)
-#pragma unroll
-                for (int t = 0; t < TV; t++) if (t < nchunk_v && vok[t]) xs[lane + 64 * t] = xv[t];
-                SYNC();
+                qp_flag = 1;                                  // x stays xbar (last iterate is returned)
                 continue;
             }
             la_solve<NZL>(Mi, H0, vg, vy, vr, vd, dxi, nz, lane);
             // x = xbar + Z xi ; zi = h - G x ; s, z shifted (Auxilary.c:716-746)
             double mn = 1e300, mx = -1e300;
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    const int v = lane + 64 * t;
-                    const double dx = row_dot<NZL>(R + (v < n4 ? v : 0) * LDR, dxi);
-                    if (vok[t]) xv[t] += dx;
-                    if (aon[t]) {
-                        const double zp = hAp[t] - xv[t], zm = hAm[t] + xv[t];
-                        A[t].s[0] = zp; A[t].s[1] = zm;               // zi, shifted below
-                        mn = fmin(mn, fmin(zp, zm)); mx = fmax(mx, fmax(zp, zm));
-                    }
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    const double f = slot_f(q, xs, 0.0) + row_dot<NZL>(R + q.r * LDR, dxi);
+                    q.jd = f;                                 // f(x) for the shift below
+                    const double z0 = q.h[0] - f, z1 = q.h[1] + f;
+                    if (q.m[0] != 0.0) { mn = fmin(mn, z0); mx = fmax(mx, z0); }
+                    if (q.m[1] != 0.0) { mn = fmin(mn, z1); mx = fmax(mx, z1); }
                 }
-            double ge = 0.0;
-            if (e_on) {
-                ge = xb[e_p] - xb[e_u] + row_dot<NZL>(Rt + lane * LDR, dxi);
-                const double zp = fr - ge, zm = fr + ge;
-                E.s[0] = zp; E.s[1] = zm;
-                mn = fmin(mn, fmin(zp, zm)); mx = fmax(mx, fmax(zp, zm));
-            }
-            mn = wmin(mn); mx = wmax(mx);
-            const double sa = -mn, za = mx;
-            const double ssh = (sa < 0) ? 0.0 : 1.0 + sa, zsh = (za < 0) ? 0.0 : 1.0 + za;
+            double rv[2] = {-mn, mx};
+            wred<2, 3u>(rv);
+            mn = -rv[0]; mx = rv[1];
+            const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn, zsh = (mx < 0) ? 0.0 : 1.0 + mx;
+            SYNC();                                           // every lane has read xs = xbar
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-#pragma unroll
-                    for (int r = 0; r < 2; r++) {
-                        const double zi = A[t].s[r];
-                        A[t].s[r] = aon[t] ? zi + ssh : 1.0;
-                        A[t].z[r] = aon[t] ? -zi + zsh : 1.0;
-                    }
-                    if (vok[t]) xs[lane + 64 * t] = xv[t];
-                    rx[t] = 0.0;      // = G'(dz_init - z) = -(1+za) G'1 = 0: every G row comes in a +- pair
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    const double f = q.jd, z0 = q.h[0] - f, z1 = q.h[1] + f;
+                    q.s[0] = (q.m[0] != 0.0) ? z0 + ssh : 1.0; q.z[0] = (q.m[0] != 0.0) ? -z0 + zsh : 1.0;
+                    q.s[1] = (q.m[1] != 0.0) ? z1 + ssh : 1.0; q.z[1] = (q.m[1] != 0.0) ? -z1 + zsh : 1.0;
+                    if (q.kind == K_VAR) xs[q.i0] = f;
+                    q.rx = 0.0;      // = G'(dz_init - z) = -(1+za) G'1 = 0: every G row comes in a +- pair
                 }
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const double zi = E.s[r];
-                E.s[r] = e_on ? zi + ssh : 1.0;
-                E.z[r] = e_on ? -zi + zsh : 1.0;
-            }
             SYNC();
             STAMP_END(1);
         } else {
             // ---------------- NLP stage setup (replaces SnoptSolver::Solve, MPC_dist.cpp:402-427) ----------------
             if (x_qp_out)
-#pragma unroll
-                for (int t = 0; t < TV; t++) if (t < nchunk_v && vok[t]) x_qp_out[(size_t)agent * n + lane + 64 * t] = xv[t];
-            mrows = 2 * NE + 2 * (6 * N) + 2 * C * N + NK + 4 * N;
+                for (int v = lane; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = xs[v];
             // obstacles per grid: the K_obs nearest static obstacles (MPC_dist.cpp:371-396,
             // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
             // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
@@ -653,85 +742,54 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             }
             SYNC();
             // slacks: shifted h - g(x) over every NLP row; duals 1
+            const double s_var = xs[n - 1];
             double mn = 1e300;
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    if (aon[t]) mn = fmin(mn, fmin(hAp[t] - xv[t], hAm[t] + xv[t]));
-                    if (vel[t]) mn = fmin(mn, fmin(prm.vsat - xv[t], prm.vsat + xv[t]));
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    if (q.kind == K_OBS) {
+                        const int o = lane + 64 * t - sO;
+                        q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K];
+                    }
+                    const double f = slot_f(q, xs, s_var);
+                    q.jd = f;
+                    if (q.m[0] != 0.0) mn = fmin(mn, q.h[0] - f);
+                    if (q.m[1] != 0.0) mn = fmin(mn, q.h[1] + f);
                 }
-            const double ge0 = e_on ? xs[e_p] - xs[e_u] : 0.0;
-            if (e_on) mn = fmin(mn, fmin(fr - ge0, fr + ge0));
-            const double s_var = xs[n - 1];
-#pragma unroll
-            for (int t = 0; t < TO; t++) {
-                const int o = lane + 64 * t;
-                ook[t] = o < NK;
-                const int k = ook[t] ? o / K : 0, j = ook[t] ? o - (o / K) * K : 0;
-                ok_[t] = k;
-                ox[t] = ook[t] ? obs[2 * o] : 0.0; oy[t] = ook[t] ? obs[2 * o + 1] : 0.0;
-                oh[t] = ook[t] ? -eps[j] : 0.0;
-                if (ook[t]) {
-                    const double dx = xs[4 * k] - ox[t], dy = xs[4 * k + 2] - oy[t];
-                    const double g = -(dx * dx + dy * dy) - s_var;
-                    mn = fmin(mn, oh[t] - g);
-                }
-            }
             mn = wmin(mn);
-            const double sa = -mn, ssh = (sa < 0) ? 0.0 : 1.0 + sa;
+            const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn;
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    A[t].s[0] = aon[t] ? hAp[t] - xv[t] + ssh : 1.0;
-                    A[t].s[1] = aon[t] ? hAm[t] + xv[t] + ssh : 1.0;
-                    B[t].s[0] = vel[t] ? prm.vsat - xv[t] + ssh : 1.0;
-                    B[t].s[1] = vel[t] ? prm.vsat + xv[t] + ssh : 1.0;
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    const double f = q.jd;
+                    q.s[0] = (q.m[0] != 0.0) ? q.h[0] - f + ssh : 1.0;
+                    q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
+                    q.z[0] = q.z[1] = 1.0;
+                    if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x
+                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
 #pragma unroll
-                    for (int r = 0; r < 2; r++) { A[t].z[r] = 1.0; B[t].z[r] = 1.0; }
+                        for (int a = 0; a < NZL; a++)
+                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                    }
+                    // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = 1: J'1 vanishes on every
+                    // +- pair, leaving the obstacle rows
+                    if (q.kind == K_VAR) { W[q.r] = 1.0; CF[q.r] = fma(q.a0, f, q.a1); }
+                    else if (q.kind == K_COP) { W[q.r] = 0.0; CF[q.r] = 0.0; }
+                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = 1.0; }
                 }
-            E.s[0] = e_on ? fr - ge0 + ssh : 1.0;
-            E.s[1] = e_on ? fr + ge0 + ssh : 1.0;
-            E.z[0] = E.z[1] = 1.0;
-#pragma unroll
-            for (int t = 0; t < TO; t++) {
-                const int o = lane + 64 * t, k = ok_[t];
-                const double dx = xs[4 * k] - ox[t], dy = xs[4 * k + 2] - oy[t];
-                const double g = -(dx * dx + dy * dy) - s_var;
-                O[t].s[0] = ook[t] ? oh[t] - g + ssh : 1.0;
-                O[t].z[0] = 1.0;
-                // M_o = J_o Z at the current x
-                const double jx = -2.0 * dx, jy = -2.0 * dy;
-                if (o < NK4)
-#pragma unroll
-                    for (int a = 0; a < NZM; a++)
-                        Ro[o * LDR + a] = ook[t] ? fma(jx, R[(4 * k) * LDR + a], jy * R[(4 * k + 2) * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0) : 0.0;
-            }
-            // Z'Z (delta shifts) and the projection rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = 1:
-            // J'1 vanishes on every +- pair, leaving the obstacle rows.
-#pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    const int v = lane + 64 * t;
-                    if (v < n4) { W[v] = vok[t] ? 1.0 : 0.0; CF[v] = vok[t] ? fma(Pv[t], xv[t], cv[t]) : 0.0; }
-                }
-            if (lane < E4) { W[n4 + lane] = 0.0; CF[n4 + lane] = 0.0; }
-#pragma unroll
-            for (int t = 0; t < TO; t++) {
-                const int o = lane + 64 * t;
-                if (o < NK4) { W[n4 + E4 + o] = 0.0; CF[n4 + E4 + o] = ook[t] ? 1.0 : 0.0; }
-            }
             SYNC();
-            gram<NZM>(R, W, n4, ZZ, lane);
-            rmul<NZM>(R, CF, cnt, vg, nz, lane);
+            gram_rhs<NZL, true>(R, W, CF, cnt, ZZ, vg, nz, lane);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_invert<NZL>(Mi, nz, lane, 0);
             la_solve<NZL>(Mi, ZZ, vg, vy, vr, vd, dxi, nz, lane);
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    const int v = lane + 64 * t;
-                    rx[t] = vok[t] ? -row_dot<NZL>(R + (v < n4 ? v : 0) * LDR, dxi) : 0.0;
+            for (int t = 0; t < TS; t++)
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    q.rx = (q.kind == K_VAR) ? -row_dot<NZL>(R + q.r * LDR, dxi) : 0.0;
                 }
             SYNC();
             STAMP_END(2);
@@ -747,55 +805,38 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             STAMP_BEGIN();
             // ---- residuals (computeresiduals, Auxilary.c:524-553), norms, reciprocals
             const double s_var = xs[n - 1];
-            const double ge = e_on ? xs[e_p] - xs[e_u] : 0.0;
-            double go[TO];
             double nrx = 0.0, nrz = 0.0, sz = 0.0, gm = 1.0;
+            double fv[TS];
 #pragma unroll
-            for (int t = 0; t < TV; t++)
-                if (t < nchunk_v) {
-                    nrx = fma(rx[t], rx[t], nrx);
-                    if (nl && vok[t]) gm = fmax(gm, fabs(fma(Pv[t], xv[t], cv[t])));
+            for (int t = 0; t < TS; t++) {
+                fv[t] = 0.0;
+                if (t < nts) {
+                    Slot &q = Q[t];
+                    const double f = slot_f(q, xs, s_var);
+                    fv[t] = f;
+                    if (kind_of(q) == K_VAR) {
+                        nrx = fma(q.rx, q.rx, nrx);
+                        gm = fmax(gm, fabs(fma(q.a0, f, q.a1)));
+                    }
+                    const double rz0 = q.h[0] - q.s[0] - f, rz1 = q.h[1] - q.s[1] + f;
+                    nrz = fma(q.m[0] * rz0, rz0, fma(q.m[1] * rz1, rz1, nrz));
+                    sz = fma(q.m[0] * q.s[0], q.z[0], fma(q.m[1] * q.s[1], q.z[1], sz));
 #pragma unroll
-                    for (int r = 0; r < 2; r++) {
-                        const double rzA = rz_of(A[t], r, xv[t], r ? hAm[t] : hAp[t]);
-                        const double rzB = rz_of(B[t], r, xv[t], prm.vsat);
-                        const bool bon = nl && vel[t];
-                        nrz += (aon[t] ? rzA * rzA : 0.0) + (bon ? rzB * rzB : 0.0);
-                        sz += (aon[t] ? A[t].s[r] * A[t].z[r] : 0.0) + (bon ? B[t].s[r] * B[t].z[r] : 0.0);
-                        A[t].iz[r] = rcp_d(A[t].z[r]); A[t].is[r] = rcp_d(A[t].s[r]);
-                        B[t].iz[r] = rcp_d(B[t].z[r]); B[t].is[r] = rcp_d(B[t].s[r]);
+                    for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
+                    if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z
+                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
+#pragma unroll
+                        for (int a = 0; a < NZL; a++)
+                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                        zo[q.r - rO] = q.z[0];
                     }
                 }
-#pragma unroll
-            for (int r = 0; r < 2; r++) {
-                const double rzE = rz_of(E, r, ge, fr);
-                nrz += e_on ? rzE * rzE : 0.0;
-                sz += e_on ? E.s[r] * E.z[r] : 0.0;
-                E.iz[r] = rcp_d(E.z[r]); E.is[r] = rcp_d(E.s[r]);
             }
-#pragma unroll
-            for (int t = 0; t < TO; t++) {
-                go[t] = 0.0;
-                if (nl && t < nchunk_o) {
-                    const int k = ok_[t];
-                    const double dx = xs[4 * k] - ox[t], dy = xs[4 * k + 2] - oy[t];
-                    go[t] = -(dx * dx + dy * dy) - s_var;
-                    const double rzO = rz_of(O[t], 0, go[t], oh[t]);
-                    nrz += ook[t] ? rzO * rzO : 0.0;
-                    sz += ook[t] ? O[t].s[0] * O[t].z[0] : 0.0;
-                    O[t].iz[0] = rcp_d(O[t].z[0]); O[t].is[0] = rcp_d(O[t].s[0]);
-                    // re-linearise: M_o = J_o(x) Z
-                    const double jx = -2.0 * dx, jy = -2.0 * dy;
-                    const int o = lane + 64 * t;
-                    if (o < NK4)
-#pragma unroll
-                        for (int a = 0; a < NZM; a++)
-                            Ro[o * LDR + a] = ook[t] ? fma(jx, R[(4 * k) * LDR + a], jy * R[(4 * k + 2) * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0) : 0.0;
-                    if (o < NK4) zo[o] = ook[t] ? O[t].z[0] : 0.0;
-                }
+            {
+                double rv[4] = {nrx, nrz, sz, gm};
+                wred<4, 8u>(rv);
+                nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3];
             }
-            nrx = sqrt(wsum(nrx)); nrz = sqrt(wsum(nrz)); sz = wsum(sz);
-            if (nl) gm = wmax(gm);
             const double mu = sz * inv_m;
             STAMP_END(3);
             if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
@@ -804,38 +845,73 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             if (nrx < thx && nrz < th && sz * inv_m < tol) { flag = 0; break; }
             const bool pc = nl || (sigma > sigma_d);
             double delta = 0.0;
+            // right-hand side of pass (0 predictor, 1 corrector / centring):
+            //   dsT, r3 = rz - dsT / z, w = om r3, coefficient of term row r = rx + J'w
+            auto set_rhs = [&](int pass) {
+                const double smu = (pass == 0) ? 0.0 : (pc ? sigma * mu : sigma_d * mu);
+                const bool corr = pass == 1 && pc;
+                double cfs[TS];
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    cfs[t] = 0.0;
+                    if (t < nts) {
+                        Slot &q = Q[t];
+                        const double f = fv[t];
+                        double cf = (kind_of(q) == K_VAR) ? q.rx : 0.0;
+#pragma unroll
+                        for (int r = 0; r < 2; r++) {
+                            double dsT = -q.s[r] * q.z[r];
+                            if (corr) dsT -= q.ds[r] * q.dz[r];
+                            dsT += smu;
+                            q.dsT[r] = dsT;
+                            const double rz = r ? (q.h[1] - q.s[1] + f) : (q.h[0] - q.s[0] - f);
+                            q.r3[r] = fma(-dsT, q.iz[r], rz);
+                            cf = fma((r ? -q.m[1] : q.m[0]) * q.z[r] * q.is[r], q.r3[r], cf);
+                        }
+                        cfs[t] = cf;
+                        CF[q.wr] = cf;
+                    }
+                }
+                if (nl)
+#pragma unroll
+                    for (int t = 0; t < TS; t++)
+                        if (t < nts && kind_of(Q[t]) == K_VEL)
+                            __hip_atomic_fetch_add(&CF[Q[t].r], cfs[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            };
             if (pc) {
                 // ---- weights W^-1 = z/s (updatekktmatrix, Auxilary.c:197-205), Lagrangian
-                //      Hessian -2 sum_j z_kj on (x_k, y_k) (NLP), assembly and factorisation
+                //      Hessian -2 sum_j z_kj on (x_k, y_k) (NLP), and the predictor right-hand
+                //      side; one pass over the term rows assembles Z'HZ and Z'(rx + J'w)
+                SYNC();
 #pragma unroll
-                for (int t = 0; t < TV; t++)
-                    if (t < nchunk_v) {
-                        const int v = lane + 64 * t;
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = Q[t];
+                        const double om = fma(q.m[0] * q.z[0], q.is[0], q.m[1] * q.z[1] * q.is[1]);
                         double hs = 0.0;
-                        if (nl && pos[t]) {
-                            const int k = v >> 2;
+                        if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
+                            const int k = q.i0 >> 2;
                             for (int j = 0; j < K; j++) hs += zo[k * K + j];
                             hs *= -2.0;
                         }
-                        const double wa = aon[t] ? A[t].z[0] * A[t].is[0] + A[t].z[1] * A[t].is[1] : 0.0;
-                        const double wb = (nl && vel[t]) ? B[t].z[0] * B[t].is[0] + B[t].z[1] * B[t].is[1] : 0.0;
-                        if (v < n4) W[v] = vok[t] ? Pv[t] + hs + wa + wb : 0.0;
+                        W[q.wr] = om + ((kind_of(q) == K_VAR) ? q.a0 + hs : 0.0);
                     }
-                if (lane < E4) W[n4 + lane] = e_on ? E.z[0] * E.is[0] + E.z[1] * E.is[1] : 0.0;
+                if (nl)
 #pragma unroll
-                for (int t = 0; t < TO; t++) {
-                    const int o = lane + 64 * t;
-                    if (nl && t < nchunk_o && o < NK4) W[n4 + E4 + o] = ook[t] ? O[t].z[0] * O[t].is[0] : 0.0;
-                }
+                    for (int t = 0; t < TS; t++)
+                        if (t < nts && kind_of(Q[t]) == K_VEL)
+                            __hip_atomic_fetch_add(&W[Q[t].r], Q[t].z[0] * Q[t].is[0] + Q[t].z[1] * Q[t].is[1], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+                set_rhs(0);
                 SYNC();
-                gram<NZM>(R, W, cnt, H0, lane);
+                gram_rhs<NZL, true>(R, W, CF, cnt, H0, vg, nz, lane);
                 SYNC();
                 STAMP_END(4);
                 double dstart = 0.0;
                 int ok = 0;
                 for (int tries = 0; tries < (nl ? 14 : 1); tries++) {
                     if (tries == 0) {       // scale-aware first shift: 1e-10 * max(1, max diag of Z'HZ)
-                        double dm = (lane < nz) ? H0[lane * LDH + lane] : 1.0;
+                        const double dm = (lane < nz) ? H0[lane * LDH + lane] : 1.0;
                         dstart = 1e-10 * fmax(1.0, wmax(dm));
                     }
                     gj_load<NZL>(Mi, H0, ZZ, delta, nz, lane);
@@ -858,119 +934,36 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             double ap = 1.0, ad = 1.0;
 #pragma clang loop unroll(disable)
             for (int pass = (pc ? 0 : 1); pass < 2; pass++) {
-                // right-hand side: dsT, r3 = rz - dsT / z, w = om r3, coef = rx + J'w
-                const double smu = (pass == 0) ? 0.0 : (pc ? sigma * mu : sigma_d * mu);
-#pragma unroll
-                for (int t = 0; t < TV; t++)
-                    if (t < nchunk_v) {
-                        const int v = lane + 64 * t;
-                        double cf = rx[t];
-#pragma unroll
-                        for (int r = 0; r < 2; r++) {
-                            const double sg = r ? -1.0 : 1.0;
-                            {
-                                Pair &q = A[t];
-                                double dsT = -q.s[r] * q.z[r];
-                                if (pass == 1 && pc) dsT -= q.ds[r] * q.dz[r];
-                                dsT += smu;
-                                q.dsT[r] = dsT;
-                                q.r3[r] = fma(-dsT, q.iz[r], rz_of(q, r, xv[t], r ? hAm[t] : hAp[t]));
-                                if (aon[t]) cf = fma(sg, q.z[r] * q.is[r] * q.r3[r], cf);
-                            }
-                            {
-                                Pair &q = B[t];
-                                double dsT = -q.s[r] * q.z[r];
-                                if (pass == 1 && pc) dsT -= q.ds[r] * q.dz[r];
-                                dsT += smu;
-                                q.dsT[r] = dsT;
-                                q.r3[r] = fma(-dsT, q.iz[r], rz_of(q, r, xv[t], prm.vsat));
-                                if (nl && vel[t]) cf = fma(sg, q.z[r] * q.is[r] * q.r3[r], cf);
-                            }
-                        }
-                        if (v < n4) CF[v] = vok[t] ? cf : 0.0;
-                    }
-                {
-                    double cf = 0.0;
-#pragma unroll
-                    for (int r = 0; r < 2; r++) {
-                        double dsT = -E.s[r] * E.z[r];
-                        if (pass == 1 && pc) dsT -= E.ds[r] * E.dz[r];
-                        dsT += smu;
-                        E.dsT[r] = dsT;
-                        E.r3[r] = fma(-dsT, E.iz[r], rz_of(E, r, ge, fr));
-                        cf = fma(r ? -1.0 : 1.0, E.z[r] * E.is[r] * E.r3[r], cf);
-                    }
-                    if (lane < E4) CF[n4 + lane] = e_on ? cf : 0.0;
+                if (pass == 1 || !pc) {
+                    set_rhs(pass);
+                    SYNC();
+                    STAMP_END(6 + 4 * pass);
+                    rhs_only<NZL>(R, CF, cnt, vg, nz, lane);
+                    SYNC();
+                    STAMP_END(7 + 4 * pass);
                 }
-#pragma unroll
-                for (int t = 0; t < TO; t++)
-                    if (nl && t < nchunk_o) {
-                        Pair &q = O[t];
-                        double dsT = -q.s[0] * q.z[0];
-                        if (pass == 1 && pc) dsT -= q.ds[0] * q.dz[0];
-                        dsT += smu;
-                        q.dsT[0] = dsT;
-                        q.r3[0] = fma(-dsT, q.iz[0], rz_of(q, 0, go[t], oh[t]));
-                        const int o = lane + 64 * t;
-                        if (o < NK4) CF[n4 + E4 + o] = ook[t] ? q.z[0] * q.is[0] * q.r3[0] : 0.0;
-                    }
-                SYNC();
-                STAMP_END(6 + 4 * pass);
-                rmul<NZM>(R, CF, cnt, vg, nz, lane);
-                SYNC();
-                STAMP_END(7 + 4 * pass);
                 la_solve<NZL>(Mi, Hsv, vg, vy, vr, vd, dxi, nz, lane);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
-                double dxv[TV];
 #pragma unroll
-                for (int t = 0; t < TV; t++) {
-                    dxv[t] = 0.0;
-                    if (t < nchunk_v) {
-                        const int v = lane + 64 * t;
-                        dxv[t] = vok[t] ? row_dot<NZL>(R + (v < n4 ? v : 0) * LDR, dxi) : 0.0;
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = Q[t];
+                        q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
-                            const double sg = r ? -1.0 : 1.0;
-                            {
-                                Pair &q = A[t];
-                                q.dz[r] = aon[t] ? q.z[r] * q.is[r] * fma(sg, dxv[t], -q.r3[r]) : 0.0;
-                                q.ds[r] = aon[t] ? fma(-q.s[r], q.dz[r], q.dsT[r]) * q.iz[r] : 0.0;
-                                mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
-                            }
-                            {
-                                Pair &q = B[t];
-                                const bool bon = nl && vel[t];
-                                q.dz[r] = bon ? q.z[r] * q.is[r] * fma(sg, dxv[t], -q.r3[r]) : 0.0;
-                                q.ds[r] = bon ? fma(-q.s[r], q.dz[r], q.dsT[r]) * q.iz[r] : 0.0;
-                                mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
-                            }
+                            q.dz[r] = q.m[r] * q.z[r] * q.is[r] * fma(r ? -1.0 : 1.0, q.jd, -q.r3[r]);
+                            q.ds[r] = q.m[r] * fma(-q.s[r], q.dz[r], q.dsT[r]) * q.iz[r];
+                            mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
                         }
                     }
-                }
-                {
-                    const double jd = e_on ? row_dot<NZL>(Rt + (e_on ? lane : 0) * LDR, dxi) : 0.0;
-#pragma unroll
-                    for (int r = 0; r < 2; r++) {
-                        const double sg = r ? -1.0 : 1.0;
-                        E.dz[r] = e_on ? E.z[r] * E.is[r] * fma(sg, jd, -E.r3[r]) : 0.0;
-                        E.ds[r] = e_on ? fma(-E.s[r], E.dz[r], E.dsT[r]) * E.iz[r] : 0.0;
-                        mxs = fmax(mxs, -E.ds[r] * E.is[r]); mxz = fmax(mxz, -E.dz[r] * E.iz[r]);
-                    }
-                }
-#pragma unroll
-                for (int t = 0; t < TO; t++)
-                    if (nl && t < nchunk_o) {
-                        const int o = lane + 64 * t;
-                        const double jd = ook[t] ? row_dot<NZL>(Ro + (o < NK4 ? o : 0) * LDR, dxi) : 0.0;
-                        Pair &q = O[t];
-                        q.dz[0] = ook[t] ? q.z[0] * q.is[0] * (jd - q.r3[0]) : 0.0;
-                        q.ds[0] = ook[t] ? fma(-q.s[0], q.dz[0], q.dsT[0]) * q.iz[0] : 0.0;
-                        mxs = fmax(mxs, -q.ds[0] * q.is[0]); mxz = fmax(mxz, -q.dz[0] * q.iz[0]);
-                    }
                 // findsteplength (Auxilary.c:271-294): 1 / max(-dv / v), 1 when no dv < 0
-                mxs = wmax(mxs); mxz = wmax(mxz);
+                {
+                    double rv[2] = {mxs, mxz};
+                    wred<2, 3u>(rv);
+                    mxs = rv[0]; mxz = rv[1];
+                }
                 ap = (mxs > 0.0) ? 1.0 / mxs : 1.0;
                 ad = (mxz > 0.0) ? 1.0 / mxz : 1.0;
                 STAMP_END(9 + 4 * pass);
@@ -978,19 +971,12 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     // rho = (s + ap ds)'(z + ad dz) / s'z ; sigma = min(1, rho)^3  (formrho, Prime.c:160-170)
                     double num = 0.0;
 #pragma unroll
-                    for (int t = 0; t < TV; t++)
-                        if (t < nchunk_v)
-#pragma unroll
-                            for (int r = 0; r < 2; r++) {
-                                const Pair &a = A[t], &b = B[t];
-                                num += aon[t] ? fma(ap, a.ds[r], a.s[r]) * fma(ad, a.dz[r], a.z[r]) : 0.0;
-                                num += (nl && vel[t]) ? fma(ap, b.ds[r], b.s[r]) * fma(ad, b.dz[r], b.z[r]) : 0.0;
-                            }
-#pragma unroll
-                    for (int r = 0; r < 2; r++) num += e_on ? fma(ap, E.ds[r], E.s[r]) * fma(ad, E.dz[r], E.z[r]) : 0.0;
-#pragma unroll
-                    for (int t = 0; t < TO; t++)
-                        if (nl && t < nchunk_o) num += ook[t] ? fma(ap, O[t].ds[0], O[t].s[0]) * fma(ad, O[t].dz[0], O[t].z[0]) : 0.0;
+                    for (int t = 0; t < TS; t++)
+                        if (t < nts) {
+                            const Slot &q = Q[t];
+                            num = fma(q.m[0] * fma(ap, q.ds[0], q.s[0]), fma(ad, q.dz[0], q.z[0]), num);
+                            num = fma(q.m[1] * fma(ap, q.ds[1], q.s[1]), fma(ad, q.dz[1], q.z[1]), num);
+                        }
                     num = wsum(num);
                     const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
                     sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
@@ -999,76 +985,68 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 // ---- update (Prime.c:208-216): step 0.99 alpha capped at 1
                 ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
                 ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
-                // new per-grid obstacle dual sums for the Jacobian-change term of rx
+                // rx' = (1-ad) rx + (ad-ap) P dx + ad (hess + delta) dx - (J(x') - J(x))' z'
+                // (hess from the old obstacle duals in zo, the Jacobian change from the new ones)
+                double hso[TS];
 #pragma unroll
-                for (int t = 0; t < TO; t++)
-                    if (nl && t < nchunk_o) {
-                        const int o = lane + 64 * t;
-                        O[t].s[0] = fma(ap, O[t].ds[0], O[t].s[0]);
-                        O[t].z[0] = fma(ad, O[t].dz[0], O[t].z[0]);
-                    }
-                // (the hess term uses the old duals still in zo)
-#pragma unroll
-                for (int t = 0; t < TV; t++)
-                    if (t < nchunk_v) {
-                        const int v = lane + 64 * t;
-                        double hs_old = 0.0;
-                        if (nl && pos[t]) {
-                            const int k = v >> 2;
-                            for (int j = 0; j < K; j++) hs_old += zo[k * K + j];
+                for (int t = 0; t < TS; t++) {
+                    hso[t] = 0.0;
+                    if (t < nts) {
+                        Slot &q = Q[t];
+                        if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
+                            const int k = q.i0 >> 2;
+                            for (int j = 0; j < K; j++) hso[t] += zo[k * K + j];
                         }
-                        rx[t] = (1.0 - ad) * rx[t] + ((ad - ap) * Pv[t]) * dxv[t];
-                        if (nl) rx[t] = fma(ad * (delta - 2.0 * hs_old), dxv[t], rx[t]);
-                        xv[t] = fma(ap, dxv[t], xv[t]);
 #pragma unroll
-                        for (int r = 0; r < 2; r++) {
-                            A[t].s[r] = fma(ap, A[t].ds[r], A[t].s[r]); A[t].z[r] = fma(ad, A[t].dz[r], A[t].z[r]);
-                            B[t].s[r] = fma(ap, B[t].ds[r], B[t].s[r]); B[t].z[r] = fma(ad, B[t].dz[r], B[t].z[r]);
-                        }
+                        for (int r = 0; r < 2; r++) { q.s[r] = fma(ap, q.ds[r], q.s[r]); q.z[r] = fma(ad, q.dz[r], q.z[r]); }
                     }
-#pragma unroll
-                for (int r = 0; r < 2; r++) {
-                    E.s[r] = fma(ap, E.ds[r], E.s[r]); E.z[r] = fma(ad, E.dz[r], E.z[r]);
                 }
-                SYNC();          // every lane has read the old duals
+                SYNC();          // every lane has read the old duals and x
 #pragma unroll
-                for (int t = 0; t < TO; t++)
-                    if (nl && t < nchunk_o) {
-                        const int o = lane + 64 * t;
-                        if (o < NK4) zo[o] = ook[t] ? O[t].z[0] : 0.0;
-                    }
-                SYNC();
-#pragma unroll
-                for (int t = 0; t < TV; t++)
-                    if (t < nchunk_v) {
-                        const int v = lane + 64 * t;
-                        if (nl && pos[t]) {      // -(J(x') - J(x))' z' on (x_k, y_k): +2 ap dx sum_j z'_kj
-                            const int k = v >> 2;
-                            double hs_new = 0.0;
-                            for (int j = 0; j < K; j++) hs_new += zo[k * K + j];
-                            rx[t] = fma(2.0 * ap * hs_new, dxv[t], rx[t]);
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = Q[t];
+                        if (nl && kind_of(q) == K_OBS) zo[q.r - rO] = q.z[0];
+                        if (kind_of(q) == K_VAR) {
+                            q.rx = (1.0 - ad) * q.rx + ((ad - ap) * q.a0) * q.jd;
+                            if (nl) q.rx = fma(ad * (delta - 2.0 * hso[t]), q.jd, q.rx);
+                            xs[q.i0] = fma(ap, q.jd, fv[t]);
                         }
-                        if (vok[t]) xs[v] = xv[t];
                     }
                 SYNC();
+                if (nl)
+#pragma unroll
+                    for (int t = 0; t < TS; t++)
+                        if (t < nts) {
+                            Slot &q = Q[t];
+                            if (kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {   // +2 ap dx sum_j z'_kj on (x_k, y_k)
+                                const int k = q.i0 >> 2;
+                                double hs_new = 0.0;
+                                for (int j = 0; j < K; j++) hs_new += zo[k * K + j];
+                                q.rx = fma(2.0 * ap * hs_new, q.jd, q.rx);
+                            }
+                        }
                 STAMP_END(14);
             }
             it++;
         }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
     }
+    SYNC();
     if (x_qp_out && nstage == 1)
-#pragma unroll
-        for (int t = 0; t < TV; t++) if (t < nchunk_v && vok[t]) x_qp_out[(size_t)agent * n + lane + 64 * t] = xv[t];
+        for (int v = lane; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = xs[v];
 
     // ---- outputs
     double f = 0.0;
 #pragma unroll
-    for (int t = 0; t < TV; t++)
-        if (t < nchunk_v && vok[t]) {
-            x_out[(size_t)agent * n + lane + 64 * t] = xv[t];
-            f += fma(0.5 * Pv[t] * xv[t], xv[t], cv[t] * xv[t]);
+    for (int t = 0; t < TS; t++) {
+        const Slot &q = Q[t];
+        if (q.kind == K_VAR) {
+            const double xv = xs[q.i0];
+            x_out[(size_t)agent * n + q.i0] = xv;
+            f += fma(0.5 * q.a0 * xv, xv, q.a1 * xv);
         }
+    }
     f = wsum(f);
     STAMP_END(15);
     STAMP_FLUSH(agent);
@@ -1079,8 +1057,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     }
 }
 
-#define SRB_NMPC_KERNEL(NZL, TV, TO)                                                                           \
-    extern "C" __global__ void __launch_bounds__(WAVE) srb_nmpc_kernel_##NZL##_##TV##_##TO(                   \
+#define SRB_NMPC_KERNEL(NZL, TS)                                                                               \
+    extern "C" __global__ void __launch_bounds__(WAVE) srb_nmpc_kernel_##NZL##_##TS(                          \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
@@ -1090,7 +1068,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        nmpc_agent<NZL, TV, TO>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
+        nmpc_agent<NZL, TS>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
                                 x_qp_out, x_out, obj_out, status_out, iters_out, lds);                         \
     }
 

@@ -1,4 +1,4 @@
-"""Diagnostic: per-phase s_memtime cycles of agent 0 (libsrbnmpc_stamps.so).
+"""Diagnostic: per-phase s_memtime cycles of agent 0 (libsrbnmpc_stamps.so, make stamps).
 
     python tools/stamps.py [N C K_obs K_nbr agents]
 """
@@ -22,14 +22,15 @@ for _ in range(reps):
 L.srb_debug_stamps(buf, 1)
 v = np.array(buf[:], dtype=float) / reps
 it = out['iters'][0]
-names = ['resid+norms', 'om', 'build_D', "Z'HZ (mfma)", 'chol', 'pred rhs',
-         'P: om*r3 + J\'w', "P: Z'v", 'P: tri-solves', 'P: Z xi', 'P: J dx',
-         'step/rho/corr rhs',
-         'C: om*r3 + J\'w', "C: Z'v", 'C: tri-solves', 'C: Z xi', 'C: J dx', 'dq+update']
-print(f"agent0 iters qp={it[0]} nlp={it[1]}; kernel ms {s.last_kernel_ms()}")
-print("setup", v[28], "qp-init", v[29], "nlp-init", v[30], "output", v[31], "init-solve", v[20:25].sum())
-for stage, base, nit in (("QP", 0, it[0]), ("NLP", 32, it[1])):
-    tot = v[base:base + 18].sum()
-    print(stage, "total cycles", tot, "per iter", tot / max(nit, 1))
-    for i, nm in enumerate(names):
-        print(f"   {nm:20s} {v[base + i] / max(nit, 1):10.0f} cyc/iter  {100 * v[base + i] / max(tot, 1):5.1f}%")
+names = {0: 'setup', 1: 'qp-init', 2: 'nlp-init', 3: 'resid+norms', 4: 'weights+gram', 5: 'factor (GJ)',
+         6: 'P: rhs', 7: 'P: rmul', 8: 'P: solve', 9: 'P: Jdx+steplen', 10: 'rho + C: rhs', 11: 'C: rmul',
+         12: 'C: solve', 13: 'C: Jdx+steplen', 14: 'update', 15: 'output'}
+print(f"agent0 iters qp={it[0]} nlp={it[1]}; kernel ms {s.last_kernel_ms()[1]:.4f}")
+tot_all = v.sum()
+for stage, nit in ((0, it[0]), (1, it[1])):
+    blk = v[32 * stage:32 * stage + 16]
+    per = blk[3:15].sum() / max(nit, 1)
+    print(f"{'QP' if stage == 0 else 'NLP'}: total {blk.sum():.0f} cyc, per iteration {per:.0f}")
+    for i, nm in names.items():
+        if blk[i] > 0:
+            print(f"   {nm:18s} {blk[i]:10.0f} cyc  {blk[i] / max(nit, 1) if 3 <= i <= 14 else 0:8.0f} /iter  {100 * blk[i] / tot_all:5.1f}%")

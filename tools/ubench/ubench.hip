@@ -70,6 +70,35 @@ __global__ void k(unsigned long long *out, double *sink, double seed) {
   // 14 v_readlane_b32 pair alone (to SGPR), dependent via scalar add
   int si = 0;
   TIME({ int q = __builtin_amdgcn_readlane((int)idx + si, r & 63); si = q & 7; } asm volatile("" : "+s"(si)));
+  // 15 16 independent readlane pairs -> 16 independent fma (per rep)
+  double rr[16];
+  for (int i = 0; i < 16; i++) rr[i] = x + i;
+  TIME({
+#pragma unroll
+    for (int i = 0; i < 16; i++) rr[i] = fma(rdl(rr[(i + 1) & 15], i), y, rr[i]);
+  } asm volatile("" : "+v"(rr[0]), "+v"(rr[5]), "+v"(rr[9]), "+v"(rr[15])));
+  for (int i = 0; i < 16; i++) x += rr[i];
+  // 16 v_rcp_f64 + 2 NR dependent
+  TIME({ double q = __builtin_amdgcn_rcp(x); q = fma(q, fma(-x, q, 1.0), q); q = fma(q, fma(-x, q, 1.0), q); x = q + 1.0; } asm volatile("" : "+v"(x)));
+  // 17 16 independent fma (per rep)
+  TIME({
+#pragma unroll
+    for (int i = 0; i < 16; i++) rr[i] = fma(rr[i], y, 1e-12);
+  } asm volatile("" : "+v"(rr[0]), "+v"(rr[5]), "+v"(rr[9]), "+v"(rr[15])));
+  for (int i = 0; i < 16; i++) x += rr[i];
+  // 18 __syncthreads (single-wave workgroup) with one LDS write before
+  TIME({ lds[t] = x; __syncthreads(); x = lds[t ^ 1] * y; } asm volatile("" : "+v"(x)));
+  // 19 16 ds_read_b64 of independent lane-varying addresses then sum (per rep)
+  TIME({ double acc2 = 0;
+#pragma unroll
+    for (int i = 0; i < 16; i++) acc2 += lds[(t * 17 + i * 3 + (idx & 1)) & 1023];
+    x = acc2 * 1e-3; } asm volatile("" : "+v"(x)));
+  // 20 v_cndmask-heavy select chain 16 (per rep)
+  TIME({
+#pragma unroll
+    for (int i = 0; i < 16; i++) rr[i] = (t == i) ? rr[i] * y : rr[i];
+  } asm volatile("" : "+v"(rr[0]), "+v"(rr[5]), "+v"(rr[9]), "+v"(rr[15])));
+  for (int i = 0; i < 16; i++) x += rr[i];
   sink[t] = x + idx + si;
 }
 int main() {
@@ -77,12 +106,13 @@ int main() {
   hipMalloc(&o, 64 * 8); hipMalloc(&s, 64 * 8);
   const char *names[] = {"empty loop", "dep f64 fma", "4 indep fma chains (per rep)", "LDS write->read rt", "readlane->fma",
                          "rsq+2NR", "DPP wave sum", "readlane+uniform branch+fma", "LDS load dep via addr", "shfl_xor f64",
-                         "f64 div", "LDS write + 8 bcast reads", "mfma f64 dep", "4 indep mfma (per rep)", "readlane->salu"};
+                         "f64 div", "LDS write + 8 bcast reads", "mfma f64 dep", "4 indep mfma (per rep)", "readlane->salu",
+                         "16 indep readlane+fma (per rep)", "rcp+2NR dep", "16 indep fma (per rep)", "LDS wr+syncthreads+rd", "16 ds_read_b64 lane-var (per rep)", "16 cndmask-mul (per rep)"};
   for (int pass = 0; pass < 2; pass++) {
     hipLaunchKernelGGL(k, dim3(1), dim3(64), 0, 0, o, s, 1.5);
     hipDeviceSynchronize();
   }
-  unsigned long long h[64]; hipMemcpy(h, o, 15 * 8, hipMemcpyDeviceToHost);
-  for (int i = 0; i < 15; i++) printf("%-32s %8.1f cycles/rep\n", names[i], (double)h[i] / REP);
+  unsigned long long h[64]; hipMemcpy(h, o, 21 * 8, hipMemcpyDeviceToHost);
+  for (int i = 0; i < 21; i++) printf("%-32s %8.1f cycles/rep\n", names[i], (double)h[i] / REP);
   return 0;
 }
