@@ -4,8 +4,8 @@
     python bench.py [--gpus N --steps K --warmup W] [--config 2] [--agents A]
 
 One "step" = one pass of the hot path over one batch: (configs with inter-agent rows:
-all-gather of the neighbour snapshot over RCCL) + kNN + QP stage + NLP stage for every
-agent of the batch, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun),
+all-gather of the neighbour snapshot over RCCL) + kNN + QP stage + NLP stage + Bezier fit
+(alpha_COM) for every agent of the batch, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun),
 agents sharded agent-major, weak scaling (fixed agents per GPU).  Rank 0 prints one JSON
 line.  Configs (BASELINE.json "configs"):
     1  1 agent, N=4 reference mode (KAT-2 shape)            -- CPU plumbing case
@@ -50,7 +50,7 @@ def dense_equiv_flops(p, iters):
 
 def io_bytes(p, n_agents, n_obs, n_all):
     """Algorithmic HBM bytes per launch: inputs + outputs once."""
-    per = 8 * (4 + 4 * p.N + 2 * p.C * p.N) + 8 * (2 * p.nv + 1) + 16
+    per = 8 * (4 + 4 * p.N + 2 * p.C * p.N + 4) + 8 * (p.nv + 1 + 20) + 16
     return n_agents * per + 16 * n_obs + 32 * n_all
 
 
@@ -111,7 +111,12 @@ def main():
     nbr_local = t["nbr_state"][lo:hi].contiguous()
     nbr_all = t["nbr_state"] if cfg["K_nbr"] > 0 else None
     n_loc = hi - lo
-    out = dict(x_qp=None, x=torch.zeros((n_loc, p.nv), dtype=torch.float64, device=dev),
+    # Bezier buffer state (fitComTrajectory_eventbase runs fused in the solve kernel): start
+    # position with zero velocity, as before an agent's first solve (MPC_dist.cpp:792)
+    alpha_buf = torch.stack([t["x0"][:, 0], torch.zeros_like(t["x0"][:, 0]), t["x0"][:, 2],
+                             torch.zeros_like(t["x0"][:, 0])], 1).contiguous()
+    out = dict(x_qp=None, alpha=torch.zeros((n_loc, 20), dtype=torch.float64, device=dev),
+               x=torch.zeros((n_loc, p.nv), dtype=torch.float64, device=dev),
                obj=torch.zeros(n_loc, dtype=torch.float64, device=dev),
                status=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
                iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev))
@@ -125,7 +130,7 @@ def main():
     def step():
         nb = sdist.gather_states(nbr_local, A_total, world) if exchange else nbr_all
         solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nb, out, agent_offset=lo,
-                            stream=stream.cuda_stream)
+                            stream=stream.cuda_stream, alpha_buf=alpha_buf)
 
     for _ in range(args.warmup):
         step()

@@ -74,12 +74,19 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *   obj       [A]           0.5 x'Q_qp x + f'x (ExCost::GetCost)
  *   status    [A][2] int    QP, NLP exit codes
  *   iters     [A][2] int    QP, NLP interior-point iterations
+ * Bezier fit of the predicted CoM (fitComTrajectory_eventbase, MPC_dist.cpp:784-855), fused
+ * into the solve; both NULL = not fitted (needs N >= 4):
+ *   alpha_buf [A][4]        mpc_state_alpha_buffer_ (the previous solve's X_3; the start
+ *                           position with zero velocity before the first one, :792, :798)
+ *   alpha     [A][20]       get_alphaCOM(): 4 x 5 row-major (state row, Bernstein index)
  */
 typedef struct srb_batch {
     const double *x0, *ref, *foot, *obstacles, *nbr_state;
     int n_obs, n_all, agent_offset;
     double *x_qp, *x, *obj;
     int *status, *iters;
+    const double *alpha_buf;
+    double *alpha;
 } srb_batch;
 
 typedef struct srb_ctx srb_ctx;

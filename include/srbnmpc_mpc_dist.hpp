@@ -6,9 +6,9 @@
  * unchanged; see INTEGRATION.md for the two-line switch.
  *
  * What stays on the host, as in the reference: copPlanner_eventbase (MPC_dist.cpp:702-782),
- * footholdsPlanner (:1204-1266), fitComTrajectory_eventbase (:784-855, srb_fit_bezier) and
- * the bookkeeping of gaitDomain_ / the alpha buffer (:450-453, :798).  What goes to the GPU:
- * the QP assembly + iSWIFT QP + closest-obstacle scan + NLP (:99-427).
+ * footholdsPlanner (:1204-1266) and the bookkeeping of gaitDomain_ / the alpha buffer
+ * (:450-453, :798).  What goes to the GPU: the QP assembly + iSWIFT QP + closest-obstacle
+ * scan + NLP (:99-427) and fitComTrajectory_eventbase (:784-855, fused epilogue).
  *
  * Matrix types: with Eigen available (define SRBNMPC_USE_EIGEN, or have <eigen3/Eigen/Dense>
  * on the include path) the getters return Eigen::MatrixXd / Eigen::Vector4d exactly as the
@@ -153,16 +153,13 @@ public:
         b.n_obs = (int)(pobs_real_.size() / 2);
         b.nbr_state = nullptr; b.n_all = 0; b.agent_offset = 0;
         b.x_qp = x_qp_.data(); b.x = x_.data(); b.obj = &obj; b.status = status_; b.iters = iters_;
+        /* fitComTrajectory_eventbase :784-855 runs as the solve kernel's epilogue */
+        b.alpha_buf = alpha_buffer_.data(); b.alpha = alpha_.data();
         const int rc = use_snopt ? srb_solve_batch(ctx, 1, &b) : srb_solve_qp(ctx, 1, &b);
         if (rc != SRB_OK) throw std::runtime_error(std::string("srb_solve_batch: ") + srb_last_error());
-        /* copy-out :431-440 */
+        /* copy-out :431-440, buffer update :798 */
         for (int i = 0; i < 4 * N; i++) X_[(size_t)i] = x_[(size_t)i];
         for (int i = 0; i < N; i++) U0_[(size_t)i] = x_[(size_t)(4 * N + 2 * i)];
-        /* fitComTrajectory_eventbase :784-855 and the buffer update :798 */
-        double alpha[20];
-        srb_fit_bezier(alpha_buffer_.data(), X_.data(), alpha);
-        for (int d = 0; d < 4; d++)
-            for (int j = 0; j < 5; j++) alpha_[(size_t)(d * 5 + j)] = alpha[d * 5 + j];
         for (int d = 0; d < 4; d++) alpha_buffer_[(size_t)d] = X_[(size_t)(12 + d)];
         gaitDomain_++;
     }

@@ -16,12 +16,14 @@
     extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS(                                                  \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
-        double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out);
+        double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
+        const double *alpha_buf, double *alpha_out);
 SRB_KERNEL_INSTANCES(DECL_NMPC)
 #undef DECL_NMPC
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
-                              const double *, int, int, double *, double *, double *, int *, int *);
+                              const double *, int, int, double *, double *, double *, int *, int *, const double *,
+                              double *);
 struct srb_instance { int nzl, ts; srb_kernel_fn fn; };
 #define ENTRY_NMPC(NZL, TS) {NZL, TS, srb_nmpc_kernel_##NZL##_##TS},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
@@ -57,7 +59,7 @@ struct srb_ctx {
     hipStream_t stream;
     hipEvent_t ev[4];
     // device staging
-    double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj;
+    double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj, *abuf, *alpha;
     int *status, *iters;
     size_t cap_obs, cap_nbr;
     float knn_ms, solve_ms;
@@ -85,6 +87,32 @@ static void mm4(const double *X, const double *Y, double *Z)
             for (int k = 0; k < 4; k++) s += X[i * 4 + k] * Y[k * 4 + j];
             Z[i * 4 + j] = s;
         }
+}
+
+// Inverse of the 5x5 Bernstein matrix B[i][j] = C(4,j) s_i^j (1-s_i)^(4-j), s_i = i/4
+// (fitComTrajectory_eventbase, MPC_dist.cpp:801-806), Gauss-Jordan with partial pivoting.
+static void bernstein_inverse(double Binv[25])
+{
+    static const double binom[5] = {1, 4, 6, 4, 1};
+    double M[5][10];
+    for (int i = 0; i < 5; i++) {
+        const double s = i * 0.25;
+        for (int j = 0; j < 5; j++) { M[i][j] = binom[j] * std::pow(s, j) * std::pow(1 - s, 4 - j); M[i][5 + j] = (i == j); }
+    }
+    for (int k = 0; k < 5; k++) {
+        int piv = k;
+        for (int i = k + 1; i < 5; i++) if (std::fabs(M[i][k]) > std::fabs(M[piv][k])) piv = i;
+        for (int j = 0; j < 10; j++) std::swap(M[k][j], M[piv][j]);
+        const double inv = 1.0 / M[k][k];
+        for (int j = 0; j < 10; j++) M[k][j] *= inv;
+        for (int i = 0; i < 5; i++)
+            if (i != k) {
+                const double f = M[i][k];
+                for (int j = 0; j < 10; j++) M[i][j] -= f * M[k][j];
+            }
+    }
+    for (int i = 0; i < 5; i++)
+        for (int j = 0; j < 5; j++) Binv[i * 5 + j] = M[i][5 + j];
 }
 
 // LIP discretisation MPC_dist.cpp:99-127 (Ad by third-order series, Bd = A^-1 (Ad - I) B)
@@ -117,6 +145,7 @@ static SrbKParams make_kparams(const srb_params *p, int use_nlp)
     k.Qw = p->Qw; k.Pw = p->Pw; k.Rw = p->Rw; k.Sw = p->Sw; k.box = p->box;
     k.fr = p->mu * p->hcom / std::sqrt(2.0);
     k.eps_obs = p->eps_obs; k.eps_nbr = p->eps_nbr; k.vsat = p->vsat; k.tol = p->tol; k.Ts = p->Ts;
+    bernstein_inverse(k.Binv);
     return k;
 }
 
@@ -166,6 +195,8 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->obj, A * sizeof(double)));
     HIPCHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
+    HIPCHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
+    HIPCHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
     *out = c;
     return SRB_OK;
 }
@@ -175,7 +206,8 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
-    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr};
+    void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr,
+                    c->abuf, c->alpha};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -191,6 +223,9 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     const srb_params *p = &c->p;
     if (!d->x0 || !d->ref || !d->foot || !d->x || !d->obj || !d->status || !d->iters)
         return fail(SRB_ERR_ARG, "missing buffer");
+    if ((d->alpha != nullptr) != (d->alpha_buf != nullptr))
+        return fail(SRB_ERR_ARG, "alpha and alpha_buf go together (both or neither)");
+    if (d->alpha && p->N < 4) return fail(SRB_ERR_ARG, "the Bezier fit needs N >= 4 (X_0..X_3)");
     if (use_nlp && p->K_obs > 0 && (d->n_obs < 0 || (d->n_obs > 0 && !d->obstacles)))
         return fail(SRB_ERR_ARG, "obstacles missing");
     if (use_nlp && p->K_nbr > 0 && d->nbr_state && (d->agent_offset < 0 || d->agent_offset + n_agents > d->n_all))
@@ -209,7 +244,8 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     HIPCHK(hipEventRecord(c->ev[0], s));
     // one launch: nearest-obstacle selection, QP stage and NLP stage per agent
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
-                       n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters);
+                       n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
+                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
@@ -259,6 +295,13 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
     srb_batch d = *h;
     d.x0 = c->x0; d.ref = c->ref; d.foot = c->foot;
     d.x_qp = c->x_qp; d.x = c->x; d.obj = c->obj; d.status = c->status; d.iters = c->iters;
+    d.alpha_buf = nullptr; d.alpha = nullptr;
+    if (h->alpha && h->alpha_buf) {
+        HIPCHK(hipMemcpyAsync(c->abuf, h->alpha_buf, A * 4 * sizeof(double), hipMemcpyHostToDevice, s));
+        d.alpha_buf = c->abuf; d.alpha = c->alpha;
+    } else if (h->alpha || h->alpha_buf) {
+        return fail(SRB_ERR_ARG, "alpha and alpha_buf go together (both or neither)");
+    }
     d.obstacles = nullptr; d.nbr_state = nullptr;
     if (h->n_obs > 0 && h->obstacles) {
         if ((size_t)h->n_obs > c->cap_obs) {
@@ -285,6 +328,7 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
     HIPCHK(hipMemcpyAsync(h->obj, c->obj, A * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h->status, c->status, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h->iters, c->iters, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
+    if (d.alpha) HIPCHK(hipMemcpyAsync(h->alpha, c->alpha, A * 20 * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipStreamSynchronize(s));
     return SRB_OK;
 }

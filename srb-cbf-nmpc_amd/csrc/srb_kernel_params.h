@@ -13,6 +13,7 @@ struct SrbKParams {
     double Ad[16], Bd[8];                  // LIP discretisation (MPC_dist.cpp:126-127)
     double Qw, Pw, Rw, Sw, box, fr;        // gains (:172-175), box (:317), mu*h/sqrt(2) (:315)
     double eps_obs, eps_nbr, vsat, tol, Ts;
+    double Binv[25];                       // inverse 5x5 Bernstein matrix at s = 0, 1/4, .., 1 (Bezier fit)
 };
 
 // Kernel instances (NZL, TS): register bound on nz (one reduced-matrix row per lane) and

@@ -513,7 +513,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ nbr_state, int n_all, int agent_offset,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
-                double *lds)
+                const double *__restrict__ alpha_buf, double *__restrict__ alpha_out, double *lds)
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, LDH = NZM + 1;
@@ -1048,6 +1048,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         }
     }
     f = wsum(f);
+    // ---- fitComTrajectory_eventbase (MPC_dist.cpp:784-855) as an epilogue: alpha_COM (4 x 5)
+    // interpolates [buffer, X_0..X_3] at s = 0, 1/4, 1/2, 3/4, 1 (the reference's 24 x 24 KKT
+    // keeps only the s = 0 end-point row, so its solution is this interpolation), i.e.
+    // alpha[d][j] = sum_i Binv[j][i] p_i[d] with the host-inverted 5 x 5 Bernstein matrix.
+    if (alpha_out && lane < 20) {
+        const int d = lane / 5, j = lane - 5 * (lane / 5);
+        double acc = prm.Binv[5 * j] * alpha_buf[(size_t)agent * 4 + d];
+        for (int i = 1; i < 5; i++) acc = fma(prm.Binv[5 * j + i], xs[4 * (i - 1) + d], acc);
+        alpha_out[(size_t)agent * 20 + 5 * d + j] = acc;
+    }
     STAMP_END(15);
     STAMP_FLUSH(agent);
     if (lane == 0) {
@@ -1063,13 +1073,13 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
-        int *__restrict__ iters_out)                                                                           \
+        int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out)        \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
         nmpc_agent<NZL, TS>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
-                                x_qp_out, x_out, obj_out, status_out, iters_out, lds);                         \
+                                x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, lds);  \
     }
 
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)

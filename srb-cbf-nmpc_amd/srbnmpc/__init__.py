@@ -46,7 +46,8 @@ class Batch(ctypes.Structure):
     """Mirror of srb_batch."""
     _fields_ = [("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
                 ("n_obs", ctypes.c_int), ("n_all", ctypes.c_int), ("agent_offset", ctypes.c_int),
-                ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip)]
+                ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip),
+                ("alpha_buf", _dp), ("alpha", _dp)]
 
 
 _lib = None
@@ -131,7 +132,10 @@ class BatchSolver:
             pass
 
     # --------------------------------------------------------------- host path
-    def solve(self, x0, ref, foot, obstacles=None, nbr_state=None, agent_offset: int = 0, qp_only: bool = False):
+    def solve(self, x0, ref, foot, obstacles=None, nbr_state=None, agent_offset: int = 0, qp_only: bool = False,
+              alpha_buf=None):
+        """Host arrays in, dict of outputs back.  alpha_buf ([A][4], the Bezier buffer state)
+        additionally returns alpha ([A][4][5], get_alphaCOM) from the fused fit."""
         p = self.params
         x0 = _f64(x0).reshape(-1, 4)
         A = x0.shape[0]
@@ -141,17 +145,24 @@ class BatchSolver:
         nb = _f64(nbr_state).reshape(-1, 4) if nbr_state is not None else None
         out = dict(x_qp=np.zeros((A, p.nv)), x=np.zeros((A, p.nv)), obj=np.zeros(A),
                    status=np.zeros((A, 2), np.int32), iters=np.zeros((A, 2), np.int32))
+        ab = None
+        if alpha_buf is not None:
+            ab = _f64(alpha_buf).reshape(A, 4)
+            out["alpha"] = np.zeros((A, 4, 5))
         b = Batch(_p(x0), _p(ref), _p(foot), _p(ob) if ob.size else None, _p(nb) if nb is not None else None,
                   ob.shape[0], nb.shape[0] if nb is not None else 0, int(agent_offset),
-                  _p(out["x_qp"]), _p(out["x"]), _p(out["obj"]), _p(out["status"]), _p(out["iters"]))
+                  _p(out["x_qp"]), _p(out["x"]), _p(out["obj"]), _p(out["status"]), _p(out["iters"]),
+                  _p(ab) if ab is not None else None, _p(out["alpha"]) if ab is not None else None)
         fn = lib().srb_solve_qp if qp_only else lib().srb_solve_batch
         _check(fn(self._h, A, ctypes.byref(b)))
         return out
 
     # --------------------------------------------------------------- device path
-    def solve_device(self, x0, ref, foot, obstacles, nbr_state, out, agent_offset: int = 0, stream=None):
+    def solve_device(self, x0, ref, foot, obstacles, nbr_state, out, agent_offset: int = 0, stream=None,
+                     alpha_buf=None):
         """All arguments torch tensors on this solver's device (float64 / int32), contiguous.
-        `out` is a dict with x_qp (or None), x, obj, status, iters.  Asynchronous."""
+        `out` is a dict with x_qp (or None), x, obj, status, iters and, with alpha_buf [A][4],
+        alpha [A][20].  Asynchronous."""
         def dptr(t):
             return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
 
@@ -161,7 +172,8 @@ class BatchSolver:
         b = Batch(dptr(x0), dptr(ref), dptr(foot), dptr(obstacles), dptr(nbr_state),
                   0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],
                   int(agent_offset), dptr(out.get("x_qp")), dptr(out["x"]), dptr(out["obj"]),
-                  iptr(out["status"]), iptr(out["iters"]))
+                  iptr(out["status"]), iptr(out["iters"]), dptr(alpha_buf),
+                  dptr(out.get("alpha") if alpha_buf is not None else None))
         s = ctypes.c_void_p(stream) if stream is not None else None
         _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), s))
 

@@ -125,7 +125,6 @@ class MPCDist:
 
     def run_NMPC(self):
         """MPC_dist.cpp:81-454 with the QP/NLP solve on the GPU."""
-        from . import fit_bezier
         N = NDOMAIN
         ref = self.copPlanner_eventbase(N)
         F = self.footholdsPlanner()
@@ -133,16 +132,17 @@ class MPCDist:
         foot = np.repeat(F[None], N, 0)             # same block on every grid (:1256-1260)
         x0 = np.array([self.q[0], self.dq[0], self.q[1], self.dq[1]])
         solver = self._solver(C, bool(self.use_snopt))
-        out = solver.solve(x0[None], ref[None], foot[None], self.Pobs_real.T.copy())
+        # the solve and fitComTrajectory_eventbase (:784-855, fused epilogue) in one call
+        out = solver.solve(x0[None], ref[None], foot[None], self.Pobs_real.T.copy(),
+                           alpha_buf=self.mpc_state_alpha_buffer_[None])
         x = out["x"][0]
         self.qp_solution_eventbased_ = out["x_qp"][0]
         self.mpc_state_e_x_eventbased_ = x[:4 * N].copy()
         self.last_status = out["status"][0]
         self.last_iters = out["iters"][0]
-        # fitComTrajectory_eventbase (:784-855), buffer update (:798)
         X = self.mpc_state_e_x_eventbased_.reshape(N, 4)
-        self.alpha_COM_traj_e_ = fit_bezier(self.mpc_state_alpha_buffer_, X)
-        self.mpc_state_alpha_buffer_ = X[3].copy()
+        self.alpha_COM_traj_e_ = out["alpha"][0]
+        self.mpc_state_alpha_buffer_ = X[3].copy()              # buffer update (:798)
         self.gaitDomain_ += 1
         return x
 

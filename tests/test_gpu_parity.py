@@ -258,3 +258,23 @@ def test_mpcdist_surface_on_reference_instance(kat2):
     np.testing.assert_allclose(alpha, oracle.fit_bezier([0, 0, 0, 0], np.asarray(kat2["x_nlp"])[:16].reshape(4, 4)),
                                atol=1e-6)
     assert m.gaitDomain_ == 1
+
+
+@pytest.mark.parametrize("N,C,Kn", [(4, 4, 0), (10, 2, 8)])
+def test_fused_bezier_epilogue_matches_reference_fit(N, C, Kn):
+    """fitComTrajectory_eventbase (MPC_dist.cpp:784-855) fused into the solve == the oracle's
+    literal 24x24 KKT restatement on the same predicted states and buffer."""
+    A = 48
+    b = workload.make_batch(A, N, C, seed=31 + N)
+    rng = np.random.default_rng(5)
+    buf = np.stack([b["x0"][:, 0], rng.uniform(-0.2, 0.2, A), b["x0"][:, 2], rng.uniform(-0.2, 0.2, A)], 1)
+    s = solver(N, C, 3, Kn)
+    out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], alpha_buf=buf)
+    plain = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    np.testing.assert_array_equal(out["x"], plain["x"])          # the epilogue does not touch the solve
+    for a in range(A):
+        X = out["x"][a, :16].reshape(4, 4)
+        want = oracle.fit_bezier(buf[a], X)
+        np.testing.assert_allclose(out["alpha"][a], want, rtol=0, atol=1e-10 * max(1.0, np.abs(want).max()))
+        np.testing.assert_allclose(out["alpha"][a][:, 0], buf[a], atol=1e-12)   # a_0 = buffer (s = 0 row)
+        np.testing.assert_allclose(out["alpha"][a][:, 4], X[3], atol=1e-9)       # a_4 = X_3 (s = 1)
