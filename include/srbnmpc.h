@@ -106,6 +106,35 @@ int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
 int srb_sync(srb_ctx *ctx);
 
+/*
+ * Input assembly on the device (the planners run_NMPC calls before its solve; SURVEY.md 8(f)
+ * row 2), one batch of agents, asynchronous on `stream` like srb_solve_batch_device:
+ *   updateState + x0 (MPC_dist.cpp:1195-1202, :226-229), get_lastState (:1272-1276),
+ *   copPlanner_eventbase (:702-782) and footholdsPlanner (:1204-1266).
+ * All pointers are device pointers.  Inputs:
+ *   Pr, Prd      [T][n_rows]   the HL path Pr_refined_ / Prd_refined_ (2*NA x T, column-major as
+ *                              Eigen stores it); agent id uses rows 2 id, 2 id + 1
+ *   agent_id     [A] int       (NULL: agent_offset + a)
+ *   gait_domain  [A] int       gaitDomain_: the window starts at column 4 * gaitDomain_ (NDOMAIN
+ *                              grids per domain) and spans N columns
+ *   contact      [A][4] int    contactInd (FR, FL, RR, RL); must give C contacts
+ *   toe          [A][3][4]     toePos (row-major 3 x 4)
+ *   start        [A][2]        agent_Initial_ (default stance while gaitDomain_ <= 1)
+ *   q, dq        [A][18]       generalised coordinates / velocities (q[0], q[1], dq[0], dq[1] used)
+ * Outputs: x0 [A][4], ref [A][4N], foot [A][N][2][C] (the srb_batch inputs), last_state [A][4]
+ * (the neighbour-snapshot row), status [A] int: 0 ok, 1 contact pattern does not give C
+ * contacts, 2 reference window outside the path.
+ */
+typedef struct srb_prep {
+    const double *Pr, *Prd;
+    int n_rows, T, agent_offset;
+    const int *agent_id, *gait_domain, *contact;
+    const double *toe, *start, *q, *dq;
+    double *x0, *ref, *foot, *last_state;
+    int *status;
+} srb_prep;
+int srb_prepare_batch_device(srb_ctx *ctx, int n_agents, const srb_prep *dev_io, void *stream);
+
 /* Per-launch timing of the last srb_solve_batch_device call, measured with HIP events on
  * the stream the kernel ran on (ms).  The nearest-obstacle selection is fused into the
  * solve kernel, so knn_ms is always 0 (kept for ABI stability). */

@@ -258,6 +258,30 @@ extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch 
     return launch(c, n_agents, dev_io, s, c->p.use_nlp);
 }
 
+extern "C" __global__ void srb_prepare_kernel(int n_agents, int N, int C, int n_rows, int T, int agent_offset,
+                                              const double *Pr, const double *Prd, const int *agent_id,
+                                              const int *gait_domain, const int *contact, const double *toe,
+                                              const double *start, const double *q, const double *dq, double *x0,
+                                              double *ref, double *foot, double *last_state, int *status);
+
+extern "C" int srb_prepare_batch_device(srb_ctx *c, int n_agents, const srb_prep *d, void *stream)
+{
+    if (!c || !d) return fail(SRB_ERR_ARG, "null argument");
+    if (n_agents < 0) return fail(SRB_ERR_ARG, "negative n_agents");
+    if (n_agents == 0) return SRB_OK;
+    if (!d->Pr || !d->Prd || !d->gait_domain || !d->contact || !d->toe || !d->start || !d->q || !d->dq || !d->x0 ||
+        !d->ref || !d->foot || !d->last_state || !d->status)
+        return fail(SRB_ERR_ARG, "missing buffer");
+    if (d->n_rows < 2 || d->T < 1) return fail(SRB_ERR_ARG, "empty HL path");
+    HIPCHK(hipSetDevice(c->device));
+    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipLaunchKernelGGL(srb_prepare_kernel, dim3((n_agents + 255) / 256), dim3(256), 0, s, n_agents, c->p.N, c->p.C,
+                       d->n_rows, d->T, d->agent_offset, d->Pr, d->Prd, d->agent_id, d->gait_domain, d->contact,
+                       d->toe, d->start, d->q, d->dq, d->x0, d->ref, d->foot, d->last_state, d->status);
+    HIPCHK(hipGetLastError());
+    return SRB_OK;
+}
+
 extern "C" int srb_sync(srb_ctx *c)
 {
     if (!c) return fail(SRB_ERR_ARG, "null ctx");

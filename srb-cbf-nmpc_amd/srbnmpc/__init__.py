@@ -50,6 +50,14 @@ class Batch(ctypes.Structure):
                 ("alpha_buf", _dp), ("alpha", _dp)]
 
 
+class Prep(ctypes.Structure):
+    """Mirror of srb_prep (input assembly on the device)."""
+    _fields_ = [("Pr", _dp), ("Prd", _dp), ("n_rows", ctypes.c_int), ("T", ctypes.c_int), ("agent_offset", ctypes.c_int),
+                ("agent_id", _ip), ("gait_domain", _ip), ("contact", _ip),
+                ("toe", _dp), ("start", _dp), ("q", _dp), ("dq", _dp),
+                ("x0", _dp), ("ref", _dp), ("foot", _dp), ("last_state", _dp), ("status", _ip)]
+
+
 _lib = None
 
 
@@ -69,6 +77,7 @@ def lib():
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch)]
         L.srb_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_void_p]
         L.srb_sync.argtypes = [ctypes.c_void_p]
+        L.srb_prepare_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Prep), ctypes.c_void_p]
         L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.srb_fit_bezier.argtypes = [_dp, _dp, _dp]
         L.srb_last_error.restype = ctypes.c_char_p
@@ -176,6 +185,24 @@ class BatchSolver:
                   dptr(out.get("alpha") if alpha_buf is not None else None))
         s = ctypes.c_void_p(stream) if stream is not None else None
         _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), s))
+
+    def prepare_device(self, Pr, Prd, gait_domain, contact, toe, start, q, dq, out, agent_id=None,
+                       agent_offset: int = 0, stream=None):
+        """Input assembly on the device (srb_prepare_batch_device): torch tensors on this
+        solver's device.  Pr, Prd: [T, 2*NA] (column-major 2*NA x T); gait_domain [A] int32;
+        contact [A,4] int32; toe [A,3,4]; start [A,2]; q, dq [A,18].  `out` holds x0 [A,4],
+        ref [A,4N], foot [A,N*2*C], last_state [A,4], status [A] int32.  Asynchronous."""
+        def dptr(t):
+            return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
+
+        def iptr(t):
+            return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _ip)
+        A = q.shape[0]
+        pr = Prep(dptr(Pr), dptr(Prd), Pr.shape[1], Pr.shape[0], int(agent_offset), iptr(agent_id),
+                  iptr(gait_domain), iptr(contact), dptr(toe), dptr(start), dptr(q), dptr(dq),
+                  dptr(out["x0"]), dptr(out["ref"]), dptr(out["foot"]), dptr(out["last_state"]), iptr(out["status"]))
+        s = ctypes.c_void_p(stream) if stream is not None else None
+        _check(lib().srb_prepare_batch_device(self._h, A, ctypes.byref(pr), s))
 
     def sync(self):
         _check(lib().srb_sync(self._h))

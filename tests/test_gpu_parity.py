@@ -278,3 +278,50 @@ def test_fused_bezier_epilogue_matches_reference_fit(N, C, Kn):
         np.testing.assert_allclose(out["alpha"][a], want, rtol=0, atol=1e-10 * max(1.0, np.abs(want).max()))
         np.testing.assert_allclose(out["alpha"][a][:, 0], buf[a], atol=1e-12)   # a_0 = buffer (s = 0 row)
         np.testing.assert_allclose(out["alpha"][a][:, 4], X[3], atol=1e-9)       # a_4 = X_3 (s = 1)
+
+
+@pytest.mark.parametrize("C", [2, 4])
+def test_device_input_assembly_matches_host_planners(C):
+    """srb_prepare_batch_device == the reference's copPlanner_eventbase / footholdsPlanner /
+    updateState / get_lastState (restated host-side in srbnmpc.MPCDist) for a batch."""
+    N, A, NA, T = 4, 40, 40, 64
+    rng = np.random.default_rng(17 + C)
+    Pr = rng.uniform(-3, 9, (2 * NA, T)); Prd = rng.uniform(-0.4, 0.4, (2 * NA, T))
+    gd = rng.integers(0, 10, A).astype(np.int32)
+    contact = np.zeros((A, 4), np.int32)
+    for a in range(A):
+        contact[a] = [1, 1, 1, 1] if C == 4 else ([1, 0, 0, 1] if a % 2 else [0, 1, 1, 0])
+    toe = rng.uniform(-1, 9, (A, 3, 4)); start = rng.uniform(0, 9, (A, 2))
+    q = rng.normal(size=(A, 18)); dq = rng.normal(size=(A, 18))
+    dev = torch.device("cuda:0")
+    tt = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    s = solver(N, C, 1, 0, 1, max_agents=64)
+    out = dict(x0=torch.zeros((A, 4), dtype=torch.float64, device=dev), ref=torch.zeros((A, 4 * N), dtype=torch.float64, device=dev),
+               foot=torch.zeros((A, N * 2 * C), dtype=torch.float64, device=dev),
+               last_state=torch.zeros((A, 4), dtype=torch.float64, device=dev), status=torch.full((A,), -1, dtype=torch.int32, device=dev))
+    s.prepare_device(tt(Pr.T), tt(Prd.T), tt(gd, torch.int32), tt(contact, torch.int32), tt(toe), tt(start), tt(q), tt(dq), out)
+    s.sync()
+    got = {k: v.cpu().numpy() for k, v in out.items()}
+    ok = 4 * gd + N <= T
+    np.testing.assert_array_equal(got["status"], np.where(ok, 0, 2))
+    for a in range(A):
+        m = srbnmpc.MPCDist()
+        m.setAgentID(a)
+        Ps = np.zeros(2 * NA); Ps[2 * a:2 * a + 2] = start[a]
+        m.setPstart(Ps)
+        m.setReferenceTrajectory(Pr, Prd)
+        m.updateState(q[a], dq[a], contact[a], toe[a], np.zeros(4))
+        m.gaitDomain_ = int(gd[a])
+        np.testing.assert_array_equal(got["x0"][a], [q[a, 0], dq[a, 0], q[a, 1], dq[a, 1]])
+        np.testing.assert_array_equal(got["last_state"][a], m.get_lastState())
+        F = m.footholdsPlanner()
+        np.testing.assert_array_equal(got["foot"][a].reshape(N, 2, C), np.repeat(F[None], N, 0))
+        if ok[a]:
+            # window of the current domain: columns 4 gaitDomain_ .. + N (N == NDOMAIN here)
+            np.testing.assert_array_equal(got["ref"][a], m.copPlanner_eventbase(N))
+    # and the assembled batch solves like the host-assembled one
+    good = np.where(ok)[0][:16]
+    sub = {k: v[good] for k, v in got.items()}
+    obst = rng.uniform(0, 9, (20, 2))
+    r1 = s.solve(sub["x0"], sub["ref"], sub["foot"], obst)
+    assert (r1["status"] >= 0).all()
