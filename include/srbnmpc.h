@@ -135,6 +135,16 @@ typedef struct srb_prep {
 } srb_prep;
 int srb_prepare_batch_device(srb_ctx *ctx, int n_agents, const srb_prep *dev_io, void *stream);
 
+/*
+ * HL reference planner (generateReferenceTrajectory, MPC_dist.cpp:930-1104; SURVEY.md 8(f)
+ * row 3) on HIP device `device`, host buffers, synchronous.  NA agents (1..1024) starting at
+ * Pstart [NA][2], planner obstacles Pobs [n_obs][2] (n_obs <= 2048), `loop` steps (reference:
+ * 100000).  Outputs Pr_refined_ / Prd_refined_ as column-major 2NA x (loop / 40) arrays (the
+ * layout setReferenceTrajectory / srb_prep take).  Returns 0 or a negative error code.
+ */
+int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr,
+                double *Prd);
+
 /* Per-launch timing of the last srb_solve_batch_device call, measured with HIP events on
  * the stream the kernel ran on (ms).  The nearest-obstacle selection is fused into the
  * solve kernel, so knn_ms is always 0 (kept for ABI stability). */

@@ -175,6 +175,17 @@ def solve_batch(p: OrcParams, x0, ref, foot, obstacles, nbr_state=None, agent_of
     return dict(x_qp=xq, x=x, obj=obj, status=st, iters=it)
 
 
+def hl_plan(Pstart, Pobs, loop=100000):
+    """generateReferenceTrajectory (MPC_dist.cpp:930-1104) restated: Pr, Prd (2NA x loop/40)."""
+    Ps = _c(Pstart).reshape(-1)
+    NA = Ps.size // 2
+    ob = _c(Pobs).reshape(-1, 2)
+    T = loop // 40
+    Pr = np.zeros((T, 2 * NA)); Prd = np.zeros((T, 2 * NA))
+    lib().orc_hl_plan(NA, _ptr(Ps), _ptr(ob), ob.shape[0], int(loop), _ptr(Pr), _ptr(Prd))
+    return Pr.T.copy(), Prd.T.copy()
+
+
 def fit_bezier(buf, X):
     a = np.zeros(20)
     lib().orc_fit_bezier(_ptr(_c(buf)), _ptr(_c(X)), _ptr(a))

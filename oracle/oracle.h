@@ -105,6 +105,11 @@ int orc_solve_batch(const orc_params *p, int n_agents, const double *x0, const d
  * from the buffer state (4) and the first 4 predicted states X[0..3]. */
 void orc_fit_bezier(const double buf[4], const double *X, double alpha[20]);
 
+/* HL reference planner (generateReferenceTrajectory, MPC_dist.cpp:930-1104) for NA agents,
+ * n_obs planner obstacles Pobs [n_obs][2], `loop` steps (reference: 100000).  Pr, Prd:
+ * column-major 2NA x (loop / 40). */
+void orc_hl_plan(int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr, double *Prd);
+
 /* dense helpers (linalg.c) */
 int orc_chol(int n, double *A);                               /* in place, lower */
 void orc_chol_solve(int n, const double *L, double *x);

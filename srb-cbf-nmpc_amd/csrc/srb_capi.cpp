@@ -282,6 +282,50 @@ extern "C" int srb_prepare_batch_device(srb_ctx *c, int n_agents, const srb_prep
     return SRB_OK;
 }
 
+extern "C" __global__ void srb_hlplan_kernel(int NA, const double *Pstart, const double *Pobs, int n_obs, int loop,
+                                             double *Pr, double *Prd);
+
+extern "C" int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr,
+                           double *Prd)
+{
+    if (NA < 1 || NA > 1024) return fail(SRB_ERR_SIZE, "HL planner: 1 <= NA <= 1024 (one workgroup)");
+    if (n_obs < 0 || n_obs > 2048 || (n_obs > 0 && !Pobs)) return fail(SRB_ERR_ARG, "HL planner: bad obstacle table");
+    if (loop < 80 || !Pstart || !Pr || !Prd) return fail(SRB_ERR_ARG, "HL planner: bad arguments (loop >= 80)");
+    int ndev = 0;
+    HIPCHK(hipGetDeviceCount(&ndev));
+    if (device < 0 || device >= ndev) return fail(SRB_ERR_ARG, "device index out of range");
+    HIPCHK(hipSetDevice(device));
+    const int T = loop / 40;
+    const size_t out = (size_t)T * 2 * NA * sizeof(double);
+    double *dPs = nullptr, *dOb = nullptr, *dPr = nullptr, *dPrd = nullptr;
+    int rc = SRB_OK;
+    auto chk = [&](hipError_t e, const char *what) {
+        if (e != hipSuccess && rc == SRB_OK) rc = fail(SRB_ERR_HIP, std::string(what) + ": " + hipGetErrorString(e));
+    };
+    chk(hipMalloc(&dPs, 2 * NA * sizeof(double)), "hipMalloc");
+    chk(hipMalloc(&dOb, (n_obs > 0 ? n_obs : 1) * 2 * sizeof(double)), "hipMalloc");
+    chk(hipMalloc(&dPr, out), "hipMalloc");
+    chk(hipMalloc(&dPrd, out), "hipMalloc");
+    if (rc == SRB_OK) {
+        chk(hipMemcpy(dPs, Pstart, 2 * NA * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+        if (n_obs > 0) chk(hipMemcpy(dOb, Pobs, n_obs * 2 * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+    }
+    if (rc == SRB_OK) {
+        const int threads = ((NA + 63) / 64) * 64;
+        const size_t lds = (4 * (size_t)NA + 2 * (size_t)n_obs) * sizeof(double);
+        hipLaunchKernelGGL(srb_hlplan_kernel, dim3(1), dim3(threads), lds, 0, NA, dPs, dOb, n_obs, loop, dPr, dPrd);
+        chk(hipGetLastError(), "srb_hlplan_kernel");
+        chk(hipDeviceSynchronize(), "srb_hlplan_kernel");
+    }
+    if (rc == SRB_OK) {
+        chk(hipMemcpy(Pr, dPr, out, hipMemcpyDeviceToHost), "hipMemcpy");
+        chk(hipMemcpy(Prd, dPrd, out, hipMemcpyDeviceToHost), "hipMemcpy");
+    }
+    for (void *b : {(void *)dPs, (void *)dOb, (void *)dPr, (void *)dPrd})
+        if (b) (void)hipFree(b);
+    return rc;
+}
+
 extern "C" int srb_sync(srb_ctx *c)
 {
     if (!c) return fail(SRB_ERR_ARG, "null ctx");

@@ -77,6 +77,7 @@ def lib():
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch)]
         L.srb_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_void_p]
         L.srb_sync.argtypes = [ctypes.c_void_p]
+        L.srb_hl_plan.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.srb_prepare_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Prep), ctypes.c_void_p]
         L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.srb_fit_bezier.argtypes = [_dp, _dp, _dp]
@@ -211,6 +212,19 @@ class BatchSolver:
         a = ctypes.c_float(); b = ctypes.c_float()
         _check(lib().srb_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+
+def hl_plan(Pstart, Pobs, loop: int = 100000, device: int = 0):
+    """HL reference planner on the GPU (generateReferenceTrajectory, MPC_dist.cpp:930-1104).
+    Pstart [NA, 2] (or flat 2NA), Pobs [n_obs, 2].  Returns Pr, Prd as (2NA, loop // 40)."""
+    Ps = _f64(Pstart).reshape(-1)
+    NA = Ps.size // 2
+    ob = _f64(Pobs).reshape(-1, 2)
+    T = int(loop) // 40
+    Pr = np.zeros((T, 2 * NA)); Prd = np.zeros((T, 2 * NA))
+    _check(lib().srb_hl_plan(int(device), NA, _p(Ps), _p(ob) if ob.size else None, ob.shape[0], int(loop),
+                             _p(Pr), _p(Prd)))
+    return Pr.T.copy(), Prd.T.copy()
 
 
 def fit_bezier(buf, X):

@@ -325,3 +325,20 @@ def test_device_input_assembly_matches_host_planners(C):
     obst = rng.uniform(0, 9, (20, 2))
     r1 = s.solve(sub["x0"], sub["ref"], sub["foot"], obst)
     assert (r1["status"] >= 0).all()
+
+
+@pytest.mark.parametrize("NA,n_obs,loop", [(4, 20, 20000), (64, 40, 4000), (300, 60, 2000)])
+def test_hl_planner_bitwise_vs_oracle(NA, n_obs, loop):
+    """generateReferenceTrajectory on the device == the CPU restatement, bit for bit (same
+    operation order, no contraction); reference start layout for NA = 4."""
+    rng = np.random.default_rng(NA)
+    if NA == 4:
+        Ps = np.array([0.0, 0.0, 0.0, -0.9, -1, 0, -1, -0.9])         # src/A1_Sim.cpp:1013
+    else:
+        Ps = np.stack([rng.uniform(-4, 0, NA), rng.uniform(-3, 3, NA)], 1).ravel()
+    Po = np.stack([rng.uniform(0, 9, n_obs), rng.uniform(-2, 2, n_obs)], 1)
+    Pr, Prd = srbnmpc.hl_plan(Ps, Po, loop=loop)
+    R, Rd = oracle.hl_plan(Ps, Po, loop=loop)
+    assert Pr.shape == (2 * NA, loop // 40)
+    np.testing.assert_array_equal(Pr, R)
+    np.testing.assert_array_equal(Prd, Rd)

@@ -162,3 +162,22 @@ def test_bezier_fit_interpolates():
     for i, s in enumerate([0, .25, .5, .75, 1.0]):
         val = sum(comb(4, j) * s ** j * (1 - s) ** (4 - j) * alpha[:, j] for j in range(5))
         np.testing.assert_allclose(val, buf if i == 0 else X[i - 1], atol=1e-12)
+
+
+def test_hl_plan_restatement_structure():
+    """generateReferenceTrajectory restated (MPC_dist.cpp:930-1104): the goal pull, a longer
+    run extending a shorter one, and the reference's subsampling quirk -- the last two output
+    columns are the unsampled states T and T+1 (as in the reference's own
+    Sim_Outputs/HLPath.txt, whose last two columns jump back to early positions)."""
+    Ps = np.array([0.0, 0.0, 0.0, -0.9, -1, 0, -1, -0.9])          # src/A1_Sim.cpp:1013
+    loop = 8000
+    Pr, Prd = oracle.hl_plan(Ps, np.array([[3.0, 0.2], [5.0, -1.0]]), loop=loop)
+    T = loop // 40
+    assert Pr.shape == (8, T) and Prd.shape == (8, T)
+    # column j < T-2 is the state at step 40 (j + 2): a longer run shares the prefix exactly
+    longer = oracle.hl_plan(Ps, np.array([[3.0, 0.2], [5.0, -1.0]]), loop=2 * loop)[0]
+    np.testing.assert_array_equal(Pr[:, :T - 2], longer[:, :T - 2])
+    # column T-2 is the state at step T = 200 = 40 * 5, i.e. column 3
+    np.testing.assert_array_equal(Pr[:, T - 2], Pr[:, T // 40 - 2])
+    assert (Pr[0::2, T - 3] > Ps[0::2] + 0.5).all()                     # every agent moved toward the goal
+    assert np.isfinite(Pr).all() and np.isfinite(Prd).all()
