@@ -12,8 +12,8 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
-#define DECL_NMPC(NZL, TS)                                                                                    \
-    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS(                                                  \
+#define DECL_NMPC(NZL, TS, NW)                                                                                \
+    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS##_##NW(                                           \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
@@ -24,18 +24,27 @@ SRB_KERNEL_INSTANCES(DECL_NMPC)
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
                               double *);
-struct srb_instance { int nzl, ts; srb_kernel_fn fn; };
-#define ENTRY_NMPC(NZL, TS) {NZL, TS, srb_nmpc_kernel_##NZL##_##TS},
+struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; };
+#define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 #undef ENTRY_NMPC
 
-// first instance whose register bounds cover the problem (nz reduced rows, all row slots);
-// NULL when none does
-static const srb_instance *pick_instance(const SrbKParams &k)
+// Waves per agent: small batches (up to one agent per CU) spread each agent over the four
+// SIMDs of a CU (NW = 4) for latency; larger batches run one wave per agent so that agents,
+// not waves of one agent, fill the SIMDs.
+static int g_cu_count = 0;
+static int wanted_waves(int n_agents) { return (g_cu_count > 0 && n_agents <= g_cu_count) ? 4 : 1; }
+
+// first instance with NW waves whose register bounds cover the problem (nz reduced rows, all
+// row slots); falls back to one wave per agent; NULL when none fits
+static const srb_instance *pick_instance(const SrbKParams &k, int nw = 1)
 {
     const int S = srb_slots(k.N, k.C, k.K_obs + k.K_nbr);
-    for (const srb_instance &in : g_instances)
-        if (in.nzl >= k.nz && 64 * in.ts >= S) return &in;
+    for (int pass = 0; pass < 2; pass++) {
+        const int want = pass == 0 ? nw : 1;
+        for (const srb_instance &in : g_instances)
+            if (in.nw == want && in.nzl >= k.nz && 64 * in.nw * in.ts >= S) return &in;
+    }
     return nullptr;
 }
 
@@ -64,6 +73,7 @@ struct srb_ctx {
     size_t cap_obs, cap_nbr;
     float knn_ms, solve_ms;
     bool timed;
+    int last_nw;
 };
 
 extern "C" void srb_params_default(srb_params *p, int N, int C)
@@ -160,7 +170,7 @@ static int validate(const srb_params *p)
     SrbKParams k = make_kparams(p, p->use_nlp);
     const srb_instance *in = pick_instance(k);
     if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers the row slots (n + 4N - 2 + N K <= 512)");
-    if ((size_t)srb_lds_doubles(k, in->nzl) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
+    if ((size_t)srb_lds_doubles(k, in->nzl, in->nw) * sizeof(double) > 160 * 1024) return fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
     return SRB_OK;
 }
 
@@ -168,7 +178,7 @@ extern "C" int srb_lds_bytes(const srb_params *p)
 {
     SrbKParams k = make_kparams(p, p->use_nlp);
     const srb_instance *in = pick_instance(k);
-    return in ? srb_lds_doubles(k, in->nzl) * (int)sizeof(double) : -1;
+    return in ? srb_lds_doubles(k, in->nzl, in->nw) * (int)sizeof(double) : -1;
 }
 
 extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out)
@@ -180,6 +190,11 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipGetDeviceCount(&ndev));
     if (device < 0 || device >= ndev) return fail(SRB_ERR_ARG, "device index out of range");
     HIPCHK(hipSetDevice(device));
+    if (g_cu_count == 0) {
+        hipDeviceProp_t prop;
+        HIPCHK(hipGetDeviceProperties(&prop, device));
+        g_cu_count = prop.multiProcessorCount;
+    }
     srb_ctx *c = new srb_ctx();
     c->p = *p; c->max_agents = max_agents; c->device = device;
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false;
@@ -235,15 +250,16 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
     if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
-    const srb_instance *in = pick_instance(k);
+    const srb_instance *in = pick_instance(k, wanted_waves(n_agents));
     if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers this problem");
-    const size_t lds = (size_t)srb_lds_doubles(k, in->nzl) * sizeof(double);
+    const size_t lds = (size_t)srb_lds_doubles(k, in->nzl, in->nw) * sizeof(double);
+    c->last_nw = in->nw;
     HIPCHK(hipSetDevice(c->device));
     const int n_obs = k.K_obs > 0 ? d->n_obs : 0, n_all = k.K_nbr > 0 ? d->n_all : 0;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
     // one launch: nearest-obstacle selection, QP stage and NLP stage per agent
-    hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
+    hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr);
     HIPCHK(hipGetLastError());

@@ -16,24 +16,30 @@ struct SrbKParams {
     double Binv[25];                       // inverse 5x5 Bernstein matrix at s = 0, 1/4, .., 1 (Bezier fit)
 };
 
-// Kernel instances (NZL, TS): register bound on nz (one reduced-matrix row per lane) and
-// trips of 64 row slots (n + 2(N-1) + 2N + N K slots, see srb_kernels.hip).  The host
-// launches the first instance of this list that fits (srb_capi.cpp).
+// Kernel instances (NZL, TS, NW): register bound on nz (one reduced-matrix row per lane),
+// slot trips per thread, wavefronts per agent (n + 2(N-1) + 2N + N K row slots over 64 NW
+// threads, see srb_kernels.hip).  The host launches the first fitting instance of this list
+// with NW = 4 for small batches (one agent per CU, all four SIMDs) and NW = 1 otherwise
+// (srb_capi.cpp).
 #define SRB_KERNEL_INSTANCES(X) \
-    X(8, 1) X(16, 1) X(12, 3) X(12, 4) X(16, 4) X(24, 5) X(24, 8) X(32, 4) X(32, 8)
+    X(8, 1, 1) X(16, 1, 1) X(12, 3, 1) X(12, 4, 1) X(16, 4, 1) X(24, 5, 1) X(24, 8, 1) X(32, 4, 1) X(32, 8, 1) \
+    X(8, 1, 4) X(12, 1, 4) X(16, 1, 4) X(16, 2, 4) X(32, 2, 4)
 static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K; }
 
 static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
 // doubles of dynamic LDS one agent needs for instance bound NZL; must match the carve in
 // nmpc_agent (srb_kernels.hip)
-static inline int srb_lds_doubles(const SrbKParams &p, int NZL)
+static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
 {
     const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZM + 1;
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
-    const int TT = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + srb_r4(NK) + 15) & ~15;
+    const int q = 16 * NW;
+    const int TT = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + srb_r4(NK) + q - 1) / q * q;
+    const int red = (NW > 1) ? 8 * 4 * NW : 0;
+    const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
     return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
-           srb_r4(NK) + (K + 1)
+           srb_r4(NK) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64
 #endif

@@ -112,6 +112,27 @@ __device__ __forceinline__ void wred(double (&v)[NV])
         v[i] = ((MX >> i) & 1u) ? fmax(a, b) : a + b;
     }
 }
+// wred over all NW waves of the workgroup: per-wave DPP reduction, then lane 0 of every wave
+// publishes to `scr` (NW x NV doubles, one scratch block per call site) and every thread
+// combines the NW partials in the same order (identical results on every lane and wave).
+template <int NV, unsigned MX, int NW>
+__device__ __forceinline__ void wred_x(double (&v)[NV], double *scr, int tid)
+{
+    wred<NV, MX>(v);
+    if constexpr (NW > 1) {
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int i = 0; i < NV; i++) scr[(tid >> 6) * NV + i] = v[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            double r = scr[i];
+#pragma unroll
+            for (int w = 1; w < NW; w++) r = ((MX >> i) & 1u) ? fmax(r, scr[w * NV + i]) : r + scr[w * NV + i];
+            v[i] = r;
+        }
+    }
+}
 // sum over the lanes that share (lane mod W), W = 16 or 32: permlane butterflies only
 __device__ __forceinline__ double chunk_sum16(double v)
 {
@@ -156,7 +177,7 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 #define STAMP_END(slot) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
     __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0) atomicAdd(&stamp_lds[st_off + (slot)], _t - st_t0); st_t0 = _t; } while (0)
 #define STAMP_STAGE(s) (st_off = 32 * (s))
-#define STAMP_FLUSH(agent) do { SYNC(); if ((agent) == 0) atomicAdd(&srb_stamp_buf[threadIdx.x], stamp_lds[threadIdx.x]); } while (0)
+#define STAMP_FLUSH(agent) do { SYNC(); if ((agent) == 0 && threadIdx.x < 64) atomicAdd(&srb_stamp_buf[threadIdx.x], stamp_lds[threadIdx.x]); } while (0)
 #else
 #define STAMP_DECL do {} while (0)
 #define STAMP_BEGIN() do {} while (0)
@@ -183,13 +204,16 @@ struct TermLayout {
 //   (column, term) pair needs, so the right-hand side costs one FMA per load; the four term
 //   chunks combine by permlane swaps.
 // cnt is a multiple of 16; rows / W / CF are zero beyond every real row.
-template <int NZL, bool RHS>
+// NW > 1: wave w takes the term rows [w cnt/NW, (w+1) cnt/NW) and the per-wave partial
+// tiles / right-hand sides are summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
+template <int NZL, bool RHS, int NW>
 __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt,
-                                         double *H, double *g, int nz, int lane)
+                                         double *H, double *g, int nz, int tid, double *part)
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, LDH = NZM + 1;
     constexpr int NT = (NZM == 16) ? 1 : 3, NTC = NZM / 16;
+    const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
     d4 acc[NT];
     double ps[NTC];
@@ -197,9 +221,10 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     for (int t = 0; t < NT; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < NTC; t++) ps[t] = 0.0;
+    const int chunk = cnt / NW, tb = wv * chunk;
     // four term groups per batch: every operand load of the batch issues before the first
     // MFMA waits on one, and the next batch's loads issue while the MFMAs drain
-    for (int t0 = 0; t0 < cnt; t0 += 16) {
+    for (int t0 = tb; t0 < tb + chunk; t0 += 16) {
         double a[4][NTC], w[4], c[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
@@ -224,38 +249,71 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
             }
         }
     }
-    if (RHS) {
+    double gs[NTC];
+    if (RHS)
 #pragma unroll
-        for (int tc = 0; tc < NTC; tc++) {
-            const double sv = chunk_sum16(ps[tc]);
-            if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
+        for (int tc = 0; tc < NTC; tc++) gs[tc] = chunk_sum16(ps[tc]);
+    if constexpr (NW == 1) {
+        if (RHS)
+#pragma unroll
+            for (int tc = 0; tc < NTC; tc++)
+                if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = gs[tc];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int r = kq + 4 * q;
+            H[r * LDH + li] = acc[0][q];
+            if constexpr (NZM == 32) {
+                H[r * LDH + 16 + li] = acc[1][q];
+                H[(16 + li) * LDH + r] = acc[1][q];
+                H[(16 + r) * LDH + 16 + li] = acc[2][q];
+            }
         }
-    }
+    } else {
+        double *pg = part + NW * NT * 256;
 #pragma unroll
-    for (int q = 0; q < 4; q++) {
-        const int r = kq + 4 * q;
-        H[r * LDH + li] = acc[0][q];
-        if constexpr (NZM == 32) {
-            H[r * LDH + 16 + li] = acc[1][q];
-            H[(16 + li) * LDH + r] = acc[1][q];
-            H[(16 + r) * LDH + 16 + li] = acc[2][q];
+        for (int t = 0; t < NT; t++)
+#pragma unroll
+            for (int q = 0; q < 4; q++) part[((wv * NT + t) * 4 + q) * 64 + lane] = acc[t][q];
+        if (RHS)
+#pragma unroll
+            for (int tc = 0; tc < NTC; tc++)
+                if (kq == 0) pg[wv * NZM + 16 * tc + li] = gs[tc];
+        __syncthreads();
+        for (int e = tid; e < NT * 256; e += 64 * NW) {
+            const int t = e >> 8, q = (e >> 6) & 3, ln = e & 63;
+            double v = 0.0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; w2++) v += part[((w2 * NT + t) * 4 + q) * 64 + ln];
+            const int r = (ln >> 4) + 4 * q, cl = ln & 15;
+            if (t == 0) H[r * LDH + cl] = v;
+            else if (t == 1) { H[r * LDH + 16 + cl] = v; H[(16 + cl) * LDH + r] = v; }
+            else H[(16 + r) * LDH + 16 + cl] = v;
+        }
+        if (RHS && tid < nz) {
+            double v = 0.0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; w2++) v += pg[w2 * NZM + tid];
+            g[tid] = v;
         }
     }
 }
 
 // g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping as gram_rhs, eight term
 // groups per batch so that 16 LDS loads are in flight before the FMAs need them.
-template <int NZL>
-__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, double *g, int nz, int lane)
+template <int NZL, int NW>
+__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, double *g, int nz, int tid,
+                                         double *part)
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, NTC = NZM / 16;
+    const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
     double ps[2][NTC];
 #pragma unroll
     for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
-    int t0 = 0;
-    for (; t0 + 32 <= cnt; t0 += 32) {
+    const int chunk = cnt / NW, tb = wv * chunk, te = tb + chunk;
+    int t0 = tb;
+    for (; t0 + 32 <= te; t0 += 32) {
         double a[8][NTC], c[8];
 #pragma unroll
         for (int u = 0; u < 8; u++) {
@@ -270,7 +328,7 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
             for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
     }
-    for (; t0 < cnt; t0 += 4) {
+    for (; t0 < te; t0 += 4) {
         const int r = t0 + kq;
         const double cc = CF[r];
 #pragma unroll
@@ -279,7 +337,20 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
     for (int tc = 0; tc < NTC; tc++) {
         const double sv = chunk_sum16(ps[0][tc] + ps[1][tc]);
-        if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
+        if constexpr (NW == 1) {
+            if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
+        } else {
+            if (kq == 0) part[wv * NZM + 16 * tc + li] = sv;
+        }
+    }
+    if constexpr (NW > 1) {
+        __syncthreads();
+        if (tid < nz) {
+            double v = 0.0;
+#pragma unroll
+            for (int w2 = 0; w2 < NW; w2++) v += part[w2 * NZM + tid];
+            g[tid] = v;
+        }
     }
 }
 
@@ -305,29 +376,32 @@ __device__ __forceinline__ double row_dot(const double *row, const double (&v)[N
 template <int NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
+    // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
+    // elimination is one basic block: the scheduler overlaps step k's row updates with the
+    // broadcast of row k+1, whose entries are updated first.
     int fail = 0;
-    double dinv = 1.0;
+    double cs = 1.0;
 #pragma unroll
     for (int k = 0; k < NZL; k++) {
-        if (k < nz) {
-            double piv = readlane_d(A[k], k);
-            if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
-            fail |= !(piv > 0.0);
-            const double inv = rcp_d(piv);
-            double rk[NZL];
+        double piv = readlane_d(A[k], k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        fail |= !(piv > 0.0);
+        const double inv = rcp_d(piv);
+        double rk[NZL];
 #pragma unroll
-            for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
-            const bool me = lane == k;
-            const double f = me ? 0.0 : A[k] * inv;
+        for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
+        const bool me = lane == k;
+        const double f = me ? 0.0 : A[k] * inv;
 #pragma unroll
-            for (int j = 0; j < NZL; j++)
-                if (j != k) A[j] = fma(-f, rk[j], A[j]);
-            A[k] = me ? 1.0 : -f;
-            dinv = me ? inv : dinv;
+        for (int jj = 0; jj < NZL; jj++) {
+            const int j = (k + 1 + jj) % NZL;           // next pivot row's entries first
+            if (j != k) A[j] = fma(-f, rk[j], A[j]);
         }
+        A[k] = me ? 1.0 : -f;
+        cs = me ? inv : cs;
     }
 #pragma unroll
-    for (int j = 0; j < NZL; j++) A[j] *= dinv;
+    for (int j = 0; j < NZL; j++) A[j] *= cs;
     return fail;
 }
 
@@ -505,8 +579,12 @@ __device__ __forceinline__ double slot_f(const Slot &q, const double *xs, double
 
 
 // --------------------------------------------------------------------------- main kernel
-// NZL: register bound on nz (one reduced-matrix row per lane); TS: trips of 64 slots.
-template <int NZL, int TS>
+// NZL: register bound on nz (one reduced-matrix row per lane); TS: slot trips per thread;
+// NW: wavefronts per agent (1, or 4 = one per SIMD of a CU for small batches).  With NW > 1
+// the row slots and the term-row passes are split across the waves and combined through LDS;
+// the reduced-system factorisation and solves run redundantly in every wave (identical data,
+// identical results, no communication).
+template <int NZL, int TS, int NW>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
                 const double *__restrict__ obstacles, int n_obs,
@@ -517,12 +595,13 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, LDH = NZM + 1;
-    const int lane = threadIdx.x;
+    constexpr int NTH = 64 * NW;                        // threads per agent
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz;
     const int NK = N * K, NE = 2 * (N - 1);
     const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N);
     // term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | obstacles (NK4) | 4 zero rows
-    const int rC = 4 * N, rU = rC + E4, rO = rU + UL4, TT = (rO + NK4 + 15) & ~15;
+    const int rC = 4 * N, rU = rC + E4, rO = rU + UL4, TT = (rO + NK4 + 16 * NW - 1) / (16 * NW) * (16 * NW);
     const TermLayout TL{N, C, n, nz, E4};
     const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK;
     const double tol = prm.tol, th = tol / sqrt(3.0);
@@ -545,23 +624,25 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double *eps = p; p += K + 1;
     double *zo = p; p += NK4;                           // obstacle duals (per-grid sums)
     int *sel = (int *)p; p += (K + 1);
+    double *red = p; p += (NW > 1) ? 8 * 4 * NW : 0;      // cross-wave reduction scratch, 8 sites
+    double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   // partial Gram / rhs
 #ifdef SRB_STAMPS
     unsigned long long *stamp_lds = (unsigned long long *)p; p += SRB_NSTAMP;
-    stamp_lds[lane] = 0;
+    if (tid < 64) stamp_lds[tid] = 0;
 #endif
     double *Rt = R + rC * LDR;                          // CoM-CoP rows
 
     STAMP_BEGIN();
     // ---- load inputs (a1/a2/a3: x0, reference window, footholds); zero the padded tables
     const double *x0 = x0g + 4 * (size_t)agent;
-    for (int i = lane; i < 4 * N; i += WAVE) ref[i] = refg[(size_t)agent * 4 * N + i];
-    for (int i = lane; i < 2 * C * N; i += WAVE) foot[i] = footg[(size_t)agent * 2 * C * N + i];
-    for (int i = lane; i < (int)(xs - R) + 2 * n4; i += WAVE) R[i] = 0.0;     // tables, matrices, vectors, xs, xb
-    for (int i = lane; i < NK4; i += WAVE) zo[i] = 0.0;
+    for (int i = tid; i < 4 * N; i += NTH) ref[i] = refg[(size_t)agent * 4 * N + i];
+    for (int i = tid; i < 2 * C * N; i += NTH) foot[i] = footg[(size_t)agent * 2 * C * N + i];
+    for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0;     // tables, matrices, vectors, xs, xb
+    for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0;
     SYNC();
 
     // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
-    if (lane == 0) {
+    if (tid == 0) {
         double X[4] = {x0[0], x0[1], x0[2], x0[3]};
         for (int k = 0; k < N; k++) {
             const double u0 = foot[(k * 2 + 0) * C + C - 1], u1 = foot[(k * 2 + 1) * C + C - 1];
@@ -575,7 +656,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         }
         xb[n - 1] = 0.0;
     }
-    for (int col = lane; col < nz - 1; col += WAVE) {
+    for (int col = tid; col < nz - 1; col += NTH) {
         const int j = col / (C - 1), t = col % (C - 1);
         double lam[4];
         const int is_null = lambda_basis(foot + j * 2 * C, C, t, lam);
@@ -594,21 +675,21 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int d = 0; d < 4; d++) v[d] = tt[d];
         }
     }
-    if (lane == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0;
+    if (tid == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0;
     SYNC();
     // CoM-CoP term rows M_e = Z_p - Z_u (p = CoM position of grid i, u = CoP of grid i+1); xs = xbar
-    if (lane < NE) {
-        const int i = lane >> 1, d = lane & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d;
-        for (int a = 0; a < NZL; a++) Rt[lane * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a];
+    if (tid < NE) {
+        const int i = tid >> 1, d = tid & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d;
+        for (int a = 0; a < NZL; a++) Rt[tid * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a];
     }
-    for (int v = lane; v < n; v += WAVE) xs[v] = xb[v];
+    for (int v = tid; v < n; v += NTH) xs[v] = xb[v];
 
     // ---- slot constants
     Slot Q[TS];
 #pragma unroll
     for (int t = 0; t < TS; t++) {
         Slot &q = Q[t];
-        const int sl = lane + 64 * t;
+        const int sl = tid + NTH * t;
         q.kind = K_NONE; q.i0 = q.i1 = 0; q.r = 0; q.h[0] = q.h[1] = 0.0; q.a0 = q.a1 = 0.0; q.rx = 0.0; q.jd = 0.0;
         q.m[0] = q.m[1] = 0.0; q.wr = TT;
         if (sl < sE) {                                   // VAR
@@ -648,9 +729,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
         STAMP_STAGE(stage);
-        const int nts = ((nl ? S : sV) + 63) / 64;            // active slot trips
+        const int nts = ((nl ? S : sV) + NTH - 1) / NTH;      // active slot trips
         const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
-        const int cnt = ((nl ? rO + NK4 : rO) + 15) & ~15;     // term rows in this stage (zero-padded to 16)
+        const int cnt = ((nl ? rO + NK4 : rO) + 16 * NW - 1) / (16 * NW) * (16 * NW);   // term rows (zero-padded)
         STAMP_BEGIN();
         // stage activity of each row
 #pragma unroll
@@ -676,7 +757,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
             SYNC();
-            gram_rhs<NZL, true>(R, W, CF, cnt, H0, vg, nz, lane);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
             if (gj_invert<NZL>(Mi, nz, lane, 1) != 0) {
@@ -697,7 +778,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.m[1] != 0.0) { mn = fmin(mn, z1); mx = fmax(mx, z1); }
                 }
             double rv[2] = {-mn, mx};
-            wred<2, 3u>(rv);
+            wred_x<2, 3u, NW>(rv, red + 0 * 4 * NW, tid);
             mn = -rv[0]; mx = rv[1];
             const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn, zsh = (mx < 0) ? 0.0 : 1.0 + mx;
             SYNC();                                           // every lane has read xs = xbar
@@ -716,14 +797,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         } else {
             // ---------------- NLP stage setup (replaces SnoptSolver::Solve, MPC_dist.cpp:402-427) ----------------
             if (x_qp_out)
-                for (int v = lane; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = xs[v];
+                for (int v = tid; v < n; v += NTH) x_qp_out[(size_t)agent * n + v] = xs[v];
             // obstacles per grid: the K_obs nearest static obstacles (MPC_dist.cpp:371-396,
             // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
             // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
 #pragma clang loop unroll(disable)
             for (int tsel = 0; tsel < 2; tsel++) {
                 const int Kt = tsel ? prm.K_nbr : prm.K_obs;
-                if (Kt > 0)
+                if (Kt > 0 && wv == 0)
                     knn_select(lane, x0[0], x0[2], tsel ? nbr_state : obstacles, tsel ? 4 : 2, tsel ? n_all : n_obs,
                                tsel ? agent_offset + agent : -1, Kt, sel + (tsel ? prm.K_obs : 0));
             }
@@ -731,14 +812,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int j = 0; j < K; j++) {
                 const bool st = j < prm.K_obs;
                 const int bi = sel[j];
-                if (lane < N && bi >= 0) {
-                    const int k = lane;
+                if (tid < N && bi >= 0) {
+                    const int k = tid;
                     const double tt = st ? 0.0 : prm.Ts * (k + 1);
                     const double *srcp = st ? obstacles + 2 * (size_t)bi : nbr_state + 4 * (size_t)bi;
                     obs[2 * (k * K + j)] = srcp[0] + (st ? 0.0 : srcp[2] * tt);
                     obs[2 * (k * K + j) + 1] = srcp[1] + (st ? 0.0 : srcp[3] * tt);
                 }
-                if (lane == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr;
+                if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr;
             }
             SYNC();
             // slacks: shifted h - g(x) over every NLP row; duals 1
@@ -749,7 +830,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 if (t < nts) {
                     Slot &q = Q[t];
                     if (q.kind == K_OBS) {
-                        const int o = lane + 64 * t - sO;
+                        const int o = tid + NTH * t - sO;
                         q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K];
                     }
                     const double f = slot_f(q, xs, s_var);
@@ -757,7 +838,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.m[0] != 0.0) mn = fmin(mn, q.h[0] - f);
                     if (q.m[1] != 0.0) mn = fmin(mn, q.h[1] + f);
                 }
-            mn = wmin(mn);
+            {
+                double rv[1] = {-mn};
+                wred_x<1, 1u, NW>(rv, red + 1 * 4 * NW, tid);
+                mn = -rv[0];
+            }
             const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn;
 #pragma unroll
             for (int t = 0; t < TS; t++)
@@ -780,7 +865,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = 1.0; }
                 }
             SYNC();
-            gram_rhs<NZL, true>(R, W, CF, cnt, ZZ, vg, nz, lane);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, ZZ, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_invert<NZL>(Mi, nz, lane, 0);
@@ -834,7 +919,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             }
             {
                 double rv[4] = {nrx, nrz, sz, gm};
-                wred<4, 8u>(rv);
+                wred_x<4, 8u, NW>(rv, red + 2 * 4 * NW, tid);
                 nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3];
             }
             const double mu = sz * inv_m;
@@ -872,6 +957,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         CF[q.wr] = cf;
                     }
                 }
+                if (NW > 1) SYNC();             // other waves' plain stores land before the VEL adds
                 if (nl)
 #pragma unroll
                     for (int t = 0; t < TS; t++)
@@ -896,6 +982,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                         W[q.wr] = om + ((kind_of(q) == K_VAR) ? q.a0 + hs : 0.0);
                     }
+                if (NW > 1) SYNC();
                 if (nl)
 #pragma unroll
                     for (int t = 0; t < TS; t++)
@@ -904,7 +991,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 set_rhs(0);
                 SYNC();
-                gram_rhs<NZL, true>(R, W, CF, cnt, H0, vg, nz, lane);
+                gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
                 SYNC();
                 STAMP_END(4);
                 double dstart = 0.0;
@@ -938,7 +1025,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     set_rhs(pass);
                     SYNC();
                     STAMP_END(6 + 4 * pass);
-                    rhs_only<NZL>(R, CF, cnt, vg, nz, lane);
+                    rhs_only<NZL, NW>(R, CF, cnt, vg, nz, tid, part);
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
@@ -961,7 +1048,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 // findsteplength (Auxilary.c:271-294): 1 / max(-dv / v), 1 when no dv < 0
                 {
                     double rv[2] = {mxs, mxz};
-                    wred<2, 3u>(rv);
+                    wred_x<2, 3u, NW>(rv, red + (3 + 2 * pass) * 4 * NW, tid);
                     mxs = rv[0]; mxz = rv[1];
                 }
                 ap = (mxs > 0.0) ? 1.0 / mxs : 1.0;
@@ -977,7 +1064,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             num = fma(q.m[0] * fma(ap, q.ds[0], q.s[0]), fma(ad, q.dz[0], q.z[0]), num);
                             num = fma(q.m[1] * fma(ap, q.ds[1], q.s[1]), fma(ad, q.dz[1], q.z[1]), num);
                         }
-                    num = wsum(num);
+                    {
+                        double rv[1] = {num};
+                        wred_x<1, 0u, NW>(rv, red + 4 * 4 * NW, tid);
+                        num = rv[0];
+                    }
                     const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
                     sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
                     continue;
@@ -1034,7 +1125,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     }
     SYNC();
     if (x_qp_out && nstage == 1)
-        for (int v = lane; v < n; v += WAVE) x_qp_out[(size_t)agent * n + v] = xs[v];
+        for (int v = tid; v < n; v += NTH) x_qp_out[(size_t)agent * n + v] = xs[v];
 
     // ---- outputs
     double f = 0.0;
@@ -1047,28 +1138,32 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             f += fma(0.5 * q.a0 * xv, xv, q.a1 * xv);
         }
     }
-    f = wsum(f);
+    {
+        double rv[1] = {f};
+        wred_x<1, 0u, NW>(rv, red + 6 * 4 * NW, tid);
+        f = rv[0];
+    }
     // ---- fitComTrajectory_eventbase (MPC_dist.cpp:784-855) as an epilogue: alpha_COM (4 x 5)
     // interpolates [buffer, X_0..X_3] at s = 0, 1/4, 1/2, 3/4, 1 (the reference's 24 x 24 KKT
     // keeps only the s = 0 end-point row, so its solution is this interpolation), i.e.
     // alpha[d][j] = sum_i Binv[j][i] p_i[d] with the host-inverted 5 x 5 Bernstein matrix.
-    if (alpha_out && lane < 20) {
-        const int d = lane / 5, j = lane - 5 * (lane / 5);
+    if (alpha_out && tid < 20) {
+        const int d = tid / 5, j = tid - 5 * (tid / 5);
         double acc = prm.Binv[5 * j] * alpha_buf[(size_t)agent * 4 + d];
         for (int i = 1; i < 5; i++) acc = fma(prm.Binv[5 * j + i], xs[4 * (i - 1) + d], acc);
         alpha_out[(size_t)agent * 20 + 5 * d + j] = acc;
     }
     STAMP_END(15);
     STAMP_FLUSH(agent);
-    if (lane == 0) {
+    if (tid == 0) {
         obj_out[agent] = f;
         status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
         iters_out[2 * agent] = qp_it; iters_out[2 * agent + 1] = nlp_it;
     }
 }
 
-#define SRB_NMPC_KERNEL(NZL, TS)                                                                               \
-    extern "C" __global__ void __launch_bounds__(WAVE) srb_nmpc_kernel_##NZL##_##TS(                          \
+#define SRB_NMPC_KERNEL(NZL, TS, NW)                                                                           \
+    extern "C" __global__ void __launch_bounds__(64 * NW) srb_nmpc_kernel_##NZL##_##TS##_##NW(                \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
@@ -1078,7 +1173,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        nmpc_agent<NZL, TS>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
+        nmpc_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
                                 x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, lds);  \
     }
 
