@@ -97,6 +97,8 @@ public:
         agent_initial_[0] = Pstart((long)(2 * agent_id_), 0);
         agent_initial_[1] = Pstart((long)(2 * agent_id_ + 1), 0);
         alpha_buffer_ = {agent_initial_[0], 0.0, agent_initial_[1], 0.0};
+        pstart_.resize((size_t)Pstart.rows());
+        for (long i = 0; i < (long)Pstart.rows(); i++) pstart_[(size_t)i] = Pstart(i, 0);
     }
     /* Pobs / Pobs_real: 2 x NOBS (MPC_dist.hpp:85-86); run_NMPC uses Pobs_real (:371-396) */
     template <class M> void setPobs(const M &P) { copy_obs(P, pobs_); }
@@ -106,9 +108,22 @@ public:
         pobs_real_.assign(xy_colmajor, xy_colmajor + 2 * n_obs);
     }
 
-    /* Output of the HL planner (generateReferenceTrajectory, MPC_dist.cpp:930-1104):
-     * Pr_refined_, Prd_refined_ as 2*NA x T column-major arrays.  The HL planner itself is
-     * SURVEY.md 8(f) row 3 and not part of this boundary. */
+    /* MPC_dist.cpp:930-1104 on the device (srb_hl_plan): every agent from Pstart around the
+     * planner obstacles Pobs; fills Pr_refined_ / Prd_refined_ (2NA x loop/40). */
+    void generateReferenceTrajectory(int loop = 100000)
+    {
+        if (pstart_.empty()) throw std::runtime_error("MPC_dist: setPstart() not called");
+        const int NA = (int)(pstart_.size() / 2), T = loop / 40;
+        pr_.assign((size_t)2 * NA * T, 0.0);
+        prd_.assign((size_t)2 * NA * T, 0.0);
+        if (srb_hl_plan(device_, NA, pstart_.data(), pobs_.empty() ? nullptr : pobs_.data(),
+                        (int)(pobs_.size() / 2), loop, pr_.data(), prd_.data()) != SRB_OK)
+            throw std::runtime_error(srb_last_error());
+        ref_rows_ = 2 * NA; ref_cols_ = T;
+    }
+
+    /* Output of the HL planner (generateReferenceTrajectory) when the caller already holds it:
+     * Pr_refined_, Prd_refined_ as 2*NA x T column-major arrays. */
     void setReferenceTrajectory(const double *Pr, const double *Prd, int rows, int cols)
     {
         pr_.assign(Pr, Pr + (size_t)rows * cols);
@@ -208,6 +223,9 @@ public:
     const std::vector<double> &qp_solution() const { return x_qp_; }
     std::pair<int, int> last_status() const { return {status_[0], status_[1]}; }
     std::pair<int, int> last_iters() const { return {iters_[0], iters_[1]}; }
+    /* Pr_refined_ / Prd_refined_ (2NA x T column-major) as generateReferenceTrajectory left them */
+    const std::vector<double> &Pr_refined() const { return pr_; }
+    const std::vector<double> &Prd_refined() const { return prd_; }
     size_t gaitDomain() const { return gaitDomain_; }
 
 private:
@@ -277,7 +295,7 @@ private:
     double distance_to_fail_ = 10.0;             /* MPC_dist.cpp:51 */
     std::array<double, 2> agent_initial_{{0.0, 0.0}};
     std::array<double, 4> alpha_buffer_{{0.0, 0.0, 0.0, 0.0}};
-    std::vector<double> pobs_, pobs_real_, pr_, prd_;
+    std::vector<double> pstart_, pobs_, pobs_real_, pr_, prd_;
     long ref_rows_ = 0, ref_cols_ = 0;
     double q_[18] = {0}, dq_[18] = {0};
     int contact_[4] = {1, 1, 1, 1};

@@ -9,10 +9,10 @@ reads the same:
     mpc.updateState(q, dq, contactInd, toePos, state_other); mpc.run_NMPC()
     alpha = mpc.get_alphaCOM(); X = mpc.get_MPCsol(); last = mpc.get_lastState()
 
-run_NMPC keeps the reference's host-side planners (copPlanner_eventbase, footholdsPlanner,
-fitComTrajectory_eventbase) and sends the solve to the GPU as a batch of one.
-generateReferenceTrajectory (the offline HL planner, MPC_dist.cpp:930-1104) is the
-SURVEY.md §8(f) row 3 follow-up: callers pass its output with setReferenceTrajectory.
+run_NMPC keeps the reference's host-side planners (copPlanner_eventbase, footholdsPlanner)
+and sends the solve (with the fused Bezier fit) to the GPU as a batch of one.
+generateReferenceTrajectory (the offline HL planner, MPC_dist.cpp:930-1104) runs on the
+GPU through srb_hl_plan; callers that already hold its output use setReferenceTrajectory.
 """
 from __future__ import annotations
 
@@ -73,9 +73,14 @@ class MPCDist:
         self.Pr_refined_ = np.asarray(Pr, dtype=np.float64)
         self.Prd_refined_ = np.asarray(Prd, dtype=np.float64)
 
-    def generateReferenceTrajectory(self):
-        raise NotImplementedError("HL reference planner is a SURVEY.md §8(f) follow-up; "
-                                  "pass its output with setReferenceTrajectory(Pr, Prd)")
+    def generateReferenceTrajectory(self, loop: int = 100000):
+        """MPC_dist.cpp:930-1104 on the device (srb_hl_plan): all agents from Pstart_ around
+        the planner obstacles Pobs (2 x n_obs); fills Pr_refined_ / Prd_refined_ (2NA x loop/40)."""
+        if self.Pstart_ is None:
+            raise RuntimeError("MPC_dist: setPstart() not called")
+        from . import hl_plan
+        self.Pr_refined_, self.Prd_refined_ = hl_plan(self.Pstart_.reshape(-1, 2), self.Pobs.T, loop,
+                                                      self.device)
 
     def updateState(self, q, dq, ind, toePos, state_other):
         self.q = np.asarray(q, dtype=np.float64).ravel()[:18].copy()

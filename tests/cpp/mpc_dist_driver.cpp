@@ -3,14 +3,42 @@
 //   mpc_dist_driver <input.txt> <use_snopt 0|1>
 // input.txt: x0[4] (x, xdot, y, ydot) | ref[16] (4 grids x (x, xdot, y, ydot)) | n_obs | obs xy...
 // stdout: status qp nlp, then get_MPCsol (16), qp_solution (24), get_alphaCOM (20, row-major).
+//   mpc_dist_driver hl <loop>
+// HL planner (src/A1_Sim.cpp:1152-1156): setPstart / setPobs / generateReferenceTrajectory for
+// the reference's 4-agent start and 3 obstacles; stdout: Pr_refined_ then Prd_refined_.
 #include <cstdio>
 #include <cstdlib>
 #include <fstream>
+#include <string>
 #include <vector>
 #include "srbnmpc_mpc_dist.hpp"
 
+static int hl_mode(int loop)
+{
+    srbnmpc::MPC_dist mpc;
+    mpc.setAgentID(0);
+    srbnmpc::Mat Pstart = srbnmpc::Mat::Zero(8, 1);
+    const double ps[8] = {0.0, 0.0, 0.0, -0.9, -1, 0, -1, -0.9};   // src/A1_Sim.cpp:1013
+    for (int i = 0; i < 8; i++) Pstart(i, 0) = ps[i];
+    srbnmpc::Mat Pobs = srbnmpc::Mat::Zero(2, 3);
+    const double po[6] = {3.0, 0.2, 5.0, -0.6, 7.0, 0.4};
+    for (int j = 0; j < 3; j++) { Pobs(0, j) = po[2 * j]; Pobs(1, j) = po[2 * j + 1]; }
+    try {
+        mpc.setPstart(Pstart);
+        mpc.setPobs(Pobs);
+        mpc.generateReferenceTrajectory(loop);
+    } catch (const std::exception &e) {
+        std::fprintf(stderr, "error: %s\n", e.what());
+        return 3;
+    }
+    for (double v : mpc.Pr_refined()) std::printf("%.17g\n", v);
+    for (double v : mpc.Prd_refined()) std::printf("%.17g\n", v);
+    return 0;
+}
+
 int main(int argc, char **argv)
 {
+    if (argc >= 3 && std::string(argv[1]) == "hl") return hl_mode(std::atoi(argv[2]));
     if (argc < 3) { std::fprintf(stderr, "usage: %s input.txt use_snopt\n", argv[0]); return 2; }
     std::ifstream in(argv[1]);
     double x0[4], ref[16];

@@ -54,3 +54,23 @@ def test_shim_on_reference_instance(tmp_path, kat2):
     np.testing.assert_allclose(xq, kat2["logged_qp_x"], atol=2e-9)
     import oracle
     np.testing.assert_allclose(alpha, oracle.fit_bezier([0, 0, 0, 0], X.reshape(4, 4)), atol=1e-9)
+
+
+@pytest.mark.gpu
+def test_shim_hl_planner_matches_oracle(tmp_path):
+    """generateReferenceTrajectory through the C++ shim == the CPU restatement, bit for bit."""
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    exe = build_driver(tmp_path)
+    loop = 4000
+    r = subprocess.run([exe, "hl", str(loop)], capture_output=True, text=True, timeout=120)
+    assert r.returncode == 0, r.stderr
+    nums = np.array([float(t) for t in r.stdout.split()])
+    T = loop // 40
+    Pr = nums[:8 * T].reshape(T, 8).T
+    Prd = nums[8 * T:].reshape(T, 8).T
+    import oracle
+    R, Rd = oracle.hl_plan([0.0, 0.0, 0.0, -0.9, -1, 0, -1, -0.9], [[3.0, 0.2], [5.0, -0.6], [7.0, 0.4]], loop=loop)
+    np.testing.assert_array_equal(Pr, R)
+    np.testing.assert_array_equal(Prd, Rd)

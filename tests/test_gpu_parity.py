@@ -342,3 +342,38 @@ def test_hl_planner_bitwise_vs_oracle(NA, n_obs, loop):
     assert Pr.shape == (2 * NA, loop // 40)
     np.testing.assert_array_equal(Pr, R)
     np.testing.assert_array_equal(Prd, Rd)
+
+
+def test_closed_loop_hl_to_solve_through_mpcdist():
+    """A1_Sim.cpp:1152-1156 then :180-197 for several control cycles: the device HL planner
+    feeds MPCDist.run_NMPC; every cycle's solve equals the oracle on the same inputs and the
+    agent's predicted state seeds the next cycle."""
+    Ps = np.array([0.0, 0.0, 0.0, -0.9, -1, 0, -1, -0.9])             # src/A1_Sim.cpp:1013
+    Pobs = np.array([[3.0, 0.2], [5.0, -0.6], [7.0, 0.4]])
+    m = srbnmpc.MPCDist()
+    m.setAgentID(1)
+    m.setPstart(Ps)
+    m.setPobs(Pobs.T)
+    m.setPobs_real(Pobs.T)
+    m.generateReferenceTrajectory(loop=4000)
+    R, Rd = oracle.hl_plan(Ps, Pobs, loop=4000)
+    np.testing.assert_array_equal(m.Pr_refined_, R)
+    np.testing.assert_array_equal(m.Prd_refined_, Rd)
+    m.use_snopt = True
+    p = oracle.params(4, 4, K_obs=1, use_nlp=1)
+    q = np.zeros(18); dq = np.zeros(18)
+    q[:2] = Ps[2:4]
+    for cyc in range(6):
+        m.updateState(q, dq, [1, 1, 1, 1], np.zeros((3, 4)), np.zeros(4))
+        ref = m.copPlanner_eventbase()
+        foot = np.repeat(m.footholdsPlanner()[None], 4, 0)
+        x0 = np.array([q[0], dq[0], q[1], dq[1]])
+        m.run_NMPC()
+        r = oracle.solve_batch(p, x0[None], ref[None], foot[None], Pobs)
+        assert m.last_status.tolist() == r["status"][0].tolist(), (cyc, m.last_status, r["status"])
+        assert m.last_status[0] == 0
+        np.testing.assert_allclose(m.qp_solution_eventbased_, r["x_qp"][0], atol=QP_TOL)
+        np.testing.assert_allclose(m.get_MPCsol().ravel(), r["x"][0][:16], atol=NLP_TOL)
+        X = m.get_MPCsol().reshape(4, 4)
+        q[0], dq[0], q[1], dq[1] = X[3]
+    assert m.gaitDomain_ == 6
