@@ -363,8 +363,11 @@ def test_closed_loop_hl_to_solve_through_mpcdist():
     p = oracle.params(4, 4, K_obs=1, use_nlp=1)
     q = np.zeros(18); dq = np.zeros(18)
     q[:2] = Ps[2:4]
+    from srbnmpc.mpc_dist import INIT_FOOTPRINT
     for cyc in range(6):
-        m.updateState(q, dq, [1, 1, 1, 1], np.zeros((3, 4)), np.zeros(4))
+        toe = np.zeros((3, 4))                 # stance around the current CoM (the simulator's toePos)
+        toe[0] = INIT_FOOTPRINT[:, 0] + q[0]; toe[1] = INIT_FOOTPRINT[:, 1] + q[1]
+        m.updateState(q, dq, [1, 1, 1, 1], toe, np.zeros(4))
         ref = m.copPlanner_eventbase()
         foot = np.repeat(m.footholdsPlanner()[None], 4, 0)
         x0 = np.array([q[0], dq[0], q[1], dq[1]])
@@ -372,7 +375,8 @@ def test_closed_loop_hl_to_solve_through_mpcdist():
         r = oracle.solve_batch(p, x0[None], ref[None], foot[None], Pobs)
         assert m.last_status.tolist() == r["status"][0].tolist(), (cyc, m.last_status, r["status"])
         assert m.last_status[0] == 0
-        np.testing.assert_allclose(m.qp_solution_eventbased_, r["x_qp"][0], atol=QP_TOL)
+        np.testing.assert_allclose(xus(4, m.qp_solution_eventbased_), xus(4, r["x_qp"][0]), atol=QP_TOL)   # lambda
+        # is not unique with 4 contacts
         np.testing.assert_allclose(m.get_MPCsol().ravel(), r["x"][0][:16], atol=NLP_TOL)
         X = m.get_MPCsol().reshape(4, 4)
         q[0], dq[0], q[1], dq[1] = X[3]

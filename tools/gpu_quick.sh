@@ -11,3 +11,7 @@ for c in 2 3 5; do
   timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_c$c.json 2> gpurun_out/bench_c$c.err || { tail -5 gpurun_out/bench_c$c.err; exit 1; }
   python -c "import json;d=json.load(open('gpurun_out/bench_c$c.json'));r=d['roofline'];print($c, round(d['value']), 'solves/s', round(d['ms_per_step'],3),'ms/step p99',round(d['p99_ms'],3),'kernel',round(r['kernel_ms'],3),'iters',d['iters_mean'],'opt',d['optimal_frac'])"
 done
+if [ -f srb-cbf-nmpc_amd/srbnmpc/libsrbnmpc_stamps.so ]; then
+  timeout -k 10 120 python tools/stamps.py > gpurun_out/stamps.log 2>&1 || { tail -5 gpurun_out/stamps.log; exit 1; }
+  cat gpurun_out/stamps.log
+fi
