@@ -231,3 +231,64 @@ def iswift_ref_ccs(n, m, pp, Pjc, Pir, Ppr, Ajc, Air, Apr, Gjc, Gir, Gpr, c, h, 
     f = R.iswift_ref_solve_ccs(n, m, pp, *[_ptr(a) for a in arrs], _ptr(cc), _ptr(hh), _ptr(bb), _ptr(pr), _ptr(x),
                                ctypes.byref(it))
     return x, f, it.value
+
+
+# ---------------------------------------------------------------- low-level CLF-QP (ll_ctrl.c)
+class OrcLLParams(ctypes.Structure):
+    _fields_ = [("mu", ctypes.c_double), ("kp", ctypes.c_double), ("kd", ctypes.c_double), ("useCLF", ctypes.c_int),
+                ("tauPen", ctypes.c_double), ("dfPen", ctypes.c_double), ("auxPen", ctypes.c_double),
+                ("clfPen", ctypes.c_double), ("auxMax", ctypes.c_double), ("clfEps", ctypes.c_double),
+                ("maxit", ctypes.c_int), ("tol", ctypes.c_double)]
+
+
+class OrcLLAgent(ctypes.Structure):
+    _fields_ = [("ind", ctypes.c_int * 4)] + [(k, _dp) for k in (
+        "q", "dq", "Dinv", "B", "Hv", "Jc", "dJc", "Js", "Jtoe", "Jhip", "toePos", "hipPos",
+        "H0", "dH0", "y", "dy", "hd", "dhd", "fDes")]
+
+
+LL_IN = ("q", "dq", "Dinv", "B", "Hv", "Jc", "dJc", "Js", "Jtoe", "Jhip", "toePos", "hipPos",
+         "H0", "dH0", "y", "dy", "hd", "dhd", "fDes")
+
+
+def ll_params(**kw) -> OrcLLParams:
+    p = OrcLLParams()
+    lib().orc_ll_params_default(ctypes.byref(p))
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def ll_build_qp(p: OrcLLParams, batch: dict, a: int = 0):
+    """Dense QP of LowLevelCtrl::cost/constraints for agent a: (P diag, c, A, b, G, h, V, Veps, LfV, LgV)."""
+    ag = OrcLLAgent()
+    keep = {}
+    for i in range(4):
+        ag.ind[i] = int(batch["ind"][a][i])
+    for k in LL_IN:
+        keep[k] = _c(batch[k][a]).reshape(-1)
+        setattr(ag, k, _ptr(keep[k]))
+    Pd = np.zeros(32); c = np.zeros(32); A = np.zeros(18 * 32); b = np.zeros(18); G = np.zeros(45 * 32)
+    h = np.zeros(45); clf = np.zeros(3); LgV = np.zeros(18)
+    n, pp, m = ctypes.c_int(), ctypes.c_int(), ctypes.c_int()
+    lib().orc_ll_build_qp(ctypes.byref(p), ctypes.byref(ag), ctypes.byref(n), ctypes.byref(pp), ctypes.byref(m),
+                          _ptr(Pd), _ptr(c), _ptr(A), _ptr(b), _ptr(G), _ptr(h), _ptr(clf), _ptr(LgV))
+    n, pp, m = n.value, pp.value, m.value
+    return (Pd[:n].copy(), c[:n].copy(), A[:pp * n].reshape(pp, n).copy(), b[:pp].copy(),
+            G[:m * n].reshape(m, n).copy(), h[:m].copy(), clf[0], clf[1], clf[2], LgV.copy())
+
+
+def ll_calc_torque(p: OrcLLParams, batch: dict):
+    """calcTorque (LowLevelCtrl.cpp:18-113) for every agent of a ll_workload batch."""
+    A_ = batch["ind"].shape[0]
+    arrs = [_c(batch[k]).reshape(A_, -1) for k in LL_IN]
+    ind = _c(batch["ind"], np.int32).reshape(A_, 4)
+    tau = _c(batch["tau"]).reshape(A_, 18).copy()
+    out = dict(tau=tau, QP_force=np.zeros((A_, 12)), ddq=np.zeros((A_, 18)), dq=np.zeros((A_, 18)),
+               q=np.zeros((A_, 18)), V=np.zeros(A_), dV=np.zeros(A_), x=np.zeros((A_, 32)),
+               status=np.zeros(A_, np.int32), iters=np.zeros(A_, np.int32))
+    lib().orc_ll_calc_torque_batch(ctypes.byref(p), A_, _ptr(ind), *[_ptr(a) for a in arrs], _ptr(tau),
+                                   _ptr(out["QP_force"]), _ptr(out["ddq"]), _ptr(out["dq"]), _ptr(out["q"]),
+                                   _ptr(out["V"]), _ptr(out["dV"]), _ptr(out["x"]), _ptr(out["status"]),
+                                   _ptr(out["iters"]))
+    return out

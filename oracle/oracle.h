@@ -110,6 +110,42 @@ void orc_fit_bezier(const double buf[4], const double *X, double alpha[20]);
  * column-major 2NA x (loop / 40). */
 void orc_hl_plan(int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr, double *Prd);
 
+/* ---- low-level CLF-QP controller (ll_ctrl.c; LowLevelCtrl::calcTorque, LowLevelCtrl.cpp:18-113) */
+typedef struct orc_ll_params {
+    double mu, kp, kd;                  /* Settings::LL_params (global_loco_structs.hpp:96-111) */
+    int useCLF;
+    double tauPen, dfPen, auxPen, clfPen, auxMax, clfEps;
+    int maxit;                          /* iSWIFT MAXIT 25, tolerance 1e-6 (GlobalOptions.h:23-25) */
+    double tol;
+} orc_ll_params;
+
+/* one agent's inputs; column-major matrices with the leading dimensions of srb_ll_io */
+typedef struct orc_ll_agent {
+    int ind[4];
+    const double *q, *dq, *Dinv, *B, *Hv, *Jc, *dJc, *Js, *Jtoe, *Jhip, *toePos, *hipPos;
+    const double *H0, *dH0, *y, *dy, *hd, *dhd, *fDes;
+} orc_ll_agent;
+
+typedef struct orc_ll_out {
+    double tau[18];        /* in/out (the reference's member array, tau[0..5] accumulate) */
+    double QP_force[12], ddq[18], dq[18], q[18], V, dV, x[32];
+    int status, iters;
+} orc_ll_out;
+
+void orc_ll_params_default(orc_ll_params *p);
+/* dense QP of LowLevelCtrl::cost/constraints (row-major A, G); clf = {V, Veps, LfV} */
+int orc_ll_build_qp(const orc_ll_params *prm, const orc_ll_agent *in,
+                    int *n_out, int *p_out, int *m_out, double *Pd, double *c, double *A, double *b,
+                    double *G, double *h, double clf[3], double *LgV);
+int orc_ll_calc_torque(const orc_ll_params *prm, const orc_ll_agent *in, orc_ll_out *out);
+int orc_ll_calc_torque_batch(const orc_ll_params *prm, int n_agents, const int *ind, const double *q, const double *dq,
+                             const double *Dinv, const double *B, const double *Hv, const double *Jc, const double *dJc,
+                             const double *Js, const double *Jtoe, const double *Jhip, const double *toePos,
+                             const double *hipPos, const double *H0, const double *dH0, const double *y,
+                             const double *dy, const double *hd, const double *dhd, const double *fDes, double *tau,
+                             double *QP_force, double *ddq, double *dq_out, double *q_out, double *V, double *dV,
+                             double *x, int *status, int *iters);
+
 /* dense helpers (linalg.c) */
 int orc_chol(int n, double *A);                               /* in place, lower */
 void orc_chol_solve(int n, const double *L, double *x);

@@ -21,8 +21,9 @@
 typedef struct {
     int n, m, p;
     const double *Pd, *Pf, *A, *G;   /* P diagonal (Pd) or full row-major (Pf, when non-NULL) */
-    int *gnz;      /* [m][4] column indices of row r's nonzeros (-1 padded) */
-    double *gval;  /* [m][4] */
+    int gk;        /* max nonzeros of a G row */
+    int *gnz;      /* [m][gk] column indices of row r's nonzeros (-1 padded) */
+    double *gval;  /* [m][gk] */
     double *H, *t1, *t2;
     double *K; int *piv;
 } kktws;
@@ -30,13 +31,20 @@ typedef struct {
 static void ws_init(kktws *w, int n, int m, int p, const double *Pd, const double *A, const double *G)
 {
     w->n = n; w->m = m; w->p = p; w->Pd = Pd; w->Pf = NULL; w->A = A; w->G = G;
-    w->gnz = (int *)malloc(sizeof(int) * 4 * (m ? m : 1));
-    w->gval = (double *)malloc(sizeof(double) * 4 * (m ? m : 1));
+    int gk = 1;
     for (int r = 0; r < m; r++) {
         int k = 0;
-        for (int j = 0; j < 4; j++) { w->gnz[4 * r + j] = -1; w->gval[4 * r + j] = 0; }
-        for (int j = 0; j < n && k < 4; j++)
-            if (G[(size_t)r * n + j] != 0.0) { w->gnz[4 * r + k] = j; w->gval[4 * r + k] = G[(size_t)r * n + j]; k++; }
+        for (int j = 0; j < n; j++) k += (G[(size_t)r * n + j] != 0.0);
+        if (k > gk) gk = k;
+    }
+    w->gk = gk;
+    w->gnz = (int *)malloc(sizeof(int) * (size_t)gk * (size_t)(m > 0 ? m : 1));
+    w->gval = (double *)malloc(sizeof(double) * (size_t)gk * (size_t)(m > 0 ? m : 1));
+    for (int r = 0; r < m; r++) {
+        int k = 0;
+        for (int j = 0; j < gk; j++) { w->gnz[gk * r + j] = -1; w->gval[gk * r + j] = 0; }
+        for (int j = 0; j < n; j++)
+            if (G[(size_t)r * n + j] != 0.0) { w->gnz[gk * r + k] = j; w->gval[gk * r + k] = G[(size_t)r * n + j]; k++; }
     }
     w->H = (double *)malloc(sizeof(double) * n * n);
     w->t1 = (double *)malloc(sizeof(double) * (n + p + m + 8));
@@ -55,7 +63,7 @@ static void gmul(const kktws *w, const double *x, double *y)   /* y = G x */
 {
     for (int r = 0; r < w->m; r++) {
         double s = 0;
-        for (int k = 0; k < 4; k++) if (w->gnz[4 * r + k] >= 0) s += w->gval[4 * r + k] * x[w->gnz[4 * r + k]];
+        for (int k = 0; k < w->gk; k++) if (w->gnz[w->gk * r + k] >= 0) s += w->gval[w->gk * r + k] * x[w->gnz[w->gk * r + k]];
         y[r] = s;
     }
 }
@@ -63,7 +71,7 @@ static void gmul(const kktws *w, const double *x, double *y)   /* y = G x */
 static void gtmul_add(const kktws *w, const double *v, double *y)   /* y += G' v */
 {
     for (int r = 0; r < w->m; r++)
-        for (int k = 0; k < 4; k++) if (w->gnz[4 * r + k] >= 0) y[w->gnz[4 * r + k]] += w->gval[4 * r + k] * v[r];
+        for (int k = 0; k < w->gk; k++) if (w->gnz[w->gk * r + k] >= 0) y[w->gnz[w->gk * r + k]] += w->gval[w->gk * r + k] * v[r];
 }
 
 /* factor for weights wgt (W = diag(wgt)); returns 0 on success */
@@ -76,11 +84,11 @@ static int kkt_factor(kktws *w, const double *wgt)
     else for (int i = 0; i < n; i++) H[i * n + i] = w->Pd[i];
     for (int r = 0; r < m; r++) {
         double iw = 1.0 / wgt[r];
-        for (int a = 0; a < 4; a++) {
-            int ia = w->gnz[4 * r + a]; if (ia < 0) continue;
-            for (int bb = 0; bb < 4; bb++) {
-                int ib = w->gnz[4 * r + bb]; if (ib < 0) continue;
-                H[ia * n + ib] += iw * w->gval[4 * r + a] * w->gval[4 * r + bb];
+        for (int a = 0; a < w->gk; a++) {
+            int ia = w->gnz[w->gk * r + a]; if (ia < 0) continue;
+            for (int bb = 0; bb < w->gk; bb++) {
+                int ib = w->gnz[w->gk * r + bb]; if (ib < 0) continue;
+                H[ia * n + ib] += iw * w->gval[w->gk * r + a] * w->gval[w->gk * r + bb];
             }
         }
     }

@@ -13,6 +13,10 @@ Fixtures written (data only -- inputs and expected outputs):
   qp_random.json      seeded instances (N, C in {4,10,20} x {2,4}) with genuine-iSWIFT solutions
   nlp_random.json     seeded N=10 trot instances, K_obs = 3: KKT-certified NLP optimum (oracle),
                       with SciPy SLSQP's objective from the same warm start for comparison
+  ll_ctrl.npz         low-level CLF-QP (LowLevelCtrl::calcTorque) inputs for 8 agents with
+                      contact sets trot / stand / three legs / flight, and the genuine-iSWIFT
+                      solution of each agent's QP with and without the CLF row
+                      (numpy .npz, plain arrays, loads with allow_pickle=False)
 """
 import json
 import os
@@ -29,7 +33,7 @@ sys.path.insert(0, os.path.join(ROOT, "tests"))
 
 import oracle  # noqa: E402
 from kkt import certify, nlp_rows  # noqa: E402
-from srbnmpc import workload  # noqa: E402  (pure numpy generator; no GPU needed)
+from srbnmpc import workload, ll_workload  # noqa: E402  (pure numpy generators; no GPU needed)
 
 REF = "/root/reference"
 
@@ -177,8 +181,32 @@ def nlp_random():
     dump("nlp_random.json", dict(cases=cases))
 
 
+# ----------------------------------------------------------------------------- low-level CLF-QP
+LL_IND = [[1, 0, 0, 1], [0, 1, 1, 0], [1, 1, 1, 1], [1, 1, 1, 0], [0, 0, 0, 0], [1, 0, 0, 1], [0, 1, 1, 0], [1, 1, 1, 1]]
+
+
+def ll_ctrl():
+    b = ll_workload.make_batch(len(LL_IND), seed=77, ind=LL_IND)
+    out = {k: np.asarray(v) for k, v in b.items()}
+    for clf in (1, 0):
+        p = oracle.ll_params(useCLF=clf)
+        X = np.zeros((len(LL_IND), 32)); F = np.zeros(len(LL_IND), np.int32); IT = np.zeros(len(LL_IND), np.int32)
+        for a in range(len(LL_IND)):
+            Pd, c, A, bb, G, h, *_ = oracle.ll_build_qp(p, b, a)
+            x, f, it = oracle.iswift_ref(Pd, c, A, bb, G, h, "md")
+            X[a, :x.size] = x; F[a] = f; IT[a] = it
+            print("ll case", clf, a, LL_IND[a], f, it)
+        out[f"iswift_x_clf{clf}"] = X; out[f"iswift_flag_clf{clf}"] = F; out[f"iswift_iters_clf{clf}"] = IT
+    np.savez_compressed(os.path.join(HERE, "ll_ctrl.npz"), **out)
+    print("wrote ll_ctrl.npz")
+
+
 if __name__ == "__main__":
     oracle.build()
+    if sys.argv[1:] == ["ll"]:
+        ll_ctrl()
+        sys.exit(0)
+    ll_ctrl()
     kat1()
     kat2()
     qp_random()
