@@ -13,6 +13,12 @@ line.  Configs (BASELINE.json "configs"):
     3  1024 agents/GPU, N=10, 3 static + 8 nearest agents   -- configs[2]
     4  1024 agents/GPU, as 3 with the RCCL all-gather       -- configs[3] (8 GPUs = 8192)
     5  2048 agents/GPU, N=20, 3 static + 8 nearest agents   -- configs[4] shape, fp64
+
+    python bench.py --path ll [--agents A]
+
+The low-level CLF-QP (SURVEY.md 8(f) row 4, LowLevelCtrl::calcTorque): one step = QP
+assembly + iSWIFT solve + swing PD + integration for every agent (default 8192 per GPU,
+trot / stand mix), inputs resident in HBM; its own metric and roofline, not the headline.
 """
 import argparse
 import json
@@ -93,8 +99,115 @@ def cpu_baseline(cfg, b, budget_s):
                       f"{nthreads} threads"}
 
 
+LL_METRIC = "low-level CLF-QP controller solves/sec (LowLevelCtrl::calcTorque, batched)"
+LL_IN_DOUBLES = 18 + 18 + 324 + 216 + 18 + 216 + 12 + 216 + 216 + 216 + 12 + 12 + 324 + 18 * 5 + 12
+LL_OUT_DOUBLES = 18 + 12 + 18 * 3 + 2 + 32
+
+
+def ll_executed_flops(cnt, iters):
+    """fp64 flops of srb_ll_kernel per agent: assembly [Jc;H0] Dinv (2*18^3)
+    and (.)[Jc' B] (2*18*18*nft); per IPM iteration Y = H^-1 A' (~6*18*nft), S = A Y upper
+    triangle (171 * 2 nft), Gauss-Jordan 2*18^3, two Newton solves (A u, S^-1, Y dy:
+    2*(2*18*nft + 2*18^2 + 2*n*18 + 12 n)), residuals (A'y, A x: 4*18*nft + 12 n)."""
+    nft = 3 * cnt + 12
+    n = nft + 6 + 3 * (4 - cnt) + 1
+    asm = 2 * 18 ** 3 + 2 * 18 * 18 * nft
+    it = 6 * 18 * nft + 171 * 2 * nft + 2 * 18 ** 3 + 2 * (2 * 18 * nft + 2 * 18 * 18 + 2 * n * 18 + 12 * n) + \
+        4 * 18 * nft + 12 * n
+    return float(np.sum(asm + it * iters))
+
+
+def main_ll(args, world, rank, local_rank, dev):
+    from srbnmpc import ll_workload, lowlevel
+    A_local = args.agents or 8192
+    A_total = A_local * world
+    lo, hi = sdist.shard_range(A_total, world, rank)
+    n_loc = hi - lo
+    # a pool of 512 distinct synthetic agents tiled over the batch (generation is host Python)
+    pool = ll_workload.make_batch(min(512, A_total), seed=4321)
+    reps = -(-A_total // pool["ind"].shape[0])
+    full = {k: np.concatenate([v] * reps)[:A_total] for k, v in pool.items()}
+    d = {"ind": torch.as_tensor(np.ascontiguousarray(full["ind"][lo:hi], np.int32), device=dev)}
+    for k in lowlevel.IN_KEYS:
+        d[k] = torch.as_tensor(np.ascontiguousarray(full[k][lo:hi]).reshape(n_loc, -1), dtype=torch.float64, device=dev)
+    tau0 = torch.as_tensor(np.ascontiguousarray(full["tau"][lo:hi]), dtype=torch.float64, device=dev)
+    out = {k: torch.zeros((n_loc, s), dtype=torch.float64, device=dev) for k, s in lowlevel.OUT_SIZE.items()}
+    out["status"] = torch.zeros(n_loc, dtype=torch.int32, device=dev)
+    out["iters"] = torch.zeros(n_loc, dtype=torch.int32, device=dev)
+    ctrl = srbnmpc.LowLevelCtrl(lowlevel.default_params(), n_loc, local_rank)
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+
+    def step():
+        out["tau"].copy_(tau0)        # tau is in/out (LowLevelCtrl::tau), restore the input state
+        ctrl.calc_torque_device(d, out, stream=stream.cuda_stream)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    kern = []
+    for _ in range(3):
+        step()
+        kern.append(ctrl.last_kernel_ms())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_step = np.array([a.elapsed_time(bb) for a, bb in ev])
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    status = out["status"].cpu().numpy(); iters = out["iters"].cpu().numpy()
+    cnt = full["ind"][lo:hi].sum(1)
+    kms = float(np.median(kern))
+    flops = ll_executed_flops(cnt, iters)
+    achieved = flops / (kms * 1e-3) / 1e12
+    io = n_loc * (8 * (LL_IN_DOUBLES + 18 + LL_OUT_DOUBLES) + 16 + 8)
+    line = {
+        "metric": LL_METRIC, "value": A_total * args.steps / elapsed, "unit": "solves/s", "n_gpus": world,
+        "steps": args.steps, "warmup": args.warmup, "ms_per_step": elapsed * 1e3 / args.steps,
+        "higher_is_better": True, "scaling": "weak", "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"{A_local} agents/GPU, A1-sized LL QP (numDec <= 31), trot/stand mix, useCLF=1",
+                   "agents_per_gpu": A_local, "agents_total": A_total, "parallelism": f"agents sharded x{world}"},
+        "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
+        "optimal_frac": float((status == 0).mean()), "iters_mean": float(iters.mean()),
+        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "srb_ll_kernel",
+                     "kernel_ms": kms, "flop_model": "bench.ll_executed_flops (DESIGN.md 6b); latency-bound",
+                     "io_bytes_per_launch": io, "hbm_GBps": io / (kms * 1e-3) / 1e9},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        import oracle
+        p = oracle.ll_params()
+        sample = {k: v[:256] for k, v in full.items()}
+        t1 = time.perf_counter(); n = 0
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            oracle.ll_calc_torque(p, sample)
+            n += 256
+        dt = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
+                                "sample": f"{n} calcTorque calls (256-agent slices of the same batch) in {dt:.1f} s, "
+                                          f"oracle/ll_ctrl.c, 1 thread"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    ctrl.close()
+
+
 def main():
     ap = argparse.ArgumentParser()
+    ap.add_argument("--path", choices=["nmpc", "ll"], default="nmpc")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -113,6 +226,11 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
+    if args.path == "ll":
+        main_ll(args, world, rank, local_rank, dev)
+        if world > 1:
+            dist.destroy_process_group()
+        return
 
     cfg = dict(CONFIGS[args.config])
     A_local = args.agents or cfg["agents"]

@@ -157,6 +157,74 @@ int srb_lds_bytes(const srb_params *p);
  * host-side: alpha[4][5] from the buffer state buf[4] and X[0..3] (4 states). */
 void srb_fit_bezier(const double buf[4], const double *X, double alpha[20]);
 
+/*
+ * ---- Low-level CLF-QP controller ----------------------------------
+ * Replaces LowLevelCtrl::calcTorque(state, dyn, kin, vc, con, params)
+ * (/root/reference/include/LowLevelCtrl.hpp:20, src/LowLevelCtrl.cpp:18-113) for a batch of
+ * agents: QP assembly (cost :115-137, constraints :139-236), the iswiftQp_e solve (:33-37,
+ * iSWIFT Prime.c:127-230), the parse into ll.QP_force / tau / dV (:44-64), swing-leg PD
+ * (:71-91), the integration ll.ddq / ll.dq / ll.q (:96-98) and swingInvKin (:446-488).
+ * One QP per agent: numDec = 3c + 12 + outDim + useCLF (<= 31) variables
+ * [F (3c, stance legs FR,FL,RR,RL) | tau (12) | aux (outDim = 6 + 3(4-c)) | d].
+ */
+typedef struct srb_ll_params {      /* Settings::LL_params (global_loco_structs.hpp:96-111) */
+    double mu, kp, kd;
+    int useCLF;
+    double tauPen, dfPen, auxPen, clfPen, auxMax, clfEps;
+    int maxit;                      /* iSWIFT MAXIT 25 (GlobalOptions.h:23) */
+    double tol;                     /* 1e-6 (GlobalOptions.h:24-25) */
+} srb_ll_params;
+
+/* Parameters.cpp:62-75 defaults: mu 0.7, kp 700, kd 40, useCLF 1, tauPen 1, dfPen 0.1,
+ * auxPen 1e6, clfPen 1e8, auxMax 100, clfEps 0.8. */
+void srb_ll_params_default(srb_ll_params *p);
+
+/*
+ * One batch, agent-major.  Matrices are column-major (Eigen's storage) with FIXED leading
+ * dimensions, so every agent has the same stride whatever its contact count:
+ *   ind      [A][4] int      ConInf::ind (1 stance, 0 swing; other values -> status 3)
+ *   q, dq    [A][18]         StateInfo::q, dq
+ *   Dinv     [A][18*18]      DynamicsInfo::Dinv
+ *   B        [A][12*18]      DynamicsInfo::B (18 x 12, ld 18)
+ *   H        [A][18]         DynamicsInfo::H
+ *   Jc, Js   [A][18*12]      KinematicsInfo::Jc (3c x 18), Js ((12-3c) x 18), ld 12
+ *   dJc      [A][12]         KinematicsInfo::dJc (3c used)
+ *   Jtoe, Jhip [A][18*12]    KinematicsInfo::Jtoe, Jhip (12 x 18, ld 12)
+ *   toePos, hipPos [A][12]   KinematicsInfo::toePos, hipPos (3 x 4: column per leg)
+ *   H0       [A][18*18]      VCInfo::H0 (outDim x 18, ld 18)
+ *   dH0, y, dy [A][18]       VCInfo (outDim used)
+ *   hd, dhd  [A][18]         VCInfo::hd, dhd (rows 6.. hold the swing-toe targets)
+ *   fDes     [A][12]         VCInfo::fDes
+ * In/out:
+ *   tau      [A][18]         LowLevelCtrl::tau (the member array: entries 0..5 carry over
+ *                            between calls and accumulate the swing PD, :91)
+ * Outputs:
+ *   QP_force [A][12], ddq, dq_out, q_out [A][18]  LLInfo (global_loco_structs.hpp:74-80)
+ *   V, dV    [A]             LLInfo::V, dV
+ *   x        [A][32]         QP solution (optimOut), zero-padded beyond numDec; may be NULL
+ *   status   [A] int         iSWIFT exit code (0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 bad contact flags)
+ *   iters    [A] int         interior-point iterations
+ */
+typedef struct srb_ll_io {
+    const int *ind;
+    const double *q, *dq, *Dinv, *B, *H, *Jc, *dJc, *Js, *Jtoe, *Jhip, *toePos, *hipPos;
+    const double *H0, *dH0, *y, *dy, *hd, *dhd, *fDes;
+    double *tau, *QP_force, *ddq, *dq_out, *q_out, *V, *dV, *x;
+    int *status, *iters;
+} srb_ll_io;
+
+typedef struct srb_ll_ctx srb_ll_ctx;
+
+int srb_ll_ctx_create(const srb_ll_params *p, int max_agents, int device, srb_ll_ctx **out);
+int srb_ll_ctx_destroy(srb_ll_ctx *ctx);
+/* host buffers: copies in, solves, copies out, synchronises */
+int srb_ll_calc_torque(srb_ll_ctx *ctx, int n_agents, const srb_ll_io *host_io);
+/* device buffers, asynchronous on `stream` (NULL = the context's stream); call srb_ll_sync() */
+int srb_ll_calc_torque_device(srb_ll_ctx *ctx, int n_agents, const srb_ll_io *dev_io, void *stream);
+int srb_ll_sync(srb_ll_ctx *ctx);
+/* HIP-event time of the last srb_ll_calc_torque[_device] kernel on its stream (ms) */
+int srb_ll_last_kernel_ms(srb_ll_ctx *ctx, float *ms);
+
 const char *srb_last_error(void);
 
 #ifdef __cplusplus

@@ -56,6 +56,9 @@ static int fail(int code, const std::string &msg)
     return code;
 }
 
+// shared with srb_ll_capi.cpp
+int srb_internal_fail(int code, const char *msg) { return fail(code, msg); }
+
 #define HIPCHK(expr)                                                                   \
     do {                                                                               \
         hipError_t e_ = (expr);                                                        \

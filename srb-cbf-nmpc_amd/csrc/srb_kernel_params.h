@@ -45,3 +45,22 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
 #endif
         ;
 }
+
+// ---- low-level CLF-QP (srb_llctrl.hip; LowLevelCtrl::calcTorque, src/LowLevelCtrl.cpp:18-113)
+// Host fills it from srb_ll_params (srb_capi.cpp): the gains of Settings::LL_params plus the
+// constants of the CLF Lyapunov matrix (LowLevelCtrl.cpp:176-185) folded once per launch.
+struct SrbLLKParams {
+    double mus;                       // mu / sqrt(2)                         (:157)
+    double kp, kd;
+    double tauPen, dfPen, auxPen, clfPen;
+    double p1e2, pde, p2;             // P1/eps^2, Pd/eps, P2 of tuneMat*PP*tuneMat (:176-190)
+    double cce;                       // c / eps with c = 1 / lambda_max(PP0)  (:184-185, :233)
+    double tol;
+    int useCLF, maxit;
+    int dbg_agent;                    // >= 0: that agent records a per-iteration trace (srb_ll_debug_trace)
+};
+
+// device layout of one agent (srb_ll_io, include/srbnmpc.h): column-major matrices with fixed
+// leading dimensions
+#define SRB_LL_NQ 18   // TOTAL_DOF (global_loco_opts.h:24)
+#define SRB_LL_NU 12   // TOTAL_IN  (global_loco_opts.h:25)

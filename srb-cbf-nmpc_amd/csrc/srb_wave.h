@@ -1,0 +1,171 @@
+// Wavefront helpers shared by the gfx950 kernels of this library (NMPC solve, low-level
+// CLF-QP): DPP/permlane reductions, readlane broadcasts, a refined reciprocal and the
+// register Gauss-Jordan inverse.  Header-only, device code.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#ifndef WAVE
+#define WAVE 64
+#endif
+
+typedef double d4 __attribute__((ext_vector_type(4)));
+
+// --------------------------------------------------------------------------- wave helpers
+// Cross-lane traffic stays in the VALU: DPP row permutations for the 16-lane rows and
+// gfx950's v_permlane16/32_swap across rows.  Every lane ends with the bit-identical
+// result (each stage combines a pair with a commutative op), so branches on it are uniform.
+template <int CTRL>
+__device__ __forceinline__ double dpp_d(double v)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_update_dpp(0, (int)b, CTRL, 0xf, 0xf, false);
+    const int hi = __builtin_amdgcn_update_dpp(0, (int)(b >> 32), CTRL, 0xf, 0xf, false);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// the two halves of a permlane swap of v with itself: {v, partner} in some order
+template <int W>
+__device__ __forceinline__ void swap_d(double v, double &a, double &b)
+{
+    const unsigned long long u = (unsigned long long)__double_as_longlong(v);
+    const unsigned lo = (unsigned)u, hi = (unsigned)(u >> 32);
+    auto l = (W == 16) ? __builtin_amdgcn_permlane16_swap(lo, lo, false, false) : __builtin_amdgcn_permlane32_swap(lo, lo, false, false);
+    auto h = (W == 16) ? __builtin_amdgcn_permlane16_swap(hi, hi, false, false) : __builtin_amdgcn_permlane32_swap(hi, hi, false, false);
+    a = __longlong_as_double((long long)(((unsigned long long)h[0] << 32) | l[0]));
+    b = __longlong_as_double((long long)(((unsigned long long)h[1] << 32) | l[1]));
+}
+#define SRB_WAVE_REDUCE(NAME, OP)                                                  \
+    __device__ __forceinline__ double NAME(double v)                               \
+    {                                                                              \
+        v = OP(v, dpp_d<0xB1>(v));   /* quad_perm [1,0,3,2] */                     \
+        v = OP(v, dpp_d<0x4E>(v));   /* quad_perm [2,3,0,1] */                     \
+        v = OP(v, dpp_d<0x141>(v));  /* row_half_mirror     */                     \
+        v = OP(v, dpp_d<0x140>(v));  /* row_mirror          */                     \
+        double a, b;                                                               \
+        swap_d<16>(v, a, b); v = OP(a, b);                                         \
+        swap_d<32>(v, a, b); return OP(a, b);                                      \
+    }
+__device__ __forceinline__ double op_add(double a, double b) { return a + b; }
+SRB_WAVE_REDUCE(wsum, op_add)
+SRB_WAVE_REDUCE(wmin, fmin)
+SRB_WAVE_REDUCE(wmax, fmax)
+// NV independent wave reductions interleaved stage by stage (one DPP/permlane latency per
+// stage for all of them); bit i of MX selects max (1) or sum (0) for v[i].
+template <int NV, unsigned MX>
+__device__ __forceinline__ void wred(double (&v)[NV])
+{
+#define SRB_RED_STAGE(GET)                                                                      \
+    _Pragma("unroll") for (int i = 0; i < NV; i++) {                                            \
+        const double t_ = GET;                                                                  \
+        v[i] = ((MX >> i) & 1u) ? fmax(v[i], t_) : v[i] + t_;                                   \
+    }
+    SRB_RED_STAGE(dpp_d<0xB1>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x4E>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x141>(v[i]))
+    SRB_RED_STAGE(dpp_d<0x140>(v[i]))
+#undef SRB_RED_STAGE
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        double a, b;
+        swap_d<16>(v[i], a, b);
+        v[i] = ((MX >> i) & 1u) ? fmax(a, b) : a + b;
+    }
+#pragma unroll
+    for (int i = 0; i < NV; i++) {
+        double a, b;
+        swap_d<32>(v[i], a, b);
+        v[i] = ((MX >> i) & 1u) ? fmax(a, b) : a + b;
+    }
+}
+// wred over all NW waves of the workgroup: per-wave DPP reduction, then lane 0 of every wave
+// publishes to `scr` (NW x NV doubles, one scratch block per call site) and every thread
+// combines the NW partials in the same order (identical results on every lane and wave).
+template <int NV, unsigned MX, int NW>
+__device__ __forceinline__ void wred_x(double (&v)[NV], double *scr, int tid)
+{
+    wred<NV, MX>(v);
+    if constexpr (NW > 1) {
+        if ((tid & 63) == 0)
+#pragma unroll
+            for (int i = 0; i < NV; i++) scr[(tid >> 6) * NV + i] = v[i];
+        __syncthreads();
+#pragma unroll
+        for (int i = 0; i < NV; i++) {
+            double r = scr[i];
+#pragma unroll
+            for (int w = 1; w < NW; w++) r = ((MX >> i) & 1u) ? fmax(r, scr[w * NV + i]) : r + scr[w * NV + i];
+            v[i] = r;
+        }
+    }
+}
+// sum over the lanes that share (lane mod W), W = 16 or 32: permlane butterflies only
+__device__ __forceinline__ double chunk_sum16(double v)
+{
+    double a, b;
+    swap_d<32>(v, a, b); v = a + b;
+    swap_d<16>(v, a, b); return a + b;
+}
+__device__ __forceinline__ double chunk_sum32(double v)
+{
+    double a, b;
+    swap_d<32>(v, a, b); return a + b;
+}
+// value of lane `lane` (wave-uniform index) -> wave-uniform value
+__device__ __forceinline__ double readlane_d(double v, int lane)
+{
+    const long long b = __double_as_longlong(v);
+    const int lo = __builtin_amdgcn_readlane((int)b, lane);
+    const int hi = __builtin_amdgcn_readlane((int)(b >> 32), lane);
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+
+// 1/x from the hardware estimate (v_rcp_f64) refined by two Newton steps: within an ulp
+// or two of the IEEE quotient, a handful of FMAs instead of the division sequence.
+__device__ __forceinline__ double rcp_d(double x)
+{
+    double r = __builtin_amdgcn_rcp(x);
+    r = fma(r, fma(-x, r, 1.0), r);
+    r = fma(r, fma(-x, r, 1.0), r);
+    return r;
+}
+__device__ __forceinline__ int rnd4(int x) { return (x + 3) & ~3; }
+
+// --------------------------------------------------------------------------- Gauss-Jordan
+// In-place inverse of the nz x nz SPD matrix held one row per lane (lane i: A[0..NZL)),
+// rows/columns >= nz padded with the identity.  Step k broadcasts the pivot row by
+// v_readlane and every other lane eliminates column k from its row; the pivot row itself is
+// not scaled (each lane keeps 1 / its own pivot and scales its row once at the end), so a
+// step is one multiplier and one FMA per entry.  The pivots are those of LDL' in natural
+// order, so pivot <= 0 <=> not positive definite; regularise != 0 applies iSWIFT's dynamic
+// pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7).  Returns 0 on success.
+template <int NZL>
+__device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
+{
+    // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
+    // elimination is one basic block: the scheduler overlaps step k's row updates with the
+    // broadcast of row k+1, whose entries are updated first.
+    int fail = 0;
+    double cs = 1.0;
+#pragma unroll
+    for (int k = 0; k < NZL; k++) {
+        double piv = readlane_d(A[k], k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        fail |= !(piv > 0.0);
+        const double inv = rcp_d(piv);
+        double rk[NZL];
+#pragma unroll
+        for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
+        const bool me = lane == k;
+        const double f = me ? 0.0 : A[k] * inv;
+#pragma unroll
+        for (int jj = 0; jj < NZL; jj++) {
+            const int j = (k + 1 + jj) % NZL;           // next pivot row's entries first
+            if (j != k) A[j] = fma(-f, rk[j], A[j]);
+        }
+        A[k] = me ? 1.0 : -f;
+        cs = me ? inv : cs;
+    }
+#pragma unroll
+    for (int j = 0; j < NZL; j++) A[j] *= cs;
+    return fail;
+}
+

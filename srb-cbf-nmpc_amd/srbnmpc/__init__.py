@@ -8,6 +8,8 @@ constructing a solver raises.
     MPCDist       -- per-agent object with the reference's MPC_dist call surface
                      (/root/reference/include/MPC_dist.hpp:137-190)
     workload      -- synthetic agent batches with the SURVEY.md §8d distributions
+    LowLevelCtrl  -- batched low-level CLF-QP (LowLevelCtrl::calcTorque), srbnmpc.lowlevel
+    ll_workload   -- synthetic A1-sized low-level controller inputs
 """
 from __future__ import annotations
 
@@ -244,3 +246,5 @@ def split(params: Params, x):
 
 from .mpc_dist import MPCDist  # noqa: E402
 from . import workload  # noqa: E402
+from . import ll_workload  # noqa: E402
+from .lowlevel import LowLevelCtrl  # noqa: E402
