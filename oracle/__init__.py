@@ -124,6 +124,19 @@ def qp_solve(Pd, c, A, b, G, h, maxit=25, tol=1e-6):
     return x, f, it.value, q
 
 
+def qp_solve_variants(Pd, c, A, b, G, h, maxit=25, tol=1e-6):
+    """iSWIFT semantics (with the trapped flag of its sigma <= sigma_d branch) and the kernel's
+    no-trap variant: ((x, flag, iters, trapped), (x, flag, iters))."""
+    n = Pd.size; m = h.size; pp = b.size
+    arrs = [_c(a) for a in (Pd, c, A, b, G, h)]
+    x1 = np.zeros(n); x2 = np.zeros(n); i1 = ctypes.c_int(); i2 = ctypes.c_int(); tr = ctypes.c_int()
+    f1 = lib().orc_qp_solve_trap(n, m, pp, *[_ptr(a) for a in arrs], maxit, ctypes.c_double(tol), _ptr(x1),
+                                 ctypes.byref(i1), ctypes.byref(tr))
+    f2 = lib().orc_qp_solve_nt(n, m, pp, *[_ptr(a) for a in arrs], maxit, ctypes.c_double(tol), _ptr(x2),
+                               ctypes.byref(i2))
+    return (x1, f1, i1.value, tr.value), (x2, f2, i2.value)
+
+
 def qp_solve_full(P, c, A, b, G, h, maxit=25, tol=1e-6):
     """iSWIFT restatement with a general symmetric P (KAT-1, Matrices_small.h)."""
     n = P.shape[0]; m = G.shape[0]; pp = A.shape[0]
@@ -238,7 +251,7 @@ class OrcLLParams(ctypes.Structure):
     _fields_ = [("mu", ctypes.c_double), ("kp", ctypes.c_double), ("kd", ctypes.c_double), ("useCLF", ctypes.c_int),
                 ("tauPen", ctypes.c_double), ("dfPen", ctypes.c_double), ("auxPen", ctypes.c_double),
                 ("clfPen", ctypes.c_double), ("auxMax", ctypes.c_double), ("clfEps", ctypes.c_double),
-                ("maxit", ctypes.c_int), ("tol", ctypes.c_double)]
+                ("maxit", ctypes.c_int), ("tol", ctypes.c_double), ("iswift_trap", ctypes.c_int)]
 
 
 class OrcLLAgent(ctypes.Structure):

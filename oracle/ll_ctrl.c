@@ -38,6 +38,7 @@ void orc_ll_params_default(orc_ll_params *p)
     p->tauPen = 1e0; p->dfPen = 1e-1; p->auxPen = 1e6; p->clfPen = 1e8;
     p->auxMax = 100; p->clfEps = 0.8;
     p->maxit = 25; p->tol = 1e-6;             /* GlobalOptions.h:23-25 */
+    p->iswift_trap = 0;
 }
 
 /* C (r x k, ldc r) = A (r x n, lda) * B (n x k, ldb), column-major */
@@ -184,7 +185,9 @@ int orc_ll_calc_torque(const orc_ll_params *prm, const orc_ll_agent *in, orc_ll_
     double Pd[32], c[32], A[18 * 32], b[18], G[45 * 32], h[45], clf[3], LgV[NQ], x[32];
     int n, p, m, it = 0;
     orc_ll_build_qp(prm, in, &n, &p, &m, Pd, c, A, b, G, h, clf, LgV);
-    const int flag = orc_qp_solve(n, m, p, Pd, c, A, b, G, h, prm->maxit, prm->tol, x, NULL, &it);
+    /* the kernel's solve: iSWIFT minus the rounding-only sigma <= sigma_d branch (qp_ipm.c) */
+    const int flag = prm->iswift_trap ? orc_qp_solve(n, m, p, Pd, c, A, b, G, h, prm->maxit, prm->tol, x, NULL, &it)
+                                      : orc_qp_solve_nt(n, m, p, Pd, c, A, b, G, h, prm->maxit, prm->tol, x, &it);
     out->status = flag; out->iters = it;
     for (int i = 0; i < 32; i++) out->x[i] = (i < n) ? x[i] : 0.0;
 

@@ -110,6 +110,14 @@ void orc_fit_bezier(const double buf[4], const double *X, double alpha[20]);
  * column-major 2NA x (loop / 40). */
 void orc_hl_plan(int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr, double *Prd);
 
+/* iSWIFT without the rounding-only sigma <= sigma_d branch (see qp_ipm.c), and iSWIFT
+ * semantics reporting whether that branch was taken */
+int orc_qp_solve_nt(int n, int m, int p, const double *Pd, const double *c, const double *A, const double *b,
+                    const double *G, const double *h, int maxit, double tol, double *x_out, int *iters_out);
+int orc_qp_solve_trap(int n, int m, int p, const double *Pd, const double *c, const double *A, const double *b,
+                      const double *G, const double *h, int maxit, double tol, double *x_out, int *iters_out,
+                      int *trapped);
+
 /* ---- low-level CLF-QP controller (ll_ctrl.c; LowLevelCtrl::calcTorque, LowLevelCtrl.cpp:18-113) */
 typedef struct orc_ll_params {
     double mu, kp, kd;                  /* Settings::LL_params (global_loco_structs.hpp:96-111) */
@@ -117,6 +125,7 @@ typedef struct orc_ll_params {
     double tauPen, dfPen, auxPen, clfPen, auxMax, clfEps;
     int maxit;                          /* iSWIFT MAXIT 25, tolerance 1e-6 (GlobalOptions.h:23-25) */
     double tol;
+    int iswift_trap;                    /* 1: keep iSWIFT's sigma <= sigma_d branch (default 0, as the kernel) */
 } orc_ll_params;
 
 /* one agent's inputs; column-major matrices with the leading dimensions of srb_ll_io */

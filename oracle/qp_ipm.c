@@ -137,7 +137,8 @@ static double steplen(const double *v, const double *dv, int m)
 
 static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf, const double *c,
                          const double *A, const double *b, const double *G, const double *h,
-                         int maxit, double tol, double *x_out, double *q_out, int *iters_out)
+                         int maxit, double tol, double *x_out, double *q_out, int *iters_out, int no_trap,
+                         int *trapped)
 {
     kktws w;
     ws_init(&w, n, m, p, Pd, A, G);
@@ -194,7 +195,7 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
         }
         for (int r = 0; r < m; r++) lam[r] = sqrt(s[r] * z[r]);
         double mu = dot(lam, lam, m) / m;
-        if (sigma > sigma_d) {
+        if (sigma > sigma_d || no_trap) {
             /* updatekktmatrix(indicator 0) + ldl_numeric inside kktsolve_1 (Prime.c:165-177) */
             for (int r = 0; r < m; r++) wgt[r] = s[r] / z[r];
             if (kkt_factor(&w, wgt)) { flag = 1; break; }
@@ -211,6 +212,7 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
         } else {
             /* Prime.c:193-196: no refactorisation -- kktsolve_2 reuses the previous factor */
             sigma = sigma_d;
+            if (trapped) *trapped = 1;
             for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) + sigma * mu;
         }
         for (int r = 0; r < m; r++) r3[r] = rz[r] - ds[r] / z[r];
@@ -241,7 +243,28 @@ int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
                  const double *A, const double *b, const double *G, const double *h,
                  int maxit, double tol, double *x_out, double *q_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL);
+}
+
+/* iSWIFT with the sigma <= sigma_d branch (Prime.c:193-196) disabled.  The step-length rule keeps
+ * both factors of every product in rho non-negative, so rho <= 0 (sigma = 0) arises only from
+ * rounding at a blocking row; iSWIFT then freezes the KKT factor for the rest of the solve and
+ * usually ends at MAXIT.  The low-level controller's kernel keeps the predictor-corrector path
+ * instead; this is its oracle. */
+int orc_qp_solve_nt(int n, int m, int p, const double *Pd, const double *c,
+                    const double *A, const double *b, const double *G, const double *h,
+                    int maxit, double tol, double *x_out, int *iters_out)
+{
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 1, NULL);
+}
+
+/* iSWIFT semantics, reporting whether the sigma <= sigma_d branch was taken */
+int orc_qp_solve_trap(int n, int m, int p, const double *Pd, const double *c,
+                      const double *A, const double *b, const double *G, const double *h,
+                      int maxit, double tol, double *x_out, int *iters_out, int *trapped)
+{
+    *trapped = 0;
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, trapped);
 }
 
 /* general (full, symmetric) P -- used for iSWIFT's own test QP (Matrices_small.h) */
@@ -249,5 +272,5 @@ int orc_qp_solve_full(int n, int m, int p, const double *P, const double *c,
                       const double *A, const double *b, const double *G, const double *h,
                       int maxit, double tol, double *x_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out);
+    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, NULL);
 }

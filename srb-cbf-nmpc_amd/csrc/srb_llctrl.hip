@@ -75,6 +75,8 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     const int agent = blockIdx.x;
     if (agent >= n_agents) return;
     const int lane = threadIdx.x;
+    // diagnostics: prm.dbg_agent = agent | (iteration of the state dump << 16), or -1
+    const int dag = prm.dbg_agent < 0 ? -1 : (prm.dbg_agent & 0xffff), dit = prm.dbg_agent < 0 ? -1 : (prm.dbg_agent >> 16);
 
     // ------------------------------------------------------------------ contact pattern (uniform)
     int ind[4], cnt = 0, bad = 0;
@@ -436,7 +438,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
         flag = 2;
         SYNC();
 
-        double sigma = 100.0, omf = 0.0;                     // options->sigma = SIGMA (GlobalOptions.h:26)
+        double omf = 0.0;
         const double th = prm.tol / sqrt(3.0);
         const double invm = 1.0 / (double)m;
         for (int iter = 0; iter < prm.maxit; iter++) {
@@ -450,7 +452,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             const double ry = ise ? bk - arow(sh.vx) : 0.0;
             const double rz = isr ? hr - s - grow(sh.vx) : 0.0;
             const double lam = isr ? sqrt(s * z) : 0.0;
-            const bool dbs = agent == prm.dbg_agent && iter == 7;   // state dump at iteration 7
+            const bool dbs = agent == dag && iter == dit;   // state dump at iteration dit
             if (dbs) {
                 if (isv) srb_ll_dbg[256 + lane] = xj;
                 if (ise) srb_ll_dbg[288 + lane] = yk;
@@ -460,34 +462,33 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             wred<5, 0u>(nr);
             if (sqrt(nr[0]) < th && sqrt(nr[2]) < th && sqrt(nr[1]) < th && nr[3] * invm < prm.tol) { flag = 0; break; }
             const double mu = nr[4] * invm;
-            const bool dbg = agent == prm.dbg_agent && lane == 0 && iter < 32;
+            const bool dbg = agent == dag && lane == 0 && iter < 32;
             if (dbg) { for (int q = 0; q < 5; q++) srb_ll_dbg[8 * iter + q] = nr[q]; }
             double ds, dx, dy, dz, dsv, st[2], alp, ald;
-            if (sigma > 0.0) {
-                // updatekktmatrix + kktsolve_1 (Prime.c:165-192): refactor at the current weights
-                omf = isr ? sh.vt[lane] : 0.0;
-                if (factor(sh.sc[1])) { flag = 1; break; }
-                // predictor
-                ds = -lam * lam;
-                kkt_solve(rx, ry, isr ? rz - ds / z : 0.0, omf, dx, dy, dz);
-                dsv = isr ? (ds - s * dz) / z : 0.0;
-                st[0] = (isr && dsv < 0) ? s / dsv : -1e300;   // max(v/dv) = -min(-v/dv) (findsteplength)
-                st[1] = (isr && dz < 0) ? z / dz : -1e300;
-                wred<2, 3u>(st);
-                alp = (-st[0] < 1e10) ? -st[0] : 1.0;
-                ald = (-st[1] < 1e10) ? -st[1] : 1.0;
+            // updatekktmatrix + kktsolve_1 (Prime.c:165-192): refactor at the current weights.
+            // iSWIFT's sigma <= sigma_d branch (Prime.c:193-196: the factor is frozen for the rest
+            // of the solve) is not taken: the step-length rule keeps every factor of rho's products
+            // >= 0, so sigma = 0 arises only from rounding at a blocking row
+            omf = isr ? sh.vt[lane] : 0.0;
+            if (factor(sh.sc[1])) { flag = 1; break; }
+            // predictor
+            ds = -lam * lam;
+            kkt_solve(rx, ry, isr ? rz - ds / z : 0.0, omf, dx, dy, dz);
+            dsv = isr ? (ds - s * dz) / z : 0.0;
+            st[0] = (isr && dsv < 0) ? s / dsv : -1e300;   // max(v/dv) = -min(-v/dv) (findsteplength)
+            st[1] = (isr && dz < 0) ? z / dz : -1e300;
+            wred<2, 3u>(st);
+            alp = (-st[0] < 1e10) ? -st[0] : 1.0;
+            ald = (-st[1] < 1e10) ? -st[1] : 1.0;
+            {
                 double num = isr ? (s + alp * dsv) * (z + ald * dz) : 0.0, d1 = 0.0;
                 wsum2(num, d1);
                 const double rho = num / nr[3];
                 const double mr = rho < 1 ? rho : 1;
-                sigma = mr * mr * mr;
+                double sigma = mr * mr * mr;
                 if (sigma < 0.0) sigma = 0.0;                   // sigma_d = 0 (iswift_qp.cpp:103)
                 ds = -(lam * lam) - (dsv * dz) + sigma * mu;
                 if (dbg) { srb_ll_dbg[8 * iter + 5] = alp; srb_ll_dbg[8 * iter + 6] = ald; srb_ll_dbg[8 * iter + 7] = sigma; }
-            } else {
-                // Prime.c:193-196: sigma = sigma_d, no refactorisation (previous factor and weights)
-                sigma = 0.0;
-                ds = -(lam * lam) + sigma * mu;
             }
             // corrector (kktsolve_2)
             kkt_solve(rx, ry, isr ? rz - ds / z : 0.0, omf, dx, dy, dz);

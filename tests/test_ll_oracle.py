@@ -146,3 +146,24 @@ def test_ll_oracle_vs_genuine_iswift_random():
         x, f, it = oracle.iswift_ref(Pd, c, A, bb, G, h, "md")
         assert f == o["status"][a] and it == o["iters"][a]
         assert np.abs(x - o["x"][a, :x.size]).max() < 1e-8
+
+
+def test_ll_no_trap_variant_differs_from_iswift_only_when_it_traps():
+    """The kernel (and the default LL oracle) drop iSWIFT's sigma <= sigma_d branch
+    (Prime.c:193-196), reachable only through rounding.  On every instance where the
+    iSWIFT-semantics run does not take that branch, both give the identical iterates."""
+    rng = np.random.default_rng(5)
+    ind = rng.integers(0, 2, (64, 4)).astype(np.int32)
+    b = ll_workload.make_batch(64, seed=9, ind=ind)
+    n_trap = 0
+    for clf in (1, 0):
+        p = oracle.ll_params(useCLF=clf)
+        for a in range(64):
+            Pd, c, A, bb, G, h, *_ = oracle.ll_build_qp(p, b, a)
+            (x1, f1, i1, tr), (x2, f2, i2) = oracle.qp_solve_variants(Pd, c, A, bb, G, h)
+            n_trap += tr
+            if not tr:
+                assert f1 == f2 and i1 == i2 and np.array_equal(x1, x2)
+            else:
+                assert f2 == 0 and np.abs(x1 - x2).max() < 1e-6
+    assert n_trap <= 8

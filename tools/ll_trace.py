@@ -1,5 +1,8 @@
 """Diagnostic: trace one agent's low-level CLF-QP interior-point iterations on the GPU
-(srb_ll_debug_trace) next to status / iterations / x error of every agent vs the oracle."""
+(srb_ll_debug_trace) next to status / iterations / x error of every agent vs the oracle.
+
+    python tools/ll_trace.py CASE AGENT CLF      CASE = golden | rand:SEED | trot:SEED
+Writes gpurun_out/ll_trace.npz (trace buffer + the case's inputs for offline replay)."""
 import ctypes
 import os
 import sys
@@ -10,45 +13,43 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "srb-cbf-nmpc_amd")]
 import oracle  # noqa: E402
 import srbnmpc  # noqa: E402
-from srbnmpc import lowlevel  # noqa: E402
+from srbnmpc import ll_workload, lowlevel  # noqa: E402
 
-agent = int(sys.argv[1]) if len(sys.argv) > 1 else 2
-clf = int(sys.argv[2]) if len(sys.argv) > 2 else 1
-g = np.load(os.path.join(ROOT, "tests", "golden", "ll_ctrl.npz"), allow_pickle=False)
-g = {k: g[k] for k in g.files}
+
+def make_case(case):
+    if case == "golden":
+        g = np.load(os.path.join(ROOT, "tests", "golden", "ll_ctrl.npz"), allow_pickle=False)
+        return {k: g[k] for k in g.files}
+    kind, seed = case.split(":")
+    seed = int(seed)
+    if kind == "rand":        # tests/test_ll_gpu.py::test_ll_gpu_matches_oracle_random_contacts
+        rng = np.random.default_rng(1000 + seed)
+        ind = rng.integers(0, 2, (96, 4)).astype(np.int32)
+        ind[:6] = [[0, 0, 0, 0], [1, 1, 1, 1], [1, 0, 0, 0], [0, 1, 1, 1], [1, 0, 0, 1], [0, 1, 1, 0]]
+        return ll_workload.make_batch(96, seed=200 + seed, ind=ind)
+    return ll_workload.make_batch(256, seed=seed)
+
+
+case = sys.argv[1] if len(sys.argv) > 1 else "golden"
+agent = int(sys.argv[2]) if len(sys.argv) > 2 else 0
+dump_it = int(sys.argv[4]) if len(sys.argv) > 4 else 7
+clf = int(sys.argv[3]) if len(sys.argv) > 3 else 1
+g = make_case(case)
 L = srbnmpc.lib()
 L.srb_ll_debug_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-L.srb_ll_debug_trace(agent, None)
-c = srbnmpc.LowLevelCtrl(lowlevel.default_params(useCLF=clf), 64)
+L.srb_ll_debug_trace(agent | (dump_it << 16), None)
+c = srbnmpc.LowLevelCtrl(lowlevel.default_params(useCLF=clf), 512)
 out = c.calc_torque(g)
 tr = np.zeros(512)
 L.srb_ll_debug_trace(-1, tr.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
 o = oracle.ll_calc_torque(oracle.ll_params(useCLF=clf), g)
-print("status gpu", out["status"].tolist(), "oracle", o["status"].tolist())
-print("iters  gpu", out["iters"].tolist(), "oracle", o["iters"].tolist())
-print("xerr", np.abs(out["x"] - o["x"]).max(axis=1).tolist())
-for k in ("tau", "QP_force", "ddq", "dq", "q", "V", "dV"):
-    print(k, float(np.abs(out[k] - o[k]).max()))
+bad = np.nonzero((out["status"] != o["status"]) | (out["iters"] != o["iters"]))[0]
+print("mismatching agents", [(int(a), int(out["status"][a]), int(o["status"][a]), int(out["iters"][a]),
+                              int(o["iters"][a])) for a in bad])
+print("max xerr", float(np.abs(out["x"] - o["x"]).max()))
 tr8 = tr[:256].reshape(32, 8)
-for i in range(min(26, 32)):
+for i in range(26):
     r = tr8[i]
     print(i, " ".join("%.3e" % v for v in [np.sqrt(r[0]), np.sqrt(r[1]), np.sqrt(r[2]), r[3], r[4], r[5], r[6], r[7]]))
-p = oracle.ll_params(useCLF=clf)
-for a in range(out["x"].shape[0]):
-    Pd, cc, A, b, G, h, *_ = oracle.ll_build_qp(p, g, a)
-    n = Pd.size
-    x = out["x"][a, :n]
-    xo = o["x"][a, :n]
-    print(a, "n", n, "|Ax-b| %.2e  max(Gx-h) %.2e  obj %.6f  oracle: |Ax-b| %.2e max(Gx-h) %.2e obj %.6f" % (
-        np.abs(A @ x - b).max(), (G @ x - h).max(), 0.5 * x @ (Pd * x) + cc @ x,
-        np.abs(A @ xo - b).max(), (G @ xo - h).max(), 0.5 * xo @ (Pd * xo) + cc @ xo))
-    if out["status"][a] != o["status"][a]:
-        print("   gpu x", np.round(x, 4).tolist())
-        print("   orc x", np.round(xo, 4).tolist())
-
-np.save(os.path.join(ROOT, "gpurun_out", "ll_trace_init.npy"), tr[200:250])
-print("init x", np.round(tr[200:231], 5).tolist())
-print("init y", np.round(tr[232:250], 5).tolist())
-np.save(os.path.join(ROOT, "gpurun_out", "ll_trace_rx0.npy"), tr[300:331])
-print("rx0", np.round(tr[300:331], 4).tolist())
-np.save(os.path.join(ROOT, "gpurun_out", "ll_trace_all.npy"), tr)
+os.makedirs(os.path.join(ROOT, "gpurun_out"), exist_ok=True)
+np.savez(os.path.join(ROOT, "gpurun_out", "ll_trace.npz"), tr=tr, gx=out["x"], **{"in_" + k: v for k, v in g.items()})
