@@ -68,8 +68,19 @@ __device__ __forceinline__ void wsum2(double &a, double &b)
 // diagnostic trace of one agent (prm.dbg_agent): per iteration the four residual sums, mu,
 // both predictor steps, sigma (8 doubles), read back by srb_ll_debug_trace
 __device__ double srb_ll_dbg[512];
+__device__ unsigned long long srb_ll_stamp[16];   // s_memtime cycles per phase of the traced agent
+#define LLST(slot)                                                                                   \
+    do {                                                                                             \
+        if (dstamp) {                                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+            __builtin_amdgcn_sched_barrier(0);                                                       \
+            if (lane == 0) srb_ll_stamp[slot] += t_ - tprev;                                         \
+            tprev = t_;                                                                              \
+        }                                                                                            \
+    } while (0)
 
-extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm, int n_agents, SrbLLDev io)
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) srb_ll_kernel(SrbLLKParams prm, int n_agents, SrbLLDev io)
 {
     __shared__ LLShared sh;
     const int agent = blockIdx.x;
@@ -77,6 +88,8 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     const int lane = threadIdx.x;
     // diagnostics: prm.dbg_agent = agent | (iteration of the state dump << 16), or -1
     const int dag = prm.dbg_agent < 0 ? -1 : (prm.dbg_agent & 0xffff), dit = prm.dbg_agent < 0 ? -1 : (prm.dbg_agent >> 16);
+    const bool dstamp = agent == dag;
+    unsigned long long tprev = dstamp ? __builtin_amdgcn_s_memtime() : 0ull;
 
     // ------------------------------------------------------------------ contact pattern (uniform)
     int ind[4], cnt = 0, bad = 0;
@@ -135,15 +148,15 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     }
     SYNC();
     // A = M K (18 x nft); b = M Hv - dJc | (-kp y - kd dy) + M Hv - dH0 (:147-152)
-    for (int e = lane; e < NQ * nft; e += 64) {
-        const int k = e / nft, v = e - k * nft;
+    for (int e = lane; e < NQ * 24; e += 64) {     // columns nft..23 are zero padding
+        const int k = e / 24, v = e - k * 24;
         double s0 = 0, s1 = 0;
 #pragma unroll
         for (int t = 0; t < NQ; t += 2) {
             s0 = fma(sh.u.as.M[k * LDJ + t], sh.u.as.K[v * NQ + t], s0);
             s1 = fma(sh.u.as.M[k * LDJ + t + 1], sh.u.as.K[v * NQ + t + 1], s1);
         }
-        sh.A[k * LDA + v] = s0 + s1;
+        sh.A[k * LDA + v] = (v < nft) ? s0 + s1 : 0.0;
     }
     double bk = 0.0;
     if (lane < NQ) {
@@ -162,6 +175,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
         }
     }
 
+    LLST(0);   // load + assembly
     // CLF scalars in closed form (PP = tuneMat PP0 tuneMat, eta = [y; dy], :171-235):
     //   V = eta'PP eta, LfV = eta'(FF'PP + PP FF)eta, LgV_i = 2 (Pd/e y_i + P2 dy_i)
     double Vv = 0.0, LfV = 0.0, Lgi = 0.0;
@@ -175,6 +189,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     wsum2(Vv, LfV);
     const double Veps = prm.cce * Vv;
     // u = [LgV; -1], v = u ./ diag(auxPen.., clfPen): fixed for the whole solve
+    if (lane < 32) { sh.Lg[lane] = 0.0; sh.vv[lane] = 0.0; }
     if (lane < out) { sh.Lg[lane] = Lgi; sh.vv[lane] = Lgi / prm.auxPen; }
     if (lane == out) { sh.Lg[lane] = useCLF ? -1.0 : 0.0; sh.vv[lane] = useCLF ? -1.0 / prm.clfPen : 0.0; }
     double uv = (useCLF && lane < out) ? Lgi * (Lgi / prm.auxPen) : 0.0;
@@ -217,7 +232,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     }
     if (isv && vtype >= 2) { gti[0] = rclf; gtc[0] = (vtype == 2) ? sh.Lg[lane - a0] : -1.0; }
     // aux / defect lane: D_j, v_j
-    const double Dj = (vtype == 2) ? prm.auxPen : prm.clfPen;
+    const double Dj = (vtype == 2) ? prm.auxPen : prm.clfPen, iDj = 1.0 / Dj;
     const double vj = (isv && vtype >= 2) ? sh.vv[lane - a0] : 0.0;
 
     // inequality lane r < m: three-term row (friction, torque bounds) or the CLF row
@@ -243,13 +258,23 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     if (isclf) hr = -LfV - Veps;                             // (:233)
     // equality lane k < 18
     const bool ise = lane < NQ;
+    // upper-triangle entries e = lane + 64 t of S -> (j << 8 | k), row-major
+    int sjk[3] = {0, 0, 0};
+#pragma unroll
+    for (int t = 0; t < 3; t++) {
+        int j = 0, rem = lane + 64 * t;
+        for (int q = 0; q < NQ; q++)
+            if (rem >= NQ - j) { rem -= NQ - j; j++; }
+        sjk[t] = (j << 8) | (j + rem);
+    }
 
     // G x for the inequality lanes from an LDS vector (var-indexed)
     auto grow = [&](const double *vec) -> double {
         double g = grc[0] * vec[gri[0]] + grc[1] * vec[gri[1]] + grc[2] * vec[gri[2]];
         if (isclf) {
             double s0 = 0.0;
-            for (int i = 0; i <= out; i++) s0 = fma(sh.Lg[i], vec[a0 + i], s0);
+#pragma unroll
+            for (int i = 0; i <= NQ; i++) s0 = fma(sh.Lg[i], vec[a0 + i], s0);   // Lg is 0 beyond outDim+useCLF
             g = s0;
         }
         return g;
@@ -265,11 +290,11 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
     auto arow = [&](const double *vec) -> double {
         double s0 = 0.0, s1 = 0.0;
         const int k = ise ? lane : 0;
-        for (int v = 0; v + 1 < nft; v += 2) {
+#pragma unroll 4
+        for (int v = 0; v < 24; v += 2) {            // A is zero-padded to 24 columns
             s0 = fma(sh.A[k * LDA + v], vec[v], s0);
             s1 = fma(sh.A[k * LDA + v + 1], vec[v + 1], s1);
         }
-        if (nft & 1) s0 = fma(sh.A[k * LDA + nft - 1], vec[nft - 1], s0);
         return s0 + s1 + ((k >= con) ? vec[a0 + k - con] : 0.0);
     };
     // A' y (variable lanes), y eq-indexed in LDS
@@ -310,6 +335,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             double *L = sh.leg[lane];
             L[0] = a; L[1] = b; L[2] = sig; L[3] = -mu * (w1 - w0) / a; L[4] = -mu * (w3 - w2) / b;
         }
+        LLST(1);
         gam = useCLF ? 1.0 / (wc + uv) : 0.0;
         if (vtype == 1 && isv) hinv = 1.0 / (prm.tauPen + sh.vt[gti[0]] + sh.vt[gti[1]]);
         SYNC();
@@ -319,6 +345,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             fia = (af == 0) ? 1.0 / L[0] : (af == 1) ? 1.0 / L[1] : 0.0;
             fla = (af == 0) ? fl0 : (af == 1) ? fl1 : 1.0;
         }
+        LLST(2);   // friction LDL' pieces
         // Y row j = (H^-1 A')_j (18 entries)
         if (isv) {
             double *Yj = sh.u.ip.Y + lane * LDJ;
@@ -335,33 +362,38 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
 #pragma unroll
                 for (int k = 0; k < NQ; k++) {
                     const int kk = k - con;
-                    Yj[k] = (kk >= 0) ? ((kk == i ? 1.0 / Dj : 0.0) - gam * vj * sh.vv[kk]) : 0.0;
+                    Yj[k] = (kk >= 0) ? ((kk == i ? iDj : 0.0) - gam * vj * sh.vv[kk]) : 0.0;
                 }
             }
         }
         SYNC();
+        LLST(3);   // Y
         // S = A Y, upper triangle spread over the wave (171 entries)
-        for (int e = lane; e < NQ * (NQ + 1) / 2; e += 64) {
-            // e -> (j, k), j <= k, row-major upper triangle
-            int j = 0, rem = e;
-            while (rem >= NQ - j) { rem -= NQ - j; j++; }
-            const int k = j + rem;
+#pragma unroll 1
+        for (int t = 0; t < 3; t++) {
+            const int e = lane + 64 * t;
+            if (e >= NQ * (NQ + 1) / 2) break;
+            const int jk = (t == 0) ? sjk[0] : (t == 1) ? sjk[1] : sjk[2];
+            const int j = (jk >> 8), k = jk & 255;
             double s0 = 0.0, s1 = 0.0;
-            for (int v = 0; v + 1 < nft; v += 2) {
+#pragma unroll 4
+            for (int v = 0; v < 24; v += 2) {
                 s0 = fma(sh.A[j * LDA + v], sh.u.ip.Y[v * LDJ + k], s0);
                 s1 = fma(sh.A[j * LDA + v + 1], sh.u.ip.Y[(v + 1) * LDJ + k], s1);
             }
-            if (nft & 1) s0 = fma(sh.A[j * LDA + nft - 1], sh.u.ip.Y[(nft - 1) * LDJ + k], s0);
             double s = s0 + s1;
             if (j >= con) s += sh.u.ip.Y[(a0 + j - con) * LDJ + k];
             sh.u.ip.S[j * LDJ + k] = s;
             sh.u.ip.S[k * LDJ + j] = s;
         }
         SYNC();
+        LLST(4);   // S
         const int i = ise ? lane : 0;
 #pragma unroll
         for (int j = 0; j < NQ; j++) Si[j] = ise ? sh.u.ip.S[i * LDJ + j] : ((lane == j) ? 1.0 : 0.0);
-        return gj_invert<NQ>(Si, NQ, lane, 0);
+        const int gjf = gj_invert<NQ>(Si, NQ, lane, 0);
+        LLST(5);   // Gauss-Jordan
+        return gjf;
     };
 
     // ------------------------------------------------------------------ Newton solve
@@ -385,7 +417,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             } else if (vtype == 1) {
                 uj = g * hinv;
             } else {
-                uj = r1 / Dj + gam * vj * (sh.sc[0] - vg);
+                uj = r1 * iDj + gam * vj * (sh.sc[0] - vg);
             }
             sh.vx[lane] = uj;
         }
@@ -445,8 +477,9 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             // residuals (computeresiduals, Auxilary.c:524-553)
             if (isv) sh.vx[lane] = xj;
             if (ise) sh.ve[lane] = yk;
-            if (isr) { sh.vr[lane] = z; sh.vt[lane] = z / s; }
-            if (isclf) sh.sc[1] = s / z;
+            const double iz = isr ? 1.0 / z : 0.0, is_ = isr ? 1.0 / s : 0.0;
+            if (isr) { sh.vr[lane] = z; sh.vt[lane] = z * is_; }
+            if (isclf) sh.sc[1] = s * iz;
             SYNC();
             const double rx = isv ? -Pj * xj - cj - gtcol(sh.vr) - acol(sh.ve) : 0.0;
             const double ry = ise ? bk - arow(sh.vx) : 0.0;
@@ -460,6 +493,7 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             }
             double nr[5] = {rx * rx, ry * ry, rz * rz, isr ? s * z : 0.0, lam * lam};
             wred<5, 0u>(nr);
+            LLST(10);  // residuals + norms
             if (sqrt(nr[0]) < th && sqrt(nr[2]) < th && sqrt(nr[1]) < th && nr[3] * invm < prm.tol) { flag = 0; break; }
             const double mu = nr[4] * invm;
             const bool dbg = agent == dag && lane == 0 && iter < 32;
@@ -473,8 +507,9 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             if (factor(sh.sc[1])) { flag = 1; break; }
             // predictor
             ds = -lam * lam;
-            kkt_solve(rx, ry, isr ? rz - ds / z : 0.0, omf, dx, dy, dz);
-            dsv = isr ? (ds - s * dz) / z : 0.0;
+            kkt_solve(rx, ry, isr ? rz - ds * iz : 0.0, omf, dx, dy, dz);
+            LLST(6);   // predictor solve
+            dsv = isr ? (ds - s * dz) * iz : 0.0;
             st[0] = (isr && dsv < 0) ? s / dsv : -1e300;   // max(v/dv) = -min(-v/dv) (findsteplength)
             st[1] = (isr && dz < 0) ? z / dz : -1e300;
             wred<2, 3u>(st);
@@ -490,9 +525,11 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
                 ds = -(lam * lam) - (dsv * dz) + sigma * mu;
                 if (dbg) { srb_ll_dbg[8 * iter + 5] = alp; srb_ll_dbg[8 * iter + 6] = ald; srb_ll_dbg[8 * iter + 7] = sigma; }
             }
+            LLST(7);   // predictor steps, rho
             // corrector (kktsolve_2)
-            kkt_solve(rx, ry, isr ? rz - ds / z : 0.0, omf, dx, dy, dz);
-            dsv = isr ? (ds - s * dz) / z : 0.0;
+            kkt_solve(rx, ry, isr ? rz - ds * iz : 0.0, omf, dx, dy, dz);
+            LLST(8);   // corrector solve
+            dsv = isr ? (ds - s * dz) * iz : 0.0;
             st[0] = (isr && dsv < 0) ? s / dsv : -1e300;
             st[1] = (isr && dz < 0) ? z / dz : -1e300;
             wred<2, 3u>(st);
@@ -509,9 +546,11 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
             yk += dy * ald;
             if (isr) { s += dsv * alp; z += dz * ald; }
             it++;
+            LLST(9);   // steps + update
         }
     }
 
+    LLST(11);  // init point / loop exit
     // ------------------------------------------------------------------ parse + epilogue
     const double *gq = io.q + A18, *gdq = io.dq + A18;
     if (isv) sh.vx[lane] = xj;
@@ -654,11 +693,22 @@ extern "C" __global__ void __launch_bounds__(64) srb_ll_kernel(SrbLLKParams prm,
         io.dq_out[A18 + lane] = dqn;
         io.q_out[A18 + lane] = qn;
     }
+    LLST(12);  // epilogue
 }
 
 // diagnostics: select the traced agent (-1 = none) and read the previous launch's trace
 static int g_dbg_agent = -1;
 extern "C" int srb_ll_dbg_agent(void) { return g_dbg_agent; }
+extern "C" int srb_ll_debug_stamps(unsigned long long *out, int reset)
+{
+    if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_ll_stamp), 16 * sizeof(unsigned long long), 0, hipMemcpyDeviceToHost) != hipSuccess)
+        return -2;
+    if (reset) {
+        unsigned long long z[16] = {0};
+        if (hipMemcpyToSymbol(HIP_SYMBOL(srb_ll_stamp), z, sizeof z, 0, hipMemcpyHostToDevice) != hipSuccess) return -2;
+    }
+    return 0;
+}
 extern "C" int srb_ll_debug_trace(int agent, double *out)
 {
     if (out && hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_ll_dbg), 512 * sizeof(double), 0, hipMemcpyDeviceToHost) != hipSuccess)
