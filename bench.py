@@ -191,15 +191,16 @@ def main_ll(args, world, rank, local_rank, dev):
         sys.path.insert(0, ROOT)
         import oracle
         p = oracle.ll_params()
-        sample = {k: v[:256] for k, v in full.items()}
+        nthreads = max(1, min(16, os.cpu_count() or 1))
+        sample = {k: v[:512] for k, v in full.items()}
         t1 = time.perf_counter(); n = 0
         while time.perf_counter() - t1 < args.cpu_seconds:
-            oracle.ll_calc_torque(p, sample)
-            n += 256
+            oracle.ll_calc_torque(p, sample, nthreads=nthreads)
+            n += 512
         dt = time.perf_counter() - t1
-        line["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": 1, "kind": "port",
-                                "sample": f"{n} calcTorque calls (256-agent slices of the same batch) in {dt:.1f} s, "
-                                          f"oracle/ll_ctrl.c, 1 thread"}
+        line["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
+                                "sample": f"{n} calcTorque calls (512-agent slices of the same batch) in {dt:.1f} s, "
+                                          f"oracle/ll_ctrl.c, {nthreads} threads"}
     if rank == 0:
         print(json.dumps(line), flush=True)
     ctrl.close()

@@ -291,8 +291,9 @@ def ll_build_qp(p: OrcLLParams, batch: dict, a: int = 0):
             G[:m * n].reshape(m, n).copy(), h[:m].copy(), clf[0], clf[1], clf[2], LgV.copy())
 
 
-def ll_calc_torque(p: OrcLLParams, batch: dict):
-    """calcTorque (LowLevelCtrl.cpp:18-113) for every agent of a ll_workload batch."""
+def ll_calc_torque(p: OrcLLParams, batch: dict, nthreads: int = 1):
+    """calcTorque (LowLevelCtrl.cpp:18-113) for every agent of a ll_workload batch
+    (nthreads > 1: contiguous agent ranges on pthreads)."""
     A_ = batch["ind"].shape[0]
     arrs = [_c(batch[k]).reshape(A_, -1) for k in LL_IN]
     ind = _c(batch["ind"], np.int32).reshape(A_, 4)
@@ -300,7 +301,9 @@ def ll_calc_torque(p: OrcLLParams, batch: dict):
     out = dict(tau=tau, QP_force=np.zeros((A_, 12)), ddq=np.zeros((A_, 18)), dq=np.zeros((A_, 18)),
                q=np.zeros((A_, 18)), V=np.zeros(A_), dV=np.zeros(A_), x=np.zeros((A_, 32)),
                status=np.zeros(A_, np.int32), iters=np.zeros(A_, np.int32))
-    lib().orc_ll_calc_torque_batch(ctypes.byref(p), A_, _ptr(ind), *[_ptr(a) for a in arrs], _ptr(tau),
+    fn = lib().orc_ll_calc_torque_batch if nthreads <= 1 else \
+        (lambda pp, *a: lib().orc_ll_calc_torque_batch_mt(pp, int(nthreads), *a))
+    fn(ctypes.byref(p), A_, _ptr(ind), *[_ptr(a) for a in arrs], _ptr(tau),
                                    _ptr(out["QP_force"]), _ptr(out["ddq"]), _ptr(out["dq"]), _ptr(out["q"]),
                                    _ptr(out["V"]), _ptr(out["dV"]), _ptr(out["x"]), _ptr(out["status"]),
                                    _ptr(out["iters"]))

@@ -25,6 +25,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <pthread.h>
 #include "oracle.h"
 
 #define NQ 18   /* TOTAL_DOF (global_loco_opts.h:24) */
@@ -331,5 +332,56 @@ int orc_ll_calc_torque_batch(const orc_ll_params *prm, int n_agents, const int *
         for (int i = 0; i < 32; i++) x[32 * a + i] = o.x[i];
         V[a] = o.V; dV[a] = o.dV; status[a] = o.status; iters[a] = o.iters;
     }
+    return 0;
+}
+
+/* the same, split over nthreads pthreads by contiguous agent ranges (bench.py cpu_baseline) */
+typedef struct {
+    const orc_ll_params *prm; int n;
+    const int *ind; const double *in[19]; double *tau, *QP_force, *ddq, *dq_out, *q_out, *V, *dV, *x;
+    int *status, *iters;
+} ll_job;
+
+static void *ll_worker(void *arg)
+{
+    ll_job *j = (ll_job *)arg;
+    const double *const *i = j->in;
+    orc_ll_calc_torque_batch(j->prm, j->n, j->ind, i[0], i[1], i[2], i[3], i[4], i[5], i[6], i[7], i[8], i[9], i[10],
+                             i[11], i[12], i[13], i[14], i[15], i[16], i[17], i[18], j->tau, j->QP_force, j->ddq,
+                             j->dq_out, j->q_out, j->V, j->dV, j->x, j->status, j->iters);
+    return NULL;
+}
+
+int orc_ll_calc_torque_batch_mt(const orc_ll_params *prm, int nthreads, int n_agents, const int *ind, const double *q,
+                                const double *dq, const double *Dinv, const double *B, const double *Hv,
+                                const double *Jc, const double *dJc, const double *Js, const double *Jtoe,
+                                const double *Jhip, const double *toePos, const double *hipPos, const double *H0,
+                                const double *dH0, const double *y, const double *dy, const double *hd,
+                                const double *dhd, const double *fDes, double *tau, double *QP_force, double *ddq,
+                                double *dq_out, double *q_out, double *V, double *dV, double *x, int *status,
+                                int *iters)
+{
+    static const int per[19] = {NQ, NQ, NQ * NQ, NQ * NU, NQ, NU * NQ, NU, NU * NQ, NU * NQ, NU * NQ, 12, 12,
+                                NQ * NQ, NQ, NQ, NQ, NQ, NQ, NU};
+    const double *in[19] = {q, dq, Dinv, B, Hv, Jc, dJc, Js, Jtoe, Jhip, toePos, hipPos, H0, dH0, y, dy, hd, dhd, fDes};
+    if (nthreads < 1) nthreads = 1;
+    if (nthreads > 64) nthreads = 64;
+    pthread_t th[64];
+    ll_job jobs[64];
+    int created[64] = {0};
+    for (int t = 0; t < nthreads; t++) {
+        const int lo = (int)((long long)n_agents * t / nthreads), hi = (int)((long long)n_agents * (t + 1) / nthreads);
+        ll_job *j = &jobs[t];
+        j->prm = prm; j->n = hi - lo; j->ind = ind + 4 * lo;
+        for (int k = 0; k < 19; k++) j->in[k] = in[k] + (size_t)per[k] * lo;
+        j->tau = tau + NQ * lo; j->QP_force = QP_force + 12 * lo; j->ddq = ddq + NQ * lo; j->dq_out = dq_out + NQ * lo;
+        j->q_out = q_out + NQ * lo; j->V = V + lo; j->dV = dV + lo; j->x = x + 32 * lo; j->status = status + lo;
+        j->iters = iters + lo;
+        if (j->n <= 0) continue;
+        if (pthread_create(&th[t], NULL, ll_worker, j) == 0) created[t] = 1;
+        else ll_worker(j);
+    }
+    for (int t = 0; t < nthreads; t++)
+        if (created[t]) pthread_join(th[t], NULL);
     return 0;
 }

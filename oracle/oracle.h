@@ -155,6 +155,15 @@ int orc_ll_calc_torque_batch(const orc_ll_params *prm, int n_agents, const int *
                              double *QP_force, double *ddq, double *dq_out, double *q_out, double *V, double *dV,
                              double *x, int *status, int *iters);
 
+int orc_ll_calc_torque_batch_mt(const orc_ll_params *prm, int nthreads, int n_agents, const int *ind, const double *q,
+                                const double *dq, const double *Dinv, const double *B, const double *Hv,
+                                const double *Jc, const double *dJc, const double *Js, const double *Jtoe,
+                                const double *Jhip, const double *toePos, const double *hipPos, const double *H0,
+                                const double *dH0, const double *y, const double *dy, const double *hd,
+                                const double *dhd, const double *fDes, double *tau, double *QP_force, double *ddq,
+                                double *dq_out, double *q_out, double *V, double *dV, double *x, int *status,
+                                int *iters);
+
 /* dense helpers (linalg.c) */
 int orc_chol(int n, double *A);                               /* in place, lower */
 void orc_chol_solve(int n, const double *L, double *x);
