@@ -1,7 +1,7 @@
 """Summarise rocprofv3 --pmc FETCH_SIZE / WRITE_SIZE passes (separate runs) of the solve
 kernel into a per-launch HBM traffic figure that bench.py reports as roofline.traffic.
 
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <agents> <out.json>
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <agents> <out.json> [kernel]
 
 FETCH_SIZE and WRITE_SIZE are in KiB per dispatch (rocprofv3).  No gfx950 x2 correction is
 applied to FETCH_SIZE: that correction is calibrated for 16-B/lane streaming reads
@@ -16,18 +16,23 @@ import statistics
 import sys
 
 
-def per_launch(d, counter):
+def per_launch(d, counter, kernel="srb_nmpc_kernel"):
+    """median over dispatches of the counter summed over its rows (per-XCD rows, if any)"""
     f = glob.glob(os.path.join(d, "**", "*counter_collection.csv"), recursive=True)[0]
-    vals = [float(r["Counter_Value"]) for r in csv.DictReader(open(f))
-            if "srb_nmpc_kernel" in r["Kernel_Name"] and r["Counter_Name"] == counter]
+    per = {}
+    for r in csv.DictReader(open(f)):
+        if kernel in r["Kernel_Name"] and r["Counter_Name"] == counter:
+            per[r["Dispatch_Id"]] = per.get(r["Dispatch_Id"], 0.0) + float(r["Counter_Value"])
+    vals = list(per.values())
     return statistics.median(vals), len(vals)
 
 
 def main():
     fdir, wdir, cfg, agents, out = sys.argv[1:6]
-    fk, nf = per_launch(fdir, "FETCH_SIZE")
-    wk, nw = per_launch(wdir, "WRITE_SIZE")
-    d = {"config": int(cfg), "agents": int(agents), "fetch_kib_per_launch": fk, "write_kib_per_launch": wk,
+    kernel = sys.argv[6] if len(sys.argv) > 6 else "srb_nmpc_kernel"
+    fk, nf = per_launch(fdir, "FETCH_SIZE", kernel)
+    wk, nw = per_launch(wdir, "WRITE_SIZE", kernel)
+    d = {"kernel": kernel, "config": cfg if not cfg.lstrip("-").isdigit() else int(cfg), "agents": int(agents), "fetch_kib_per_launch": fk, "write_kib_per_launch": wk,
          "hbm_bytes_per_launch": (fk + wk) * 1024.0, "dispatches": [nf, nw],
          "note": "raw FETCH_SIZE + WRITE_SIZE (KiB, median over dispatches), separate rocprofv3 --pmc passes; "
                  "no x2 FETCH correction (reads are not 16-B/lane streams)"}
