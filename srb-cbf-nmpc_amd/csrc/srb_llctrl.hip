@@ -53,6 +53,7 @@ struct LLShared {
     double A[NQ * LDA];                   // dense (F, tau) columns of A, row-major
     double vx[64], vr[64], ve[64], vg[64], vt[64];   // lane-indexed exchange vectors (slot ZS stays 0)
     double Lg[32], vv[32];                // u = [LgV; -1] and v = u / diag(auxPen, clfPen), by aux index
+    double vvp[48];                       // vv shifted by 12 with zeros in front (contact rows of Y)
     double leg[4][5];                     // per stance leg: a, b, sigma, l0, l1 of the friction LDL'
     double sc[8];
 };
@@ -129,6 +130,16 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         const int t = e / NQ, k = e - t * NQ;
         sh.u.as.J[k * LDJ + t] = (k < con) ? gJc[t * NU + k] : gH0[t * NQ + (k - con)];
     }
+    // touch the epilogue's kinematics now so that its loads hit the caches later
+    double pf = 0.0;
+    {
+        const double *gJs = io.Js + A12 * NQ, *gJt = io.Jtoe + A12 * NQ, *gJh = io.Jhip + A12 * NQ;
+#pragma unroll
+        for (int i = 0; i < 4; i++) {
+            const int e = lane + 64 * i;
+            if (e < NU * NQ) pf += gJs[e] + gJt[e] + gJh[e];
+        }
+    }
     // K = [Jc' B] (18 x nft), column v contiguous
     for (int e = lane; e < nft * NQ; e += 64) {
         const int v = e / NQ, t = e - v * NQ;
@@ -190,12 +201,14 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     const double Veps = prm.cce * Vv;
     // u = [LgV; -1], v = u ./ diag(auxPen.., clfPen): fixed for the whole solve
     if (lane < 32) { sh.Lg[lane] = 0.0; sh.vv[lane] = 0.0; }
-    if (lane < out) { sh.Lg[lane] = Lgi; sh.vv[lane] = Lgi / prm.auxPen; }
+    if (lane < 48) sh.vvp[lane] = 0.0;
+    if (lane < out) { sh.Lg[lane] = Lgi; sh.vv[lane] = Lgi / prm.auxPen; sh.vvp[12 + lane] = Lgi / prm.auxPen; }
     if (lane == out) { sh.Lg[lane] = useCLF ? -1.0 : 0.0; sh.vv[lane] = useCLF ? -1.0 / prm.clfPen : 0.0; }
     double uv = (useCLF && lane < out) ? Lgi * (Lgi / prm.auxPen) : 0.0;
     double dummy = 0.0;
     wsum2(uv, dummy);
     uv += useCLF ? 1.0 / prm.clfPen : 0.0;
+    if (pf == 1.2345e300) sh.sc[7] = pf;   // never true: keeps the cache-warming loads
     SYNC();
 
     // ------------------------------------------------------------------ lane roles
@@ -358,12 +371,14 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
 #pragma unroll
                 for (int k = 0; k < NQ; k++) Yj[k] = sh.A[k * LDA + lane] * hinv;
             } else {
+                // branch-free: vvp[12 + kk] is v_kk for output rows kk >= 0 and 0 on the contact rows
                 const int i = lane - a0;
+                const double gv = gam * vj;
+                double vk[NQ];
 #pragma unroll
-                for (int k = 0; k < NQ; k++) {
-                    const int kk = k - con;
-                    Yj[k] = (kk >= 0) ? ((kk == i ? iDj : 0.0) - gam * vj * sh.vv[kk]) : 0.0;
-                }
+                for (int k = 0; k < NQ; k++) vk[k] = sh.vvp[12 + k - con];
+#pragma unroll
+                for (int k = 0; k < NQ; k++) Yj[k] = fma(-gv, vk[k], (k - con == i) ? iDj : 0.0);
             }
         }
         SYNC();
