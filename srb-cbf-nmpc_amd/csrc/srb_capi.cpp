@@ -6,6 +6,7 @@
 // discretisation shared by every agent and the launch.
 #include <hip/hip_runtime.h>
 #include <cmath>
+#include <cstdlib>
 #include <cstdio>
 #include <cstring>
 #include <string>
@@ -33,17 +34,29 @@ static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 // SIMDs of a CU (NW = 4) for latency; larger batches run one wave per agent so that agents,
 // not waves of one agent, fill the SIMDs.
 static int g_cu_count = 0;
-static int wanted_waves(int n_agents) { return (g_cu_count > 0 && n_agents <= g_cu_count) ? 4 : 1; }
+static size_t g_lds_max = 160 * 1024;   // gfx950 LDS per CU; the device's sharedMemPerBlock once known
+// Waves per agent: small batches (up to one agent per CU) spread each agent over the four
+// SIMDs of a CU (NW = 4) for latency; larger batches run one wave per agent so that agents,
+// not waves of one agent, fill the SIMDs -- except large problems (more than five row slots per
+// lane with one wave, e.g. N = 20), where one wave spills its registers and two waves per agent
+// are 1.8x faster (profiles/r01_nw_tuning.txt).  SRB_NMPC_NW = 1 | 2 | 4 overrides (tuning).
+static int wanted_waves(int n_agents, int slots)
+{
+    static const int forced = [] { const char *e = std::getenv("SRB_NMPC_NW"); return e ? std::atoi(e) : 0; }();
+    if (forced == 1 || forced == 2 || forced == 4) return forced;
+    if (g_cu_count > 0 && n_agents <= g_cu_count) return 4;
+    return (slots > 5 * 64) ? 2 : 1;
+}
 
-// first instance with NW waves whose register bounds cover the problem (nz reduced rows, all
-// row slots); falls back to one wave per agent; NULL when none fits
 static const srb_instance *pick_instance(const SrbKParams &k, int nw = 1)
 {
     const int S = srb_slots(k.N, k.C, k.K_obs + k.K_nbr);
-    for (int pass = 0; pass < 2; pass++) {
-        const int want = pass == 0 ? nw : 1;
+    for (int pass = 0; pass < 3; pass++) {
+        const int want = pass == 0 ? nw : pass == 1 ? (nw == 4 ? 2 : 1) : 1;
         for (const srb_instance &in : g_instances)
-            if (in.nw == want && in.nzl >= k.nz && 64 * in.nw * in.ts >= S) return &in;
+            if (in.nw == want && in.nzl >= k.nz && 64 * in.nw * in.ts >= S &&
+                (size_t)srb_lds_doubles(k, in.nzl, in.nw) * sizeof(double) <= g_lds_max)
+                return &in;
     }
     return nullptr;
 }
@@ -187,7 +200,7 @@ extern "C" int srb_lds_bytes(const srb_params *p)
 extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out)
 {
     if (!out || max_agents <= 0) return fail(SRB_ERR_ARG, "bad arguments");
-    int rc = validate(p);
+    int rc = validate(p);                 // parameter checks first (no device needed)
     if (rc) return rc;
     int ndev = 0;
     HIPCHK(hipGetDeviceCount(&ndev));
@@ -197,7 +210,10 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
         hipDeviceProp_t prop;
         HIPCHK(hipGetDeviceProperties(&prop, device));
         g_cu_count = prop.multiProcessorCount;
+        g_lds_max = prop.sharedMemPerBlock;
     }
+    rc = validate(p);                     // again against this device's LDS per workgroup
+    if (rc) return rc;
     srb_ctx *c = new srb_ctx();
     c->p = *p; c->max_agents = max_agents; c->device = device;
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false;
@@ -253,7 +269,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
     if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
-    const srb_instance *in = pick_instance(k, wanted_waves(n_agents));
+    const srb_instance *in = pick_instance(k, wanted_waves(n_agents, srb_slots(k.N, k.C, k.K_obs + k.K_nbr)));
     if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers this problem");
     const size_t lds = (size_t)srb_lds_doubles(k, in->nzl, in->nw) * sizeof(double);
     c->last_nw = in->nw;

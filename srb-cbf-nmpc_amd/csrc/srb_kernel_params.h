@@ -23,7 +23,8 @@ struct SrbKParams {
 // (srb_capi.cpp).
 #define SRB_KERNEL_INSTANCES(X) \
     X(8, 1, 1) X(16, 1, 1) X(12, 3, 1) X(12, 4, 1) X(16, 4, 1) X(24, 5, 1) X(24, 8, 1) X(32, 4, 1) X(32, 8, 1) \
-    X(8, 1, 4) X(12, 1, 4) X(16, 1, 4) X(16, 2, 4) X(32, 2, 4)
+    X(8, 1, 4) X(12, 1, 4) X(16, 1, 4) X(16, 2, 4) X(32, 2, 4) \
+    X(12, 2, 2) X(16, 2, 2) X(24, 4, 2) X(24, 2, 4)
 static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K; }
 
 static inline int srb_r4(int x) { return (x + 3) & ~3; }
