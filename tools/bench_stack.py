@@ -1,0 +1,127 @@
+"""System-level timing of the whole swarm control stack on one GPU, every buffer resident in HBM:
+
+  * HL reference planner once (generateReferenceTrajectory, srb_hl_plan; shortened loop),
+  * per MPC cycle (Ts = 43 ms of robot time, MPC_dist.cpp:104): input assembly on the device
+    (srb_prepare_batch_device: updateState, get_lastState, copPlanner_eventbase,
+    footholdsPlanner) -> neighbour snapshot = last_state -> NMPC solve with inter-agent CBF
+    rows and the fused Bezier fit (srb_solve_batch_device),
+  * per low-level tick (1 ms, LL_Hz = 1000): the CLF-QP controller for every robot
+    (srb_ll_calc_torque_device).
+
+Prints one JSON line: milliseconds per MPC cycle and per LL tick, and the fraction of real
+time the GPU needs for A robots (MPC cycle / 43 ms + LL tick / 1 ms).
+
+    python tools/bench_stack.py [--agents 1024] [--cycles 20] [--horizon 4]
+
+The MPC footholds come from footholdsPlanner (one stance pattern over the whole horizon, as in
+the reference), so the default horizon is the reference's N = 4 (one gait domain).
+"""
+import argparse
+import json
+import os
+import sys
+
+import numpy as np
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "srb-cbf-nmpc_amd")]
+import torch  # noqa: E402
+
+import srbnmpc  # noqa: E402
+from srbnmpc import ll_workload, lowlevel  # noqa: E402
+
+ap = argparse.ArgumentParser()
+ap.add_argument("--agents", type=int, default=1024)
+ap.add_argument("--cycles", type=int, default=20)
+ap.add_argument("--loop", type=int, default=4000, help="HL planner steps (reference: 100000)")
+ap.add_argument("--horizon", type=int, default=4, help="MPC grids (reference: 4 = one gait domain)")
+args = ap.parse_args()
+A, N, C = args.agents, args.horizon, 2
+dev = torch.device("cuda:0")
+rng = np.random.default_rng(7)
+tt = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+
+# HL planner (one-off): start positions U[0,9] x [-2,2] (A1_Sim.cpp:944-945) and 20 obstacles,
+# the arena scaled with the swarm so that the density stays that of the reference's 4-robot runs
+sc = max(1.0, float(np.sqrt(A / 4.0)))
+start = np.stack([rng.uniform(0, 9 * sc, A), rng.uniform(-2 * sc, 2 * sc, A)], 1)
+n_obs = min(2048, int(20 * sc * sc))          # srb_hl_plan takes up to 2048 planner obstacles
+obst = np.stack([rng.uniform(0, 9 * sc, n_obs), rng.uniform(-2 * sc, 2 * sc, n_obs)], 1)
+import time  # noqa: E402
+t0 = time.perf_counter()
+parts = [srbnmpc.hl_plan(start[i:i + 1024], obst, loop=args.loop) for i in range(0, A, 1024)]   # swarms of <= 1024
+Pr = np.concatenate([a for a, _ in parts]); Prd = np.concatenate([b for _, b in parts])
+hl_s = time.perf_counter() - t0
+T = Pr.shape[1]
+
+p = srbnmpc.default_params(N, C, K_obs=3, K_nbr=8)
+s = srbnmpc.BatchSolver(p, A, 0)
+stream = torch.cuda.Stream(dev)
+torch.cuda.set_stream(stream)
+dPr, dPrd = tt(Pr.T), tt(Prd.T)
+gdh = rng.integers(0, max(1, (T - N) // 4), A)
+gd = tt(gdh, torch.int32)
+contact = tt(np.array([[1, 0, 0, 1] if a % 2 else [0, 1, 1, 0] for a in range(A)]), torch.int32)
+# the robots are on their planned paths: CoM at the window start of their gait domain
+col = 4 * gdh
+q = np.zeros((A, 18)); dq = np.zeros((A, 18))
+q[:, 0] = Pr[2 * np.arange(A), col]; q[:, 1] = Pr[2 * np.arange(A) + 1, col]
+dq[:, 0] = Prd[2 * np.arange(A), col]; dq[:, 1] = Prd[2 * np.arange(A) + 1, col]
+toe = np.zeros((A, 3, 4))
+for i, off in enumerate([(0.2188, -0.132), (0.2188, 0.132), (-0.1472, -0.132), (-0.1472, 0.132)]):
+    toe[:, 0, i] = q[:, 0] + off[0]; toe[:, 1, i] = q[:, 1] + off[1]
+dq_, q_, toe_, start_ = tt(dq), tt(q), tt(toe), tt(start)
+prep = dict(x0=torch.zeros((A, 4), dtype=torch.float64, device=dev),
+            ref=torch.zeros((A, 4 * N), dtype=torch.float64, device=dev),
+            foot=torch.zeros((A, N * 2 * C), dtype=torch.float64, device=dev),
+            last_state=torch.zeros((A, 4), dtype=torch.float64, device=dev),
+            status=torch.zeros(A, dtype=torch.int32, device=dev))
+sol = dict(x_qp=None, x=torch.zeros((A, p.nv), dtype=torch.float64, device=dev),
+           obj=torch.zeros(A, dtype=torch.float64, device=dev), status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+           iters=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+           alpha=torch.zeros((A, 20), dtype=torch.float64, device=dev))
+abuf = torch.zeros((A, 4), dtype=torch.float64, device=dev)
+obst_d = tt(obst)
+
+ll = srbnmpc.LowLevelCtrl(lowlevel.default_params(), A, 0)
+pool = ll_workload.make_batch(min(A, 512), seed=11)
+reps = -(-A // pool["ind"].shape[0])
+full = {k: np.concatenate([v] * reps)[:A] for k, v in pool.items()}
+lin = {"ind": tt(full["ind"], torch.int32)}
+for k in lowlevel.IN_KEYS:
+    lin[k] = tt(full[k].reshape(A, -1))
+lout = {k: torch.zeros((A, sz), dtype=torch.float64, device=dev) for k, sz in lowlevel.OUT_SIZE.items()}
+lout["status"] = torch.zeros(A, dtype=torch.int32, device=dev)
+lout["iters"] = torch.zeros(A, dtype=torch.int32, device=dev)
+
+
+def mpc_cycle():
+    s.prepare_device(dPr, dPrd, gd, contact, toe_, start_, q_, dq_, prep, stream=stream.cuda_stream)
+    abuf[:, 0] = prep["x0"][:, 0]; abuf[:, 2] = prep["x0"][:, 2]
+    s.solve_device(prep["x0"], prep["ref"], prep["foot"], obst_d, prep["last_state"], sol, stream=stream.cuda_stream,
+                   alpha_buf=abuf)
+
+
+def ll_tick():
+    ll.calc_torque_device(lin, lout, stream=stream.cuda_stream)
+
+
+for _ in range(3):
+    mpc_cycle(); ll_tick()
+torch.cuda.synchronize()
+res = {}
+for name, fn in (("mpc_cycle_ms", mpc_cycle), ("ll_tick_ms", ll_tick)):
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.cycles)]
+    for e0, e1 in ev:
+        e0.record(stream); fn(); e1.record(stream)
+    torch.cuda.synchronize()
+    ts = np.array([a.elapsed_time(b) for a, b in ev])
+    res[name] = float(np.median(ts)); res[name.replace("_ms", "_p99_ms")] = float(np.percentile(ts, 99))
+st = sol["status"].cpu().numpy()
+line = {"bench": "control_stack", "robots": A, "horizon": N, "K_obs": 3, "K_nbr": 8,
+        "hl_planner_s": hl_s, "hl_planner_steps": args.loop, **res,
+        "realtime_fraction": res["mpc_cycle_ms"] / 43.0 + res["ll_tick_ms"] / 1.0,
+        "mpc_prepare_ok": float((prep["status"].cpu().numpy() == 0).mean()),
+        "mpc_optimal_frac": float((st == 0).all(1).mean()),
+        "ll_optimal_frac": float((lout["status"].cpu().numpy() == 0).mean())}
+print(json.dumps(line), flush=True)
