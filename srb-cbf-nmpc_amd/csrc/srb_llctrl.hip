@@ -124,11 +124,35 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
     for (int e = lane; e < 64; e += 64) {
         sh.vx[e] = 0; sh.vr[e] = 0; sh.ve[e] = 0; sh.vg[e] = 0; sh.vt[e] = 0;
     }
-    for (int e = lane; e < NQ * NQ; e += 64) sh.D[e] = gD[e];
-    // J = [Jc (con rows); H0 (out rows)], row-major; e runs down the stored columns
-    for (int e = lane; e < NQ * NQ; e += 64) {
-        const int t = e / NQ, k = e - t * NQ;
-        sh.u.as.J[k * LDJ + t] = (k < con) ? gJc[t * NU + k] : gH0[t * NQ + (k - con)];
+    // every global load of the assembly is issued before the first LDS store (one HBM round
+    // trip instead of one per loop trip): Dinv, J = [Jc (con rows); H0 (out rows)] down the
+    // stored columns, K = [Jc' B] (18 x nft) column by column
+    {
+        double tD[6], tJ[6], tK[7];
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const int e = lane + 64 * i;
+            const int t = e / NQ, k = e - t * NQ;
+            tD[i] = (e < NQ * NQ) ? gD[e] : 0.0;
+            tJ[i] = (e < NQ * NQ) ? ((k < con) ? gJc[t * NU + k] : gH0[t * NQ + (k - con)]) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int e = lane + 64 * i;
+            const int v = e / NQ, t = e - v * NQ;
+            tK[i] = (e < nft * NQ) ? ((v < con) ? gJc[t * NU + v] : gB[(v - con) * NQ + t]) : 0.0;
+        }
+#pragma unroll
+        for (int i = 0; i < 6; i++) {
+            const int e = lane + 64 * i;
+            const int t = e / NQ, k = e - t * NQ;
+            if (e < NQ * NQ) { sh.D[e] = tD[i]; sh.u.as.J[k * LDJ + t] = tJ[i]; }
+        }
+#pragma unroll
+        for (int i = 0; i < 7; i++) {
+            const int e = lane + 64 * i;
+            if (e < nft * NQ) sh.u.as.K[e] = tK[i];
+        }
     }
     // touch the epilogue's kinematics now so that its loads hit the caches later
     double pf = 0.0;
@@ -139,11 +163,6 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
             const int e = lane + 64 * i;
             if (e < NU * NQ) pf += gJs[e] + gJt[e] + gJh[e];
         }
-    }
-    // K = [Jc' B] (18 x nft), column v contiguous
-    for (int e = lane; e < nft * NQ; e += 64) {
-        const int v = e / NQ, t = e - v * NQ;
-        sh.u.as.K[v * NQ + t] = (v < con) ? gJc[t * NU + v] : gB[(v - con) * NQ + t];
     }
     SYNC();
     // M = J Dinv (18 x 18)
