@@ -21,7 +21,9 @@ for c in 3 5; do
   timeout -k 10 200 python bench.py --config $c --no-cpu-baseline > gpurun_out/bench_c$c.json 2> gpurun_out/bench_c$c.err || { tail gpurun_out/bench_c$c.err; exit 1; }
   cat gpurun_out/bench_c$c.json
 done
-for c in 2 3; do
+timeout -k 10 300 python bench.py --path ll > gpurun_out/bench_ll.json 2> gpurun_out/bench_ll.err || { tail gpurun_out/bench_ll.err; exit 1; }
+cat gpurun_out/bench_ll.json
+for c in 2 3 5; do
   rm -rf gpurun_out/prof_c$c
   timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_c$c -o run --output-format csv -- \
       python3 bench.py --config $c --no-cpu-baseline --steps 20 > gpurun_out/prof_c$c.log 2>&1 || { tail gpurun_out/prof_c$c.log; exit 1; }
@@ -31,4 +33,7 @@ for ctr in FETCH_SIZE WRITE_SIZE; do
   timeout -k 10 300 rocprofv3 --pmc $ctr -d gpurun_out/pmc_$ctr -o run --output-format csv -- \
       python3 bench.py --config 2 --no-cpu-baseline --steps 10 > gpurun_out/pmc_$ctr.log 2>&1 || { tail gpurun_out/pmc_$ctr.log; exit 1; }
 done
+rm -rf gpurun_out/prof_ll
+timeout -k 10 300 rocprofv3 --kernel-trace --stats -d gpurun_out/prof_ll -o run --output-format csv -- \
+    python3 bench.py --path ll --no-cpu-baseline --steps 20 > gpurun_out/prof_ll.log 2>&1 || { tail gpurun_out/prof_ll.log; exit 1; }
 find gpurun_out -name "*stats*.csv" -o -name "*counter_collection*.csv" | sort
