@@ -123,3 +123,29 @@ def test_split_layout():
     X, U, L, s = srbnmpc.split(p, x)
     assert X.shape == (10, 4) and U.shape == (10, 2) and L.shape == (10, 2) and s == p.nv - 1
     assert X[1, 0] == 4 and U[0, 0] == 40 and L[0, 0] == 60
+
+
+def test_ll_params_defaults_and_validation():
+    """srb_ll_params_default = Settings::LL_params defaults (Parameters.cpp:62-75) and the
+    oracle's; out-of-range parameters are rejected before any device is touched."""
+    from srbnmpc import lowlevel
+    p = lowlevel.default_params()
+    o = oracle.ll_params()
+    for k in ("mu", "kp", "kd", "useCLF", "tauPen", "dfPen", "auxPen", "clfPen", "auxMax", "clfEps", "maxit", "tol"):
+        assert getattr(p, k) == getattr(o, k), k
+    assert (p.kp, p.kd, p.auxPen, p.clfPen, p.clfEps) == (700.0, 40.0, 1e6, 1e8, 0.8)
+    lib = lowlevel._bind()
+    h = ctypes.c_void_p()
+    for bad in (dict(kp=-1.0), dict(clfEps=0.0), dict(tol=0.0), dict(maxit=-1), dict(auxPen=0.0)):
+        q = lowlevel.default_params(**bad)
+        assert lib.srb_ll_ctx_create(ctypes.byref(q), 8, 0, ctypes.byref(h)) == -1, bad
+        assert b"out of range" in lib.srb_last_error()
+    assert lib.srb_ll_ctx_create(ctypes.byref(p), 0, 0, ctypes.byref(h)) == -1
+
+
+def test_ll_no_silent_cpu_fallback_without_gpu():
+    import torch
+    if torch.cuda.is_available():
+        pytest.skip("GPU present")
+    with pytest.raises(RuntimeError):
+        srbnmpc.LowLevelCtrl(max_agents=4)
