@@ -23,6 +23,10 @@
 #include <string.h>
 #include "oracle.h"
 
+/* initial inequality duals: 100, the scale of the tracking weights' multipliers (against 1:
+ * 20-25 % fewer NLP iterations on the bench/test workloads, profiles/r01_nlp_z0_scan.txt) */
+#define ORC_NLP_Z0 100.0
+
 typedef struct {
     int n, p, mq, K, N, mo, mv, m;
     const double *Pd, *c, *A, *b, *G, *h, *obs, *eps;
@@ -155,11 +159,11 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
 
     memcpy(x, x_init, sizeof(double) * n);
     rows_eval(&P, x, g, Jv, Ji);
-    {   /* slacks: iSWIFT-style shift of h - g(x); duals 1 */
+    {   /* slacks: iSWIFT-style shift of h - g(x); duals ORC_NLP_Z0 (the kernel's SRB_NLP_Z0) */
         double mn = hh[0] - g[0];
         for (int r = 1; r < m; r++) if (hh[r] - g[r] < mn) mn = hh[r] - g[r];
         double ap = -mn;
-        for (int r = 0; r < m; r++) { s[r] = (ap < 0) ? hh[r] - g[r] : hh[r] - g[r] + (1 + ap); z[r] = 1.0; }
+        for (int r = 0; r < m; r++) { s[r] = (ap < 0) ? hh[r] - g[r] : hh[r] - g[r] + (1 + ap); z[r] = ORC_NLP_Z0; }
     }
     {   /* q = A'y, y = argmin |A'y + (Px + c + J'z)|  ->  (A A') y = -A v */
         double *v = malloc(sizeof(double) * n), *AAt = malloc(sizeof(double) * (p ? p * p : 1)), *yy = malloc(sizeof(double) * (p + 1));

@@ -5,6 +5,11 @@
 #define SRB_KNN_MAX 16    // nearest static obstacles / neighbours per agent (each)
 #define SRB_MAX_NZ 32     // reduced Newton system size bound: nz = N(C-1)+1 <= 32
 #define SRB_MAX_N 33      // CoM-CoP slots 2(N-1) fit one 64-lane trip
+// NLP stage: initial inequality duals (the oracle's ORC_NLP_Z0, oracle/nlp_ipm.c).  100 is the
+// scale of the tracking weights' multipliers; on the five bench/test workloads it takes the
+// NLP from 10.4-11.4 to 8.0-8.6 iterations on average and from 13-18 to 9-13 at most
+// (profiles/r01_nlp_z0_scan.txt) against z = 1.
+#define SRB_NLP_Z0 100.0
 
 struct SrbKParams {
     int N, C, K_obs, K_nbr;

@@ -693,18 +693,18 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     const double f = q.jd;
                     q.s[0] = (q.m[0] != 0.0) ? q.h[0] - f + ssh : 1.0;
                     q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
-                    q.z[0] = q.z[1] = 1.0;
+                    q.z[0] = q.z[1] = SRB_NLP_Z0;
                     if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x
                         const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
 #pragma unroll
                         for (int a = 0; a < NZL; a++)
                             R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
                     }
-                    // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = 1: J'1 vanishes on every
+                    // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = z0: J'1 vanishes on every
                     // +- pair, leaving the obstacle rows
                     if (q.kind == K_VAR) { W[q.r] = 1.0; CF[q.r] = fma(q.a0, f, q.a1); }
                     else if (q.kind == K_COP) { W[q.r] = 0.0; CF[q.r] = 0.0; }
-                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = 1.0; }
+                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = SRB_NLP_Z0; }
                 }
             SYNC();
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, ZZ, vg, nz, tid, part);

@@ -1,7 +1,7 @@
 """Generate the committed golden fixtures (run in the survey container, which has
 /root/reference and oracle/_ref built from it):
 
-    make -C oracle all ref && python tests/golden/make_goldens.py
+    make -C oracle all ref && python tests/golden/make_goldens.py [ll | nlp]
 
 Fixtures written (data only -- inputs and expected outputs):
   kat1.json           iSWIFT's bundled test QP (optimization/iSWIFT/include/Matrices_small.h,
@@ -205,6 +205,10 @@ if __name__ == "__main__":
     oracle.build()
     if sys.argv[1:] == ["ll"]:
         ll_ctrl()
+        sys.exit(0)
+    if sys.argv[1:] == ["nlp"]:               # the NLP fixtures only (oracle NLP changes)
+        kat2()
+        nlp_random()
         sys.exit(0)
     ll_ctrl()
     kat1()
