@@ -321,6 +321,7 @@ def main():
                    "contacts": C, "K_obs": cfg["K_obs"], "K_nbr": cfg["K_nbr"], "parallelism": f"agents sharded x{world}"},
         "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
         "optimal_frac": float((status == 0).all(1).mean()),
+        "acceptable_frac": float(((status[:, 0] == 0) & (status[:, 1] == 4)).mean()),
         "iters_mean": [float(iters[:, 0].mean()), float(iters[:, 1].mean())],
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,

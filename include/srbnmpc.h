@@ -72,7 +72,10 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *   x_qp      [A][nv]       QP-stage solution (qp_solution_eventbased_, :350-354); may be NULL
  *   x         [A][nv]       final decision vector (mpc_state_eventbased_ after :423-426)
  *   obj       [A]           0.5 x'Q_qp x + f'x (ExCost::GetCost)
- *   status    [A][2] int    QP, NLP exit codes
+ *   status    [A][2] int    QP, NLP exit codes: 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL (iSWIFT's);
+ *                           NLP also 4 ACCEPTABLE: stopped at a near-optimal iterate (primal and
+ *                           complementarity met, dual residual within 100x of its threshold)
+ *                           whose next step was blocked or needed an inertia shift
  *   iters     [A][2] int    QP, NLP interior-point iterations
  * Bezier fit of the predicted CoM (fitComTrajectory_eventbase, MPC_dist.cpp:784-855), fused
  * into the solve; both NULL = not fitted (needs N >= 4):

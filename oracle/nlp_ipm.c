@@ -26,6 +26,8 @@
 /* initial inequality duals: 100, the scale of the tracking weights' multipliers (against 1:
  * 20-25 % fewer NLP iterations on the bench/test workloads, profiles/r01_nlp_z0_scan.txt) */
 #define ORC_NLP_Z0 100.0
+/* a step shorter than this from a near-optimal iterate ends the NLP as ACCEPTABLE (4) */
+#define ORC_NLP_BLOCKED 0.05
 
 typedef struct {
     int n, p, mq, K, N, mo, mv, m;
@@ -193,6 +195,10 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         double gmax = 1.0;
         for (int j = 0; j < n; j++) { double gj = fabs(Pd[j] * x[j] + c[j]); if (gj > gmax) gmax = gj; }
         if (nrx < th * gmax && nrz < th && nry < th && sz / m < tol) { flag = 0; break; }
+        /* near the optimum: primal and complementarity met, dual residual within 100x of its
+         * threshold.  An inertia shift or a blocked step from here is the condensed system's
+         * round-off (W = z/s ~ 1e14 swamps the soft curvature), not progress: ACCEPTABLE (4) */
+        const int near = nrz < th && nry < th && sz / m < tol && nrx < 100.0 * th * gmax;
         for (int r = 0; r < m; r++) { lam[r] = sqrt(s[r] * z[r]); wgt[r] = s[r] / z[r]; }
         double mu = dotv(lam, lam, m) / m;
 
@@ -236,6 +242,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             delta = (delta == 0.0) ? dstart : delta * 10.0;
         }
         if (!ok) { flag = 1; break; }
+        if (near && delta != 0.0) { flag = 4; break; }
         /* full-space KKT [H + delta I, A'; A, 0] */
         memset(K, 0, sizeof(double) * dim * dim);
         for (int i = 0; i < n; i++) { for (int j = 0; j < n; j++) K[i * dim + j] = Hl[i * n + j]; K[i * dim + i] += delta; }
@@ -275,6 +282,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             }
         }
         double ap = steplen(s, dsv, m), ad = steplen(z, dz, m);
+        if (near && (ap < ORC_NLP_BLOCKED || ad < ORC_NLP_BLOCKED)) { flag = 4; break; }
         ap = 0.99 * ap < 1.0 ? 0.99 * ap : 1.0;
         ad = 0.99 * ad < 1.0 ? 0.99 * ad : 1.0;
         for (int j = 0; j < n; j++) { x[j] += ap * dx[j]; q[j] += ad * dq[j]; }

@@ -68,6 +68,18 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 #define STAMP_FLUSH(agent) do {} while (0)
 #endif
 
+// --------------------------------------------------------------------------- diagnostic trace
+// Built only with -DSRB_NLPDBG (make nlpdbg -> srbnmpc/libsrbnmpc_nlpdbg.so): agent
+// srb_nlp_dbg_agent records, per NLP iteration, ||rx||, its threshold, ||rz||, s'z/m, ap, ad,
+// delta and sigma (8 doubles) into srb_nlp_dbg; nothing else reads it.
+#ifdef SRB_NLPDBG
+__device__ double srb_nlp_dbg[8 * 64];
+__device__ int srb_nlp_dbg_agent = -1;
+#define NLPDBG(it, k, v) do { if (nl && agent == srb_nlp_dbg_agent && tid == 0 && (it) < 64) srb_nlp_dbg[8 * (it) + (k)] = (v); } while (0)
+#else
+#define NLPDBG(it, k, v) do {} while (0)
+#endif
+
 // --------------------------------------------------------------------------- term rows
 // Term row t (Z row of a variable, M_e, M_o) at R + t * LDR; LDR = NZL + 1 (odd: lane-
 // parallel row reads stay conflict-free).  Rows are zero beyond nz and beyond the count.
@@ -769,7 +781,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
             // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
             const double thx = nl ? th * gm : th;
+            NLPDBG(iter, 0, nrx); NLPDBG(iter, 1, thx); NLPDBG(iter, 2, nrz); NLPDBG(iter, 3, sz * inv_m);
             if (nrx < thx && nrz < th && sz * inv_m < tol) { flag = 0; break; }
+            // NLP near the optimum (primal and complementarity met, dual residual within 100x):
+            // an inertia shift or a blocked step from here is round-off of the condensed
+            // system (W = z/s ~ 1e14 swamps the soft curvature in Z'HZ), not progress -> exit
+            // ACCEPTABLE (4) at this iterate (oracle/nlp_ipm.c, the same rule)
+            const bool near = nl && nrz < th && sz * inv_m < tol && nrx < 100.0 * thx;
+            bool acc = false;
             const bool pc = nl || (sigma > sigma_d);
             double delta = 0.0;
             // right-hand side of pass (0 predictor, 1 corrector / centring):
@@ -856,6 +875,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 }
                 STAMP_END(5);
                 if (!ok) { flag = 1; break; }
+                if (near && delta != 0.0) { flag = 4; break; }
             }
             const double *Hsv = (delta != 0.0) ? HS : H0;
 
@@ -915,9 +935,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
                     continue;
                 }
+                if (near && (ap < SRB_NLP_BLOCKED || ad < SRB_NLP_BLOCKED)) { acc = true; break; }
                 // ---- update (Prime.c:208-216): step 0.99 alpha capped at 1
                 ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
                 ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
+                NLPDBG(iter, 4, ap); NLPDBG(iter, 5, ad); NLPDBG(iter, 6, delta); NLPDBG(iter, 7, sigma);
                 // rx' = (1-ad) rx + (ad-ap) P dx + ad (hess + delta) dx - (J(x') - J(x))' z'
                 // (hess from the old obstacle duals in zo, the Jacobian change from the new ones)
                 double hso[TS];
@@ -961,6 +983,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                 STAMP_END(14);
             }
+            if (acc) { flag = 4; break; }
             it++;
         }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }

@@ -24,7 +24,7 @@ LIB_PATH = os.path.join(_HERE, "libsrbnmpc.so")
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 
-OPTIMAL, KKTFAIL, MAXIT, FATAL = 0, 1, 2, 3
+OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
 
 
 class Params(ctypes.Structure):

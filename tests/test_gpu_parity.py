@@ -173,6 +173,38 @@ def test_full_size_properties(A, Kn):
         assert cert["stat_rel"] < 1e-5 and cert["prim"] < 1e-6, (a, cert)
 
 
+def test_config5_full_size_vs_oracle_and_acceptable_exit():
+    """bench config 5 (2048 agents, N = 20, 3 static + 8 neighbour rows) at full size.
+
+    NLP status 4 (ACCEPTABLE) ends the few solves whose near-optimal iterate meets
+    a blocked step or an inertia shift, instead of MAXIT at 50 iterations.  Tolerances: on
+    these near-degenerate instances the NLP exit test (dual residual 1e-6 max(1, |Px+c|))
+    leaves x free to 1e-4..1e-3 along flat directions, so 99 % of agents must agree with the
+    oracle within NLP_TOL, all within 1e-3, and every ACCEPTABLE solution (plus a sample of the
+    rest) must pass the KKT certificate."""
+    A, N, C, Ko, Kn = 2048, 20, 2, 3, 8
+    b = workload.make_batch(A, N, C, seed=1234)
+    s = solver(N, C, Ko, Kn)
+    out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    st, it = out["status"], out["iters"]
+    assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
+    acc = np.where(st[:, 1] == srbnmpc.ACCEPTABLE)[0]
+    assert acc.size <= 0.01 * A
+    assert it[:, 1].max() <= 20                                    # no MAXIT tail
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], nthreads=16)
+    assert (r["status"] == 0).all()
+    e = np.abs(xus(N, out["x"]) - xus(N, r["x"])).max(1)
+    assert np.mean(e < NLP_TOL) >= 0.99 and e.max() < 1e-3
+    rng = np.random.default_rng(5)
+    for a in np.r_[acc, rng.choice(A, 16, replace=False)]:
+        obs, eps = oracle.select_obstacles(op, b["x0"][a], b["obstacles"], b["nbr_state"], int(a))
+        Pd, c, Aeq, beq, G, h = oracle.build_qp(op, b["x0"][a], b["ref"][a], b["foot"][a])
+        gJ, hh = nlp_rows(N, C, Pd.size, G, h, obs, eps, s.params.vsat)
+        cert = certify(Pd, c, Aeq, beq, gJ, hh, out["x"][a])
+        assert cert["stat_rel"] < 1e-5 and cert["prim"] < 1e-6, (int(a), cert)
+
+
 def test_knn_matches_bruteforce():
     """Inter-agent neighbour selection == (d^2, index) order of the reference's argmin scan."""
     N, C, Ko, Kn, A = 10, 2, 0, 8, 512

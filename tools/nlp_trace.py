@@ -1,0 +1,35 @@
+"""Diagnostic: per-iteration NLP trace of chosen agents of a bench configuration's batch
+(libsrbnmpc_nlpdbg.so, make -C srb-cbf-nmpc_amd nlpdbg).
+
+    python tools/nlp_trace.py config agent [agent ...]"""
+import ctypes
+import os
+import sys
+
+ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
+sys.path[:0] = [ROOT, os.path.join(ROOT, "srb-cbf-nmpc_amd")]
+import numpy as np  # noqa: E402
+
+import bench  # noqa: E402
+import srbnmpc  # noqa: E402
+from srbnmpc import workload  # noqa: E402
+
+srbnmpc.LIB_PATH = os.path.join(os.path.dirname(srbnmpc.__file__), "libsrbnmpc_nlpdbg.so")
+c = int(sys.argv[1])
+cfg = bench.CONFIGS[c]
+A, N, C = cfg["agents"], cfg["N"], cfg["C"]
+p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
+b = workload.make_batch(A, N, C, seed=1234)
+s = srbnmpc.BatchSolver(p, A)
+L = srbnmpc.lib()
+L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
+buf = np.zeros(8 * 64)
+for ag in map(int, sys.argv[2:]):
+    L.srb_debug_nlp_trace(ag, None)
+    out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"] if cfg["K_nbr"] else None)
+    L.srb_debug_nlp_trace(-1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
+    print(f"agent {ag}: status {out['status'][ag].tolist()} iters {out['iters'][ag].tolist()}")
+    print("  it     |rx|        thx        |rz|       s'z/m      ap        ad        delta     sigma")
+    for i in range(int(out["iters"][ag, 1]) + 1):
+        r = buf[8 * i:8 * i + 8]
+        print(f"  {i:2d} " + " ".join(f"{v:10.3e}" for v in r), flush=True)
