@@ -149,8 +149,8 @@ int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, in
                 double *Prd);
 
 /* Per-launch timing of the last srb_solve_batch_device call, measured with HIP events on
- * the stream the kernel ran on (ms).  The nearest-obstacle selection is fused into the
- * solve kernel, so knn_ms is always 0 (kept for ABI stability). */
+ * the stream the kernel ran on (ms): knn_ms the obstacle / neighbour selection kernel
+ * (0 when nothing is selected: QP only, or K_obs = K_nbr = 0), solve_ms the solve kernel. */
 int srb_last_kernel_ms(srb_ctx *ctx, float *knn_ms, float *solve_ms);
 
 /* Dynamic LDS bytes one agent's workgroup uses (for occupancy reports). */

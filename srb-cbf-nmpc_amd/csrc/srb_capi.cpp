@@ -18,13 +18,16 @@
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
-        const double *alpha_buf, double *alpha_out);
+        const double *alpha_buf, double *alpha_out, const int *sel_g);
 SRB_KERNEL_INSTANCES(DECL_NMPC)
 #undef DECL_NMPC
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
-                              double *);
+                              double *, const int *);
+extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const double *obstacles, int n_obs,
+                                          const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
+                                          int *sel_out);
 struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; };
 #define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
@@ -86,6 +89,7 @@ struct srb_ctx {
     // device staging
     double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj, *abuf, *alpha;
     int *status, *iters;
+    int *sel;                      // [max_agents][2 SRB_KNN_MAX] selected obstacle / neighbour rows
     size_t cap_obs, cap_nbr;
     float knn_ms, solve_ms;
     bool timed;
@@ -231,6 +235,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
     HIPCHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
     HIPCHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
+    HIPCHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
     *out = c;
     return SRB_OK;
 }
@@ -241,7 +246,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
     void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr,
-                    c->abuf, c->alpha};
+                    c->abuf, c->alpha, c->sel};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
@@ -277,10 +282,16 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     const int n_obs = k.K_obs > 0 ? d->n_obs : 0, n_all = k.K_nbr > 0 ? d->n_all : 0;
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
-    // one launch: nearest-obstacle selection, QP stage and NLP stage per agent
+    // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
+    if (use_nlp && k.K_obs + k.K_nbr > 0) {
+        hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, d->x0, d->obstacles, n_obs,
+                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, c->sel);
+        HIPCHK(hipGetLastError());
+    }
+    HIPCHK(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
-                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr);
+                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)c->sel);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
@@ -373,10 +384,11 @@ extern "C" int srb_last_kernel_ms(srb_ctx *c, float *knn_ms, float *solve_ms)
 {
     if (!c || !c->timed) return fail(SRB_ERR_ARG, "no timed launch");
     HIPCHK(hipEventSynchronize(c->ev[1]));
-    float b = 0;
-    HIPCHK(hipEventElapsedTime(&b, c->ev[0], c->ev[1]));
-    if (knn_ms) *knn_ms = 0.0f;         // selection is fused into the solve kernel
-    if (solve_ms) *solve_ms = b;
+    float a = 0, b = 0;
+    HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[2]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[1]));
+    if (knn_ms) *knn_ms = a;            // srb_knn_kernel (0 when there is nothing to select)
+    if (solve_ms) *solve_ms = b;        // srb_nmpc_kernel_*
     return SRB_OK;
 }
 

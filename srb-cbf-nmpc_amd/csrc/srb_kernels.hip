@@ -334,60 +334,6 @@ __device__ __forceinline__ int lambda_basis(const double *F, int C, int t, doubl
     return 0;
 }
 
-// --------------------------------------------------------------------------- kNN
-// (d, index) lexicographic wave argmin; every lane gets the winner
-__device__ __forceinline__ void wargmin(double &d, int &idx)
-{
-#pragma unroll
-    for (int o = 32; o > 0; o >>= 1) {
-        const double od = __shfl_xor(d, o, WAVE);
-        const int oi = __shfl_xor(idx, o, WAVE);
-        if (od < d || (od == d && oi < idx)) { d = od; idx = oi; }
-    }
-}
-
-// K nearest rows of a table (row i at tab[stride*i], x at +0, y at +1) to (px, py),
-// ascending in (d^2, index) -- the order of the reference's strict-'<' scan
-// (MPC_dist.cpp:373-382) -- excluding row `self`; indices to sel[0..K).  The wave scans
-// the table once: every lane keeps a sorted top-K of its own rows (visited in increasing
-// index, so a strict '<' keeps the lower index on ties), then K rounds of a wave argmin
-// over the lane heads pop the global order.  Rows stream from L2 coalesced across lanes.
-__device__ __forceinline__ void knn_select(int lane, double px, double py, const double *__restrict__ tab,
-                                           int stride, int n_rows, int self, int K, int *sel)
-{
-    double bd[SRB_KNN_MAX]; int bi[SRB_KNN_MAX];
-#pragma unroll
-    for (int j = 0; j < SRB_KNN_MAX; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
-    double wd = 1e300;
-    for (int i = lane; i < n_rows; i += WAVE) {
-        const double dx = tab[(size_t)stride * i] - px, dy = tab[(size_t)stride * i + 1] - py;
-        const double d = dx * dx + dy * dy;
-        if (i == self || !(d < wd)) continue;
-        double cd = d; int ci = i;
-#pragma unroll
-        for (int j = 0; j < SRB_KNN_MAX; j++) {
-            const bool lt = (j < K) && (cd < bd[j]);
-            const double td = bd[j]; const int ti = bi[j];
-            bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
-            cd = lt ? td : cd; ci = lt ? ti : ci;
-        }
-#pragma unroll
-        for (int j = 0; j < SRB_KNN_MAX; j++)
-            if (j == K - 1) wd = bd[j];
-    }
-#pragma clang loop unroll(disable)
-    for (int j = 0; j < K; j++) {
-        double d = bd[0]; int idx = bi[0];
-        wargmin(d, idx);
-        if (bi[0] == idx) {
-#pragma unroll
-            for (int t = 0; t + 1 < SRB_KNN_MAX; t++) { bd[t] = bd[t + 1]; bi[t] = bi[t + 1]; }
-            bd[SRB_KNN_MAX - 1] = 1e300; bi[SRB_KNN_MAX - 1] = 0x7fffffff;
-        }
-        if (lane == 0) sel[j] = (idx == 0x7fffffff) ? -1 : idx;
-    }
-}
-
 // --------------------------------------------------------------------------- slots
 // Every inequality row of the problem belongs to a SLOT: a bound pair on one scalar
 // function f of x (row 0: f <= h0, row 1: -f <= h1; a single row has row 1 off) whose
@@ -445,7 +391,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ nbr_state, int n_all, int agent_offset,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
-                const double *__restrict__ alpha_buf, double *__restrict__ alpha_out, double *lds)
+                const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
+                const int *__restrict__ sel_g, double *lds)
 {
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, LDH = NZM + 1;
@@ -655,14 +602,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // obstacles per grid: the K_obs nearest static obstacles (MPC_dist.cpp:371-396,
             // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
             // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
-#pragma clang loop unroll(disable)
-            for (int tsel = 0; tsel < 2; tsel++) {
-                const int Kt = tsel ? prm.K_nbr : prm.K_obs;
-                if (Kt > 0 && wv == 0)
-                    knn_select(lane, x0[0], x0[2], tsel ? nbr_state : obstacles, tsel ? 4 : 2, tsel ? n_all : n_obs,
-                               tsel ? agent_offset + agent : -1, Kt, sel + (tsel ? prm.K_obs : 0));
-            }
+            // (selected by srb_knn_kernel, launched just before this kernel on the same stream)
+            if (tid < K) sel[tid] = sel_g[(size_t)agent * K + tid];
             SYNC();
+            STAMP_END(6);                                     // NLP slot 6: neighbour selection
             for (int j = 0; j < K; j++) {
                 const bool st = j < prm.K_obs;
                 const int bi = sel[j];
@@ -1033,13 +976,37 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
-        int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out)        \
+        int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,       \
+        const int *__restrict__ sel_g)                                                                         \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
         nmpc_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
-                                x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, lds);  \
+                                x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, sel_g, \
+                                lds);                                                                          \
     }
 
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
+
+// Obstacle and neighbour selection (MPC_dist.cpp:371-396, generalised to K): one wave per
+// agent, the K_obs nearest static obstacles and the K_nbr nearest other agents to the
+// agent's own CoM, indices to sel_out[agent][K_obs + K_nbr] (-1: none).  A kernel of its own
+// rather than a phase of the solve: there the scan ran at the solve kernel's occupancy, one
+// or two waves per CU, and took a quarter of the solve (profiles/r01_c3_stamps.txt).
+extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(int n_agents,
+                const double *__restrict__ x0g, const double *__restrict__ obstacles, int n_obs,
+                const double *__restrict__ nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
+                int *__restrict__ sel_out)
+{
+    __shared__ double wd_lds[SRB_KNN_WAVES];
+    __shared__ int wi_lds[SRB_KNN_WAVES];
+    const int agent = blockIdx.x, tid = threadIdx.x;
+    if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
+    const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
+    int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);
+    if (K_obs > 0) knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, sel, wd_lds, wi_lds);
+    if (K_nbr > 0)
+        knn_select<SRB_KNN_WAVES>(tid, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, sel + K_obs, wd_lds,
+                                  wi_lds);
+}

@@ -169,3 +169,107 @@ __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int
     return fail;
 }
 
+// --------------------------------------------------------------------------- kNN
+// (d, index) lexicographic wave argmin; every lane gets the winner
+__device__ __forceinline__ void lexmin(double &d, int &idx, double od, int oi)
+{
+    if (od < d || (od == d && oi < idx)) { d = od; idx = oi; }
+}
+__device__ __forceinline__ void wargmin(double &d, int &idx)
+{
+    // the wsum pattern (DPP within 16-lane rows, permlane swaps across them) on the pair
+#define SRB_ARG_DPP(CTRL) lexmin(d, idx, dpp_d<CTRL>(d), __builtin_amdgcn_update_dpp(0, idx, CTRL, 0xf, 0xf, false))
+    SRB_ARG_DPP(0xB1); SRB_ARG_DPP(0x4E); SRB_ARG_DPP(0x141); SRB_ARG_DPP(0x140);
+#undef SRB_ARG_DPP
+    double a, b;
+    swap_d<16>(d, a, b);
+    auto i16 = __builtin_amdgcn_permlane16_swap((unsigned)idx, (unsigned)idx, false, false);
+    d = a; idx = (int)i16[0]; lexmin(d, idx, b, (int)i16[1]);
+    swap_d<32>(d, a, b);
+    auto i32 = __builtin_amdgcn_permlane32_swap((unsigned)idx, (unsigned)idx, false, false);
+    d = a; idx = (int)i32[0]; lexmin(d, idx, b, (int)i32[1]);
+}
+
+// K nearest rows of a table (row i at tab[stride*i], x at +0, y at +1) to (px, py),
+// ascending in (d^2, index) -- the order of the reference's strict-'<' scan
+// (MPC_dist.cpp:373-382) -- excluding row `self`; indices to sel[0..K).  KW waves (one
+// workgroup) scan the table once: lane l of wave w visits rows l + 64 (w + KW t) in
+// increasing index and keeps a sorted top-K of them (a strict '<' keeps the lower index on
+// ties); then K rounds pop the global order: a wave argmin over the lane heads, the KW wave
+// winners through LDS (wd_lds, wi_lds: KW entries each), the owning lane drops its head.
+template <int KW, int KM>
+__device__ __forceinline__ void knn_select_k(int tid, double px, double py, const double *__restrict__ tab,
+                                           int stride, int n_rows, int self, int K, int *sel,
+                                           double *wd_lds, int *wi_lds)
+{
+    const int lane = tid & 63, wv = tid >> 6;
+    double bd[KM]; int bi[KM];
+#pragma unroll
+    for (int j = 0; j < KM; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
+    double wd = 1e300;
+    // KNN_U rows per lane per batch: all their loads are issued before the first is used
+    constexpr int KNN_U = 4, STEP = 64 * KW;
+    for (int i0 = tid; i0 < n_rows; i0 += KNN_U * STEP) {
+        double tx[KNN_U], ty[KNN_U];
+#pragma unroll
+        for (int u = 0; u < KNN_U; u++) {
+            const int i = i0 + u * STEP;
+            const bool in = i < n_rows;
+            tx[u] = in ? tab[(size_t)stride * i] : 0.0;
+            ty[u] = in ? tab[(size_t)stride * i + 1] : 0.0;
+        }
+#pragma unroll
+        for (int u = 0; u < KNN_U; u++) {
+            const int i = i0 + u * STEP;
+            const double dx = tx[u] - px, dy = ty[u] - py;
+            const double d = dx * dx + dy * dy;
+            if (i >= n_rows || i == self || !(d < wd)) continue;
+            double cd = d; int ci = i;
+#pragma unroll
+            for (int j = 0; j < KM; j++) {
+                const bool lt = (j < K) && (cd < bd[j]);
+                const double td = bd[j]; const int ti = bi[j];
+                bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
+                cd = lt ? td : cd; ci = lt ? ti : ci;
+            }
+#pragma unroll
+            for (int j = 0; j < KM; j++)
+                if (j == K - 1) wd = bd[j];
+        }
+    }
+    // round j's winner is kept by lane j and stored after the last round: a store inside the
+    // loop would make every barrier wait for it (s_waitcnt vmcnt(0) before s_barrier)
+    int mine = -1;
+#pragma clang loop unroll(disable)
+    for (int j = 0; j < K; j++) {
+        double d = bd[0]; int idx = bi[0];
+        wargmin(d, idx);
+        if (KW > 1) {
+            if (lane == 0) { wd_lds[wv] = d; wi_lds[wv] = idx; }
+            __syncthreads();
+#pragma unroll
+            for (int w = 0; w < KW; w++) {
+                const double od = wd_lds[w]; const int oi = wi_lds[w];
+                if (od < d || (od == d && oi < idx)) { d = od; idx = oi; }
+            }
+            __syncthreads();                       // every wave has read the winners
+        }
+        if (bi[0] == idx) {
+#pragma unroll
+            for (int t = 0; t + 1 < KM; t++) { bd[t] = bd[t + 1]; bi[t] = bi[t + 1]; }
+            bd[KM - 1] = 1e300; bi[KM - 1] = 0x7fffffff;
+        }
+        if (tid == j) mine = (idx == 0x7fffffff) ? -1 : idx;
+    }
+    if (tid < K) sel[tid] = mine;
+}
+// the insertion network as deep as K needs (K <= KM): 4, 8 or SRB_KNN_MAX entries
+template <int KW>
+__device__ __forceinline__ void knn_select(int tid, double px, double py, const double *__restrict__ tab,
+                                           int stride, int n_rows, int self, int K, int *sel,
+                                           double *wd_lds, int *wi_lds)
+{
+    if (K <= 4) knn_select_k<KW, 4>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
+    else if (K <= 8) knn_select_k<KW, 8>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
+    else knn_select_k<KW, SRB_KNN_MAX>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
+}

@@ -32,5 +32,7 @@ for stage, nit in ((0, it[0]), (1, it[1])):
     per = blk[3:15].sum() / max(nit, 1)
     print(f"{'QP' if stage == 0 else 'NLP'}: total {blk.sum():.0f} cyc, per iteration {per:.0f}")
     for i, nm in names.items():
+        if stage == 1 and i == 6:
+            nm = 'kNN selection'
         if blk[i] > 0:
             print(f"   {nm:18s} {blk[i]:10.0f} cyc  {blk[i] / max(nit, 1) if 3 <= i <= 14 else 0:8.0f} /iter  {100 * blk[i] / tot_all:5.1f}%")
