@@ -35,6 +35,7 @@ ap.add_argument("--agents", type=int, default=1024)
 ap.add_argument("--cycles", type=int, default=20)
 ap.add_argument("--loop", type=int, default=4000, help="HL planner steps (reference: 100000)")
 ap.add_argument("--horizon", type=int, default=4, help="MPC grids (reference: 4 = one gait domain)")
+ap.add_argument("--dump", default="", help="save the last MPC cycle's solve inputs and outputs (npz)")
 args = ap.parse_args()
 A, N, C = args.agents, args.horizon, 2
 dev = torch.device("cuda:0")
@@ -123,5 +124,12 @@ line = {"bench": "control_stack", "robots": A, "horizon": N, "K_obs": 3, "K_nbr"
         "realtime_fraction": res["mpc_cycle_ms"] / 43.0 + res["ll_tick_ms"] / 1.0,
         "mpc_prepare_ok": float((prep["status"].cpu().numpy() == 0).mean()),
         "mpc_optimal_frac": float((st == 0).all(1).mean()),
+        "mpc_qp_status_counts": np.bincount(st[:, 0], minlength=5).tolist(),
+        "mpc_nlp_status_counts": np.bincount(st[:, 1], minlength=5).tolist(),
+        "mpc_nlp_iters_mean": float(sol["iters"][:, 1].float().mean().item()),
         "ll_optimal_frac": float((lout["status"].cpu().numpy() == 0).mean())}
 print(json.dumps(line), flush=True)
+if args.dump:
+    np.savez(args.dump, x0=prep["x0"].cpu().numpy(), ref=prep["ref"].cpu().numpy(), foot=prep["foot"].cpu().numpy(),
+             obstacles=obst, nbr_state=prep["last_state"].cpu().numpy(), x=sol["x"].cpu().numpy(), status=st,
+             iters=sol["iters"].cpu().numpy(), N=N, C=C)
