@@ -35,6 +35,8 @@ ap.add_argument("--agents", type=int, default=1024)
 ap.add_argument("--cycles", type=int, default=20)
 ap.add_argument("--loop", type=int, default=4000, help="HL planner steps (reference: 100000)")
 ap.add_argument("--horizon", type=int, default=4, help="MPC grids (reference: 4 = one gait domain)")
+ap.add_argument("--planned-velocity", action="store_true",
+                help="robots start at the planner's velocity instead of at rest (as A1_Sim starts them)")
 ap.add_argument("--dump", default="", help="save the last MPC cycle's solve inputs and outputs (npz)")
 args = ap.parse_args()
 A, N, C = args.agents, args.horizon, 2
@@ -67,7 +69,8 @@ contact = tt(np.array([[1, 0, 0, 1] if a % 2 else [0, 1, 1, 0] for a in range(A)
 col = 4 * gdh
 q = np.zeros((A, 18)); dq = np.zeros((A, 18))
 q[:, 0] = Pr[2 * np.arange(A), col]; q[:, 1] = Pr[2 * np.arange(A) + 1, col]
-dq[:, 0] = Prd[2 * np.arange(A), col]; dq[:, 1] = Prd[2 * np.arange(A) + 1, col]
+if args.planned_velocity:
+    dq[:, 0] = Prd[2 * np.arange(A), col]; dq[:, 1] = Prd[2 * np.arange(A) + 1, col]
 toe = np.zeros((A, 3, 4))
 for i, off in enumerate([(0.2188, -0.132), (0.2188, 0.132), (-0.1472, -0.132), (-0.1472, 0.132)]):
     toe[:, 0, i] = q[:, 0] + off[0]; toe[:, 1, i] = q[:, 1] + off[1]
