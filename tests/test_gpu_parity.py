@@ -205,14 +205,18 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
         assert cert["stat_rel"] < 1e-5 and cert["prim"] < 1e-6, (int(a), cert)
 
 
-def test_knn_matches_bruteforce():
-    """Inter-agent neighbour selection == (d^2, index) order of the reference's argmin scan."""
-    N, C, Ko, Kn, A = 10, 2, 0, 8, 512
+@pytest.mark.parametrize("Ko,Kn", [(0, 8), (3, 0), (2, 12)])
+def test_knn_matches_bruteforce(Ko, Kn):
+    """Obstacle / neighbour selection (srb_knn_kernel; its insertion network is 4, 8 or 16 deep
+    by K) == (d^2, index) order of the reference's argmin scan, ties included."""
+    N, C, A = 10, 2, 512
     b = workload.make_batch(A, N, C, seed=3)
     nb = b["nbr_state"].copy()
     nb[10:20, :2] = nb[5, :2]                     # exact distance ties: lower index first
-    out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], nb)
-    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], b["obstacles"],
+    ob = b["obstacles"].copy()
+    ob[10:20] = ob[5]
+    out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], ob, nb)
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], ob,
                            nb, nthreads=8)
     np.testing.assert_array_equal(out["status"], r["status"])
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
