@@ -9,8 +9,9 @@ all-gather of the neighbour snapshot over RCCL) + kNN + QP stage + NLP stage + B
 agents sharded agent-major, weak scaling (fixed agents per GPU).  Rank 0 prints one JSON
 line.  Configs (BASELINE.json "configs"):
     1  1 agent, N=4 reference mode (KAT-2 shape)            -- CPU plumbing case
-    2  64 agents/GPU, N=10, trot, 3 static obstacles        -- default (configs[1])
-    3  1024 agents/GPU, N=10, 3 static + 8 nearest agents   -- configs[2]
+    2  64 agents/GPU, N=10, trot, 3 static obstacles        -- configs[1]
+    3  1024 agents/GPU, N=10, 3 static + 8 nearest agents   -- configs[2], the default (the
+                                                               largest single-GPU config)
     4  1024 agents/GPU, as 3 with the RCCL all-gather       -- configs[3] (8 GPUs = 8192)
     5  2048 agents/GPU, N=20, 3 static + 8 nearest agents   -- configs[4] shape, fp64
 
@@ -38,6 +39,8 @@ from srbnmpc import dist as sdist, workload  # noqa: E402
 
 METRIC = "NMPC solves/sec (whole node) + p99 solve latency, N-agent batch horizon=10"
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 (vector and matrix) dense peak, spec
+SCLK_GHZ = 2.4               # MI355X peak engine clock (MI355X_MICROARCH.md)
+CALIBRATION = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 CONFIGS = {
     1: dict(agents=1, N=4, C=4, K_obs=1, K_nbr=0, name="1 agent, N=4, stand (reference mode, KAT-2 shape)"),
     2: dict(agents=64, N=10, C=2, K_obs=3, K_nbr=0, name="64 agents/GPU, horizon 10, trot, 3 static CBF obstacles, fp64"),
@@ -77,12 +80,24 @@ def io_bytes(p, n_agents, n_obs, n_all):
     return n_agents * per + 16 * n_obs + 32 * n_all
 
 
+def host_threads():
+    """Host threads this job may use: the box's CPU share (OMP_NUM_THREADS, 16 on the GPU
+    boxes; os.cpu_count() there reports the whole machine), else every core here."""
+    env = os.environ.get("OMP_NUM_THREADS")
+    if env and env.isdigit() and int(env) > 0:
+        return int(env)
+    return max(1, os.cpu_count() or 1)
+
+
 def cpu_baseline(cfg, b, budget_s):
     """Oracle (CPU restatement of the same algorithm, oracle/) timed on this host's cores
-    on a bounded sample of the same workload."""
+    on a bounded sample of the same workload, with its calibration against the genuine
+    vendored iSWIFT (tools/calibrate_cpu.py -> profiles/r02_cpu_calibration.json): the
+    reference's own QP solver on the same QP-stage instances, single thread, so that the
+    oracle's dense-LU rate can be read against the reference's sparse-LDL' rate."""
     sys.path.insert(0, ROOT)
     import oracle
-    nthreads = max(1, min(16, os.cpu_count() or 1))
+    nthreads = host_threads()
     p = oracle.params(cfg["N"], cfg["C"], K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"])
     A = b["x0"].shape[0]
     sample = min(A, max(nthreads * 2, 16))
@@ -94,9 +109,20 @@ def cpu_baseline(cfg, b, budget_s):
         if time.perf_counter() - t0 > budget_s:
             break
     dt = time.perf_counter() - t0
-    return {"value": solved / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
+    line = {"value": solved / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
             "sample": f"{solved} solves ({sample}-agent slices of the same batch) in {dt:.1f} s, QP+NLP, "
                       f"{nthreads} threads"}
+    try:
+        cal = json.load(open(CALIBRATION))
+        key = f"N{cfg['N']}_C{cfg['C']}"
+        if key in cal.get("cases", {}):
+            c = cal["cases"][key]
+            line["iswift_ratio"] = c["oracle_over_iswift"]
+            line["iswift_calibration"] = (f"QP stage on {c['instances']} instances, 1 thread: oracle {c['oracle_us']:.0f} us, "
+                                          f"genuine iSWIFT {c['iswift_us']:.0f} us per solve ({CALIBRATION[len(ROOT) + 1:]})")
+    except (OSError, ValueError, KeyError):
+        pass
+    return line
 
 
 LL_METRIC = "low-level CLF-QP controller solves/sec (LowLevelCtrl::calcTorque, batched)"
@@ -191,7 +217,7 @@ def main_ll(args, world, rank, local_rank, dev):
         sys.path.insert(0, ROOT)
         import oracle
         p = oracle.ll_params()
-        nthreads = max(1, min(16, os.cpu_count() or 1))
+        nthreads = host_threads()
         sample = {k: v[:512] for k, v in full.items()}
         t1 = time.perf_counter(); n = 0
         while time.perf_counter() - t1 < args.cpu_seconds:
@@ -212,11 +238,12 @@ def main():
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
-    ap.add_argument("--config", type=int, default=2)
+    ap.add_argument("--config", type=int, default=3)
     ap.add_argument("--agents", type=int, default=0, help="agents per GPU (override)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
-    ap.add_argument("--traffic-json", default=os.path.join(ROOT, "profiles", "r01_pmc_traffic.json"))
+    ap.add_argument("--traffic-json", default=None,
+                    help="PMC summary (tools/pmc_traffic.py); default profiles/r02_pmc_traffic_c<config>.json")
     args = ap.parse_args()
 
     world = int(os.environ.get("WORLD_SIZE", "1"))
@@ -261,10 +288,11 @@ def main():
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
-    exchange = cfg["K_nbr"] > 0 and world > 1
+    exchange = sdist.NeighbourExchange(A_total, world, rank, dev) if cfg["K_nbr"] > 0 and world > 1 else None
+    out["sel"] = torch.zeros((n_loc, cfg["K_obs"] + cfg["K_nbr"]), dtype=torch.int32, device=dev)
 
     def step():
-        nb = sdist.gather_states(nbr_local, A_total, world) if exchange else nbr_all
+        nb = exchange(nbr_local) if exchange is not None else nbr_all
         solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nb, out, agent_offset=lo,
                             stream=stream.cuda_stream, alpha_buf=alpha_buf)
 
@@ -305,7 +333,10 @@ def main():
     flops = executed_flops(p, iters, cfg["K_obs"] + cfg["K_nbr"])
     achieved = flops / (solve_ms * 1e-3) / 1e12
     dense_eq = dense_equiv_flops(p, iters) / (solve_ms * 1e-3) / 1e12
+    cyc_iter = solve_ms * 1e-3 * SCLK_GHZ * 1e9 / max(1, int(iters.sum(1).max()))
     traffic = None
+    if args.traffic_json is None:
+        args.traffic_json = os.path.join(ROOT, "profiles", f"r02_pmc_traffic_c{args.config}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -323,11 +354,16 @@ def main():
         "optimal_frac": float((status == 0).all(1).mean()),
         "acceptable_frac": float(((status[:, 0] == 0) & (status[:, 1] == 4)).mean()),
         "iters_mean": [float(iters[:, 0].mean()), float(iters[:, 1].mean())],
-        "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
+        "roofline": {"bound": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "cycles_per_iter": cyc_iter,
+                     "cycles_per_iter_note": "solve-kernel HIP-event time x 2.4 GHz / IPM iterations (QP + NLP) of "
+                                             "the slowest agent: the critical-path cost of one iteration; per-phase "
+                                             "split in profiles/r02_*_stamps.txt",
                      "kernel": "srb_nmpc_kernel", "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
-                     "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6); "
-                                   "the kernel is latency-bound (one wave per agent)",
+                     "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
+                                   "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
+                                   "agent), neither MFMA- nor HBM-throughput-bound",
                      "dense_equivalent_tflops": dense_eq,
                      "io_bytes_per_launch": io_bytes(p, n_loc, sh["obstacles"].shape[0], A_total if cfg["K_nbr"] else 0)},
         "cpu_baseline": None,

@@ -82,6 +82,15 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *   alpha_buf [A][4]        mpc_state_alpha_buffer_ (the previous solve's X_3; the start
  *                           position with zero velocity before the first one, :792, :798)
  *   alpha     [A][20]       get_alphaCOM(): 4 x 5 row-major (state row, Bernstein index)
+ * Selected obstacle rows (the closest-obstacle scan, MPC_dist.cpp:371-382), optional:
+ *   sel       [A][Ko + Kn] int  out: the Ko = min(K_obs, n_obs) static obstacle indices, then the
+ *                           Kn = min(K_nbr, n_all - 1) neighbour rows (global indices into
+ *                           nbr_state; -1 = none), in the reference's scan order (sqrt distance,
+ *                           lower index on ties; a static round with nothing closer than 1000 m
+ *                           selects obstacle 0, as min_dist = 1000 / min_i = 0 do).  NULL = the
+ *                           context's own scratch buffer, which makes the context usable from
+ *                           one stream at a time; with a caller buffer per stream, calls on
+ *                           different streams share nothing but read-only constants.
  */
 typedef struct srb_batch {
     const double *x0, *ref, *foot, *obstacles, *nbr_state;
@@ -90,6 +99,7 @@ typedef struct srb_batch {
     int *status, *iters;
     const double *alpha_buf;
     double *alpha;
+    int *sel;
 } srb_batch;
 
 typedef struct srb_ctx srb_ctx;
@@ -105,7 +115,10 @@ int srb_solve_batch(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 
 /* Device buffers (all pointers in `dev_io` are device pointers), asynchronous on
- * `stream` (a hipStream_t; NULL = the context's own stream).  Call srb_sync(). */
+ * `stream` (a hipStream_t).  NULL = the context's own stream, which is NOT ordered against
+ * any other stream: the caller must then make the inputs visible (and the outputs free)
+ * before the call, e.g. by a device synchronisation.  Pass the stream that produced the
+ * inputs instead (the Python layer passes torch's current stream).  Call srb_sync(). */
 int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
 int srb_sync(srb_ctx *ctx);
 

@@ -165,6 +165,19 @@ def select_obstacles(p: OrcParams, x0, obstacles, nbr_state=None, self_idx=-1):
     return obs[:, :K], eps[:K]
 
 
+def select_idx(p: OrcParams, x0, obstacles, nbr_state=None, self_idx=-1):
+    """Selected rows (K_obs static obstacle indices, then K_nbr agent indices, -1: none)
+    in the reference's order (MPC_dist.cpp:371-382: sqrt distance, first index on ties,
+    min_dist = 1000 sentinel with default index 0 for static obstacles)."""
+    K = p.K_obs + p.K_nbr
+    idx = np.zeros(max(K, 1), np.int32)
+    ob = _c(obstacles).reshape(-1, 2)
+    nb = _c(nbr_state if nbr_state is not None else np.zeros((0, 4))).reshape(-1, 4)
+    lib().orc_select_idx(ctypes.byref(p), _ptr(_c(x0)), _ptr(ob), ob.shape[0], _ptr(nb), nb.shape[0], self_idx,
+                         _ptr(idx))
+    return idx[:K]
+
+
 def nlp_solve(p: OrcParams, x0, foot, Pd, c, A, b, G, h, obs, eps, x_init):
     n = Pd.size
     x = np.zeros(n); it = ctypes.c_int()

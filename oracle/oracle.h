@@ -69,6 +69,8 @@ void orc_build_qp(const orc_params *p, const double x0[4], const double *ref, co
  * (the intent of the commented line MPC_dist.cpp:391).
  * obs_out[N][K][2], eps_out[K]; missing entries are parked far away (1e6).
  */
+void orc_select_idx(const orc_params *p, const double x0[4], const double *obstacles, int n_obs,
+                    const double *nbr_state, int n_all, int self_idx, int *idx);
 void orc_select_obstacles(const orc_params *p, const double x0[4],
                           const double *obstacles, int n_obs,
                           const double *nbr_state, int n_all, int self_idx,

@@ -128,50 +128,65 @@ void orc_build_qp(const orc_params *p, const double x0[4], const double *ref, co
     for (int j = 0; j < C * N; j++, r++) { G[(size_t)r * nv + oL + j] = 1.0; h[r] = 1.0; }   /*  lambda <= 1 */
 }
 
+/* Indices of the selected rows: idx[0..K_obs) static obstacles, idx[K_obs..K) agents.
+ *
+ * Static obstacles: MPC_dist.cpp:371-382 -- min_dist = 1000, min_i = 0, then a strict '<'
+ * scan over sqrt distances (the first index wins ties, including ties created by sqrt
+ * rounding).  Generalised to K_obs rounds over the not yet chosen rows; a round that finds
+ * no row closer than 1000 m keeps the reference's default index 0 (as the reference does
+ * when every obstacle is 1000 m or more away, or its distance is NaN).
+ * Neighbours (the reference reads one state_other, MPC_dist.cpp:385): the K_nbr nearest
+ * other agents by the same sqrt / first-index order, no distance cap; -1 when fewer finite
+ * rows exist. */
+void orc_select_idx(const orc_params *p, const double x0[4], const double *obstacles, int n_obs,
+                    const double *nbr_state, int n_all, int self_idx, int *idx)
+{
+    const double px = x0[0], py = x0[2];
+    for (int j = 0; j < p->K_obs; j++) {
+        double best = 1000.0; int bi = n_obs > 0 ? 0 : -1;
+        for (int i = 0; i < n_obs; i++) {
+            int used = 0;
+            for (int t = 0; t < j; t++) used |= (idx[t] == i);
+            if (used) continue;
+            double dx = px - obstacles[2 * i], dy = py - obstacles[2 * i + 1];
+            double d = sqrt(dx * dx + dy * dy);
+            if (d < best) { best = d; bi = i; }
+        }
+        idx[j] = bi;
+    }
+    for (int j = 0; j < p->K_nbr; j++) {
+        double best = DBL_MAX; int bi = -1;
+        for (int i = 0; i < n_all; i++) {
+            if (i == self_idx) continue;
+            int used = 0;
+            for (int t = 0; t < j; t++) used |= (idx[p->K_obs + t] == i);
+            if (used) continue;
+            double dx = px - nbr_state[4 * i], dy = py - nbr_state[4 * i + 1];
+            double d = sqrt(dx * dx + dy * dy);
+            if (d < best) { best = d; bi = i; }
+        }
+        idx[p->K_obs + j] = bi;
+    }
+}
+
+/* obstacle positions per grid (static: fixed; agents: constant-velocity prediction
+ * o_k = p + v Ts (k+1)) and their clearances; a row with no selection (-1) sits at 1e6 */
 void orc_select_obstacles(const orc_params *p, const double x0[4],
                           const double *obstacles, int n_obs,
                           const double *nbr_state, int n_all, int self_idx,
                           double *obs_out, double *eps_out)
 {
     const int N = p->N, K = p->K_obs + p->K_nbr;
-    const double px = x0[0], py = x0[2];
     int chosen[64];
-    /* static: repeated argmin with strict '<' (first index wins ties), MPC_dist.cpp:373-382 */
-    for (int j = 0; j < p->K_obs; j++) {
-        double best = DBL_MAX; int bi = -1;
-        for (int i = 0; i < n_obs; i++) {
-            int used = 0;
-            for (int t = 0; t < j; t++) used |= (chosen[t] == i);
-            if (used) continue;
-            double dx = px - obstacles[2 * i], dy = py - obstacles[2 * i + 1];
-            double d = sqrt(dx * dx + dy * dy);
-            if (d < best) { best = d; bi = i; }
-        }
-        chosen[j] = bi;
-        eps_out[j] = p->eps_obs;
+    orc_select_idx(p, x0, obstacles, n_obs, nbr_state, n_all, self_idx, chosen);
+    for (int j = 0; j < K; j++) {
+        const int st = j < p->K_obs, bi = chosen[j];
+        eps_out[j] = st ? p->eps_obs : p->eps_nbr;
         for (int k = 0; k < N; k++) {
-            obs_out[(k * K + j) * 2 + 0] = bi >= 0 ? obstacles[2 * bi] : 1e6;
-            obs_out[(k * K + j) * 2 + 1] = bi >= 0 ? obstacles[2 * bi + 1] : 1e6;
-        }
-    }
-    /* neighbours: nearest other agents by current position, constant-velocity prediction */
-    for (int j = 0; j < p->K_nbr; j++) {
-        double best = DBL_MAX; int bi = -1;
-        for (int i = 0; i < n_all; i++) {
-            if (i == self_idx) continue;
-            int used = 0;
-            for (int t = 0; t < j; t++) used |= (chosen[p->K_obs + t] == i);
-            if (used) continue;
-            double dx = px - nbr_state[4 * i], dy = py - nbr_state[4 * i + 1];
-            double d = sqrt(dx * dx + dy * dy);
-            if (d < best) { best = d; bi = i; }
-        }
-        chosen[p->K_obs + j] = bi;
-        eps_out[p->K_obs + j] = p->eps_nbr;
-        for (int k = 0; k < N; k++) {
-            double t = p->Ts * (k + 1);
-            obs_out[(k * K + p->K_obs + j) * 2 + 0] = bi >= 0 ? nbr_state[4 * bi] + nbr_state[4 * bi + 2] * t : 1e6;
-            obs_out[(k * K + p->K_obs + j) * 2 + 1] = bi >= 0 ? nbr_state[4 * bi + 1] + nbr_state[4 * bi + 3] * t : 1e6;
+            const double t = st ? 0.0 : p->Ts * (k + 1);
+            const double *row = st ? obstacles + 2 * (size_t)bi : nbr_state + 4 * (size_t)bi;
+            obs_out[(k * K + j) * 2 + 0] = bi >= 0 ? row[0] + (st ? 0.0 : row[2] * t) : 1e6;
+            obs_out[(k * K + j) * 2 + 1] = bi >= 0 ? row[1] + (st ? 0.0 : row[3] * t) : 1e6;
         }
     }
 }

@@ -9,6 +9,7 @@
 #include <cstdlib>
 #include <cstdio>
 #include <cstring>
+#include <algorithm>
 #include <string>
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
@@ -283,15 +284,16 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     c->timed = true;
     HIPCHK(hipEventRecord(c->ev[0], s));
     // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
+    int *sel = d->sel ? d->sel : c->sel;
     if (use_nlp && k.K_obs + k.K_nbr > 0) {
         hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, d->x0, d->obstacles, n_obs,
-                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, c->sel);
+                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, sel);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
-                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)c->sel);
+                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel);
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
@@ -436,8 +438,13 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
         HIPCHK(hipMemcpyAsync(c->nbr, h->nbr_state, (size_t)h->n_all * 4 * sizeof(double), hipMemcpyHostToDevice, s));
         d.nbr_state = c->nbr;
     }
+    d.sel = nullptr;                       // the context's scratch; copied out below when asked for
     int rc = launch(c, n_agents, &d, s, use_nlp);
     if (rc) return rc;
+    if (h->sel && use_nlp) {
+        const int Ko = std::min(p->K_obs, std::max(h->n_obs, 0)), Kn = h->nbr_state ? std::min(p->K_nbr, std::max(h->n_all - 1, 0)) : 0;
+        if (Ko + Kn > 0) HIPCHK(hipMemcpyAsync(h->sel, c->sel, A * (Ko + Kn) * sizeof(int), hipMemcpyDeviceToHost, s));
+    }
     if (h->x_qp) HIPCHK(hipMemcpyAsync(h->x_qp, c->x_qp, A * nv * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h->x, c->x, A * nv * sizeof(double), hipMemcpyDeviceToHost, s));
     HIPCHK(hipMemcpyAsync(h->obj, c->obj, A * sizeof(double), hipMemcpyDeviceToHost, s));

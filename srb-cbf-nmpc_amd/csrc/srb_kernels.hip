@@ -609,12 +609,13 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int j = 0; j < K; j++) {
                 const bool st = j < prm.K_obs;
                 const int bi = sel[j];
-                if (tid < N && bi >= 0) {
+                if (tid < N) {                                // no selection (-1): a row 1e6 m away, as the oracle
                     const int k = tid;
                     const double tt = st ? 0.0 : prm.Ts * (k + 1);
-                    const double *srcp = st ? obstacles + 2 * (size_t)bi : nbr_state + 4 * (size_t)bi;
-                    obs[2 * (k * K + j)] = srcp[0] + (st ? 0.0 : srcp[2] * tt);
-                    obs[2 * (k * K + j) + 1] = srcp[1] + (st ? 0.0 : srcp[3] * tt);
+                    const size_t bj = (bi >= 0) ? bi : 0;     // row 0 exists whenever K_obs / K_nbr > 0
+                    const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj;
+                    obs[2 * (k * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : 1e6;
+                    obs[2 * (k * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : 1e6;
                 }
                 if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr;
             }
@@ -989,9 +990,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
 
-// Obstacle and neighbour selection (MPC_dist.cpp:371-396, generalised to K): one wave per
-// agent, the K_obs nearest static obstacles and the K_nbr nearest other agents to the
-// agent's own CoM, indices to sel_out[agent][K_obs + K_nbr] (-1: none).  A kernel of its own
+// Obstacle and neighbour selection (MPC_dist.cpp:371-396, generalised to K): one workgroup per
+// agent, the K_obs nearest static obstacles (with the reference's 1000 m sentinel) and the
+// K_nbr nearest other agents to the agent's own CoM, indices to sel_out[agent][K_obs + K_nbr]
+// (-1: no neighbour row).  A kernel of its own
 // rather than a phase of the solve: there the scan ran at the solve kernel's occupancy, one
 // or two waves per CU, and took a quarter of the solve (profiles/r01_c3_stamps.txt).
 extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(int n_agents,
@@ -1005,8 +1007,8 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
     if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
     const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
     int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);
-    if (K_obs > 0) knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, sel, wd_lds, wi_lds);
+    if (K_obs > 0) knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds);
     if (K_nbr > 0)
-        knn_select<SRB_KNN_WAVES>(tid, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, sel + K_obs, wd_lds,
+        knn_select<SRB_KNN_WAVES>(tid, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, 0, sel + K_obs, wd_lds,
                                   wi_lds);
 }

@@ -191,22 +191,28 @@ __device__ __forceinline__ void wargmin(double &d, int &idx)
 }
 
 // K nearest rows of a table (row i at tab[stride*i], x at +0, y at +1) to (px, py),
-// ascending in (d^2, index) -- the order of the reference's strict-'<' scan
-// (MPC_dist.cpp:373-382) -- excluding row `self`; indices to sel[0..K).  KW waves (one
-// workgroup) scan the table once: lane l of wave w visits rows l + 64 (w + KW t) in
-// increasing index and keeps a sorted top-K of them (a strict '<' keeps the lower index on
+// ascending in (sqrt distance, index) -- the order of the reference's strict-'<' scan over
+// sqrt(pow(dx,2)+pow(dy,2)) (MPC_dist.cpp:373-382; two rows whose squared distances differ
+// but round to the same sqrt keep index order, as there) -- excluding row `self`; indices to
+// sel[0..K).  cap != 0 applies the reference's min_dist = 1000 / min_i = 0 start: a round
+// whose winner is not closer than 1000 m selects row 0.  NaN rows are never selected.
+// KW waves (one workgroup) scan the table once: lane l of wave w visits rows l + 64 (w + KW t)
+// in increasing index and keeps a sorted top-K of them (a strict '<' keeps the lower index on
 // ties); then K rounds pop the global order: a wave argmin over the lane heads, the KW wave
 // winners through LDS (wd_lds, wi_lds: KW entries each), the owning lane drops its head.
+// The sqrt is taken only for rows that can enter a lane's list: d^2 above its K-th entry's
+// squared key by more than a relative 1e-14 cannot round to a smaller or equal sqrt.
 template <int KW, int KM>
 __device__ __forceinline__ void knn_select_k(int tid, double px, double py, const double *__restrict__ tab,
-                                           int stride, int n_rows, int self, int K, int *sel,
+                                           int stride, int n_rows, int self, int K, int cap, int *sel,
                                            double *wd_lds, int *wi_lds)
 {
+#pragma clang fp contract(off)
     const int lane = tid & 63, wv = tid >> 6;
     double bd[KM]; int bi[KM];
 #pragma unroll
-    for (int j = 0; j < KM; j++) { bd[j] = 1e300; bi[j] = 0x7fffffff; }
-    double wd = 1e300;
+    for (int j = 0; j < KM; j++) { bd[j] = __builtin_inf(); bi[j] = 0x7fffffff; }
+    double wq = __builtin_inf();                   // filter bound on d^2 (K-th key squared, padded)
     // KNN_U rows per lane per batch: all their loads are issued before the first is used
     constexpr int KNN_U = 4, STEP = 64 * KW;
     for (int i0 = tid; i0 < n_rows; i0 += KNN_U * STEP) {
@@ -221,10 +227,10 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
 #pragma unroll
         for (int u = 0; u < KNN_U; u++) {
             const int i = i0 + u * STEP;
-            const double dx = tx[u] - px, dy = ty[u] - py;
-            const double d = dx * dx + dy * dy;
-            if (i >= n_rows || i == self || !(d < wd)) continue;
-            double cd = d; int ci = i;
+            const double dx = px - tx[u], dy = py - ty[u];
+            const double d2 = dx * dx + dy * dy;
+            if (i >= n_rows || i == self || !(d2 <= wq)) continue;
+            double cd = sqrt(d2); int ci = i;
 #pragma unroll
             for (int j = 0; j < KM; j++) {
                 const bool lt = (j < K) && (cd < bd[j]);
@@ -234,7 +240,7 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
             }
 #pragma unroll
             for (int j = 0; j < KM; j++)
-                if (j == K - 1) wd = bd[j];
+                if (j == K - 1) wq = bd[j] * bd[j] * (1.0 + 1e-14);
         }
     }
     // round j's winner is kept by lane j and stored after the last round: a store inside the
@@ -257,19 +263,19 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
         if (bi[0] == idx) {
 #pragma unroll
             for (int t = 0; t + 1 < KM; t++) { bd[t] = bd[t + 1]; bi[t] = bi[t + 1]; }
-            bd[KM - 1] = 1e300; bi[KM - 1] = 0x7fffffff;
+            bd[KM - 1] = __builtin_inf(); bi[KM - 1] = 0x7fffffff;
         }
-        if (tid == j) mine = (idx == 0x7fffffff) ? -1 : idx;
+        if (tid == j) mine = cap ? ((d < 1000.0) ? idx : 0) : ((idx == 0x7fffffff) ? -1 : idx);
     }
     if (tid < K) sel[tid] = mine;
 }
 // the insertion network as deep as K needs (K <= KM): 4, 8 or SRB_KNN_MAX entries
 template <int KW>
 __device__ __forceinline__ void knn_select(int tid, double px, double py, const double *__restrict__ tab,
-                                           int stride, int n_rows, int self, int K, int *sel,
+                                           int stride, int n_rows, int self, int K, int cap, int *sel,
                                            double *wd_lds, int *wi_lds)
 {
-    if (K <= 4) knn_select_k<KW, 4>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
-    else if (K <= 8) knn_select_k<KW, 8>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
-    else knn_select_k<KW, SRB_KNN_MAX>(tid, px, py, tab, stride, n_rows, self, K, sel, wd_lds, wi_lds);
+    if (K <= 4) knn_select_k<KW, 4>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
+    else if (K <= 8) knn_select_k<KW, 8>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
+    else knn_select_k<KW, SRB_KNN_MAX>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
 }

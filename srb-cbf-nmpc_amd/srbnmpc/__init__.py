@@ -49,7 +49,7 @@ class Batch(ctypes.Structure):
     _fields_ = [("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
                 ("n_obs", ctypes.c_int), ("n_all", ctypes.c_int), ("agent_offset", ctypes.c_int),
                 ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip),
-                ("alpha_buf", _dp), ("alpha", _dp)]
+                ("alpha_buf", _dp), ("alpha", _dp), ("sel", _ip)]
 
 
 class Prep(ctypes.Structure):
@@ -144,10 +144,17 @@ class BatchSolver:
             pass
 
     # --------------------------------------------------------------- host path
+    def n_selected(self, n_obs: int, n_all: int):
+        """(Ko, Kn): selected static obstacles / neighbours per agent for tables of these sizes
+        ("up to K nearest", the clamp the C ABI applies)."""
+        p = self.params
+        return min(p.K_obs, max(n_obs, 0)), (min(p.K_nbr, max(n_all - 1, 0)) if n_all > 0 else 0)
+
     def solve(self, x0, ref, foot, obstacles=None, nbr_state=None, agent_offset: int = 0, qp_only: bool = False,
               alpha_buf=None):
         """Host arrays in, dict of outputs back.  alpha_buf ([A][4], the Bezier buffer state)
-        additionally returns alpha ([A][4][5], get_alphaCOM) from the fused fit."""
+        additionally returns alpha ([A][4][5], get_alphaCOM) from the fused fit.  With the NLP
+        stage, sel ([A][Ko + Kn]) holds the selected obstacle / neighbour rows."""
         p = self.params
         x0 = _f64(x0).reshape(-1, 4)
         A = x0.shape[0]
@@ -161,10 +168,13 @@ class BatchSolver:
         if alpha_buf is not None:
             ab = _f64(alpha_buf).reshape(A, 4)
             out["alpha"] = np.zeros((A, 4, 5))
+        Ko, Kn = self.n_selected(ob.shape[0], nb.shape[0] if nb is not None else 0)
+        out["sel"] = np.full((A, Ko + Kn), -2, np.int32)
         b = Batch(_p(x0), _p(ref), _p(foot), _p(ob) if ob.size else None, _p(nb) if nb is not None else None,
                   ob.shape[0], nb.shape[0] if nb is not None else 0, int(agent_offset),
                   _p(out["x_qp"]), _p(out["x"]), _p(out["obj"]), _p(out["status"]), _p(out["iters"]),
-                  _p(ab) if ab is not None else None, _p(out["alpha"]) if ab is not None else None)
+                  _p(ab) if ab is not None else None, _p(out["alpha"]) if ab is not None else None,
+                  _p(out["sel"]) if out["sel"].size and not qp_only else None)
         fn = lib().srb_solve_qp if qp_only else lib().srb_solve_batch
         _check(fn(self._h, A, ctypes.byref(b)))
         return out
@@ -174,20 +184,36 @@ class BatchSolver:
                      alpha_buf=None):
         """All arguments torch tensors on this solver's device (float64 / int32), contiguous.
         `out` is a dict with x_qp (or None), x, obj, status, iters and, with alpha_buf [A][4],
-        alpha [A][20].  Asynchronous."""
+        alpha [A][20]; an optional int32 out["sel"] [A][Ko + Kn] receives the selected rows
+        (otherwise the context's scratch is used: one stream per context at a time).
+        Asynchronous on `stream` (a hipStream_t handle), by default torch's current stream on
+        this device, so the launch is ordered after the torch work that filled the inputs."""
         def dptr(t):
             return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
 
         def iptr(t):
             return ctypes.cast(ctypes.c_void_p(t.data_ptr()), _ip)
         A = x0.shape[0]
+        Ko, Kn = self.n_selected(0 if obstacles is None else obstacles.shape[0],
+                                 0 if nbr_state is None else nbr_state.shape[0])
+        sel = out.get("sel")
+        if sel is not None and (sel.dtype != torch_int32() or sel.numel() < A * (Ko + Kn) or not sel.is_contiguous()):
+            raise ValueError(f"out['sel'] must be a contiguous int32 tensor of at least {A} x {Ko + Kn}")
         b = Batch(dptr(x0), dptr(ref), dptr(foot), dptr(obstacles), dptr(nbr_state),
                   0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],
                   int(agent_offset), dptr(out.get("x_qp")), dptr(out["x"]), dptr(out["obj"]),
                   iptr(out["status"]), iptr(out["iters"]), dptr(alpha_buf),
-                  dptr(out.get("alpha") if alpha_buf is not None else None))
-        s = ctypes.c_void_p(stream) if stream is not None else None
-        _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), s))
+                  dptr(out.get("alpha") if alpha_buf is not None else None),
+                  iptr(out["sel"]) if out.get("sel") is not None else None)
+        _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), self._stream(stream)))
+
+    def _stream(self, stream):
+        """hipStream_t for a launch: the caller's, else torch's current stream on this device
+        (the C ABI's NULL would mean the context's own stream, unordered against torch's)."""
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        return ctypes.c_void_p(stream)
 
     def prepare_device(self, Pr, Prd, gait_domain, contact, toe, start, q, dq, out, agent_id=None,
                        agent_offset: int = 0, stream=None):
@@ -204,8 +230,7 @@ class BatchSolver:
         pr = Prep(dptr(Pr), dptr(Prd), Pr.shape[1], Pr.shape[0], int(agent_offset), iptr(agent_id),
                   iptr(gait_domain), iptr(contact), dptr(toe), dptr(start), dptr(q), dptr(dq),
                   dptr(out["x0"]), dptr(out["ref"]), dptr(out["foot"]), dptr(out["last_state"]), iptr(out["status"]))
-        s = ctypes.c_void_p(stream) if stream is not None else None
-        _check(lib().srb_prepare_batch_device(self._h, A, ctypes.byref(pr), s))
+        _check(lib().srb_prepare_batch_device(self._h, A, ctypes.byref(pr), self._stream(stream)))
 
     def sync(self):
         _check(lib().srb_sync(self._h))
@@ -214,6 +239,11 @@ class BatchSolver:
         a = ctypes.c_float(); b = ctypes.c_float()
         _check(lib().srb_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+
+def torch_int32():
+    import torch
+    return torch.int32
 
 
 def hl_plan(Pstart, Pobs, loop: int = 100000, device: int = 0):

@@ -20,15 +20,46 @@ def shard_range(n_total: int, world: int, rank: int):
     return lo, hi
 
 
+class NeighbourExchange:
+    """The per-cycle all-gather of the [n_local, 4] neighbour-state rows of every rank into
+    one [n_total, 4] table in global agent order, with every buffer allocated once: each
+    rank's rows go into a padded [cmax, 4] slot of one flat receive buffer
+    (all_gather_into_tensor: a single RCCL call, no per-step list or torch.cat).  With equal
+    shards (n_total % world == 0) the receive buffer IS the table; otherwise the padding is
+    squeezed out by one index_select into a preallocated table."""
+
+    def __init__(self, n_total: int, world: int, rank: int, device, dtype=None):
+        import torch as _t
+        dtype = dtype or _t.float64
+        self.n_total, self.world, self.rank = n_total, world, rank
+        self.counts = [shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0] for r in range(world)]
+        self.cmax = max(self.counts)
+        self.send = _t.zeros((self.cmax, 4), dtype=dtype, device=device)
+        self.recv = _t.zeros((world * self.cmax, 4), dtype=dtype, device=device)
+        self.equal = all(c == self.cmax for c in self.counts)
+        if not self.equal:
+            rows = [r * self.cmax + i for r in range(world) for i in range(self.counts[r])]
+            self.rows = _t.as_tensor(rows, dtype=_t.long, device=device)
+            self.table = _t.zeros((n_total, 4), dtype=dtype, device=device)
+        # gloo (CPU tests) has no all_gather_into_tensor on every torch build: list form there
+        self.flat = dist.is_initialized() and dist.get_backend() != "gloo"
+
+    def __call__(self, local_state: torch.Tensor) -> torch.Tensor:
+        if self.world == 1:
+            return local_state
+        self.send[:local_state.shape[0]].copy_(local_state)
+        if self.flat:
+            dist.all_gather_into_tensor(self.recv, self.send)
+        else:
+            dist.all_gather(list(self.recv.view(self.world, self.cmax, 4).unbind(0)), self.send)
+        if self.equal:
+            return self.recv
+        torch.index_select(self.recv, 0, self.rows, out=self.table)
+        return self.table
+
+
 def gather_states(local_state: torch.Tensor, n_total: int, world: int) -> torch.Tensor:
-    """All-gather the [n_local, 4] neighbour-state rows of every rank -> [n_total, 4]
-    (rank order == global agent order).  One collective per control cycle."""
+    """One-shot form of NeighbourExchange (allocates its buffers per call)."""
     if world == 1:
         return local_state
-    counts = [shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0] for r in range(world)]
-    cmax = max(counts)
-    buf = torch.zeros((cmax, 4), dtype=local_state.dtype, device=local_state.device)
-    buf[:local_state.shape[0]] = local_state
-    out = [torch.empty_like(buf) for _ in range(world)]
-    dist.all_gather(out, buf)
-    return torch.cat([o[:c] for o, c in zip(out, counts)], 0)
+    return NeighbourExchange(n_total, world, dist.get_rank(), local_state.device, local_state.dtype)(local_state)

@@ -85,6 +85,7 @@ class LowLevelCtrl:
     def __init__(self, params: LLParams | None = None, max_agents: int = 1, device: int = 0):
         self.params = params if params is not None else default_params()
         self.max_agents = int(max_agents)
+        self.device = int(device)
         h = ctypes.c_void_p()
         _check(_bind().srb_ll_ctx_create(ctypes.byref(self.params), self.max_agents, int(device), ctypes.byref(h)))
         self._h = h
@@ -128,7 +129,8 @@ class LowLevelCtrl:
         """torch CUDA tensors: dev holds ind (int32 [A,4]) and the IN_KEYS arrays (float64,
         contiguous, [A, IN_SIZE]); out holds tau (in/out), QP_force, ddq, dq, q, V, dV, x
         (float64) and status, iters (int32).  Asynchronous on `stream` (a raw hipStream_t
-        handle) or the context's stream."""
+        handle), by default torch's current stream on this device (ordered after the torch
+        work that filled the inputs)."""
         def dptr(t):
             return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
 
@@ -143,7 +145,10 @@ class LowLevelCtrl:
         ptrs["out_status"] = iptr(out["status"])
         ptrs["out_iters"] = iptr(out["iters"])
         io = _io_from(ptrs)
-        s = ctypes.c_void_p(stream) if stream is not None else None
+        if stream is None:
+            import torch
+            stream = torch.cuda.current_stream(self.device).cuda_stream
+        s = ctypes.c_void_p(stream)
         _check(lib().srb_ll_calc_torque_device(self._h, A, ctypes.byref(io), s))
 
     def sync(self):

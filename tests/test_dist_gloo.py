@@ -36,8 +36,14 @@ def _worker(rank, world, port, n_total, q):
         b = workload.make_batch(n_total, 10, 2, seed=42)
         lo, hi = sdist.shard_range(n_total, world, rank)
         local = torch.as_tensor(b["nbr_state"][lo:hi])
-        gathered = sdist.gather_states(local, n_total, world).numpy()
-        ok_table = bool(np.array_equal(gathered, b["nbr_state"]))
+        ex = sdist.NeighbourExchange(n_total, world, rank, torch.device("cpu"))
+        # the exchange object is reused every control cycle: a second cycle with moved agents
+        # must return the new table from the same buffers
+        moved = b["nbr_state"] + 0.5
+        first = ex(torch.as_tensor(moved[lo:hi])).clone().numpy()
+        gathered = ex(local).numpy().copy()
+        ok_table = bool(np.array_equal(gathered, b["nbr_state"])) and bool(np.array_equal(first, moved))
+        ok_table &= bool(np.array_equal(sdist.gather_states(local, n_total, world).numpy(), b["nbr_state"]))
         # neighbour choice of this shard from the gathered table == whole-batch choice
         p = oracle.params(10, 2, K_obs=2, K_nbr=4)
         ok_nbr = True
@@ -45,6 +51,8 @@ def _worker(rank, world, port, n_total, q):
             o1, _ = oracle.select_obstacles(p, b["x0"][a], b["obstacles"], gathered, a)
             o2, _ = oracle.select_obstacles(p, b["x0"][a], b["obstacles"], b["nbr_state"], a)
             ok_nbr &= bool(np.array_equal(o1, o2))
+            ok_nbr &= bool(np.array_equal(oracle.select_idx(p, b["x0"][a], b["obstacles"], gathered, a),
+                                          oracle.select_idx(p, b["x0"][a], b["obstacles"], b["nbr_state"], a)))
         # shard solve through the oracle with agent_offset == whole-batch rows
         r_local = oracle.solve_batch(p, b["x0"][lo:hi], b["ref"][lo:hi], b["foot"][lo:hi], b["obstacles"],
                                      gathered, agent_offset=lo)

@@ -205,21 +205,101 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
         assert cert["stat_rel"] < 1e-5 and cert["prim"] < 1e-6, (int(a), cert)
 
 
+def _oracle_sel(op, b, ob, nb, Ko, Kn, offset=0):
+    return np.array([oracle.select_idx(op, b["x0"][a], ob, nb, offset + a) for a in range(b["x0"].shape[0])],
+                    np.int32).reshape(-1, Ko + Kn)
+
+
 @pytest.mark.parametrize("Ko,Kn", [(0, 8), (3, 0), (2, 12)])
 def test_knn_matches_bruteforce(Ko, Kn):
     """Obstacle / neighbour selection (srb_knn_kernel; its insertion network is 4, 8 or 16 deep
-    by K) == (d^2, index) order of the reference's argmin scan, ties included."""
+    by K): the selected indices == the reference's scan order (MPC_dist.cpp:371-382: sqrt
+    distance, lower index on ties) for every agent, ties included -- exact ties at different
+    positions (so the choice changes the constraint) and sqrt-rounding ties."""
+    from test_oracle import sqrt_tie_pair
     N, C, A = 10, 2, 512
     b = workload.make_batch(A, N, C, seed=3)
+    rng = np.random.default_rng(8)
     nb = b["nbr_state"].copy()
-    nb[10:20, :2] = nb[5, :2]                     # exact distance ties: lower index first
     ob = b["obstacles"].copy()
-    ob[10:20] = ob[5]
+    # agents 0..7 at exact coordinates with exact-distance ties at mirrored positions
+    for a in range(8):
+        px, py = 2.0 + a, 1.0 - 0.25 * a
+        b["x0"][a, [0, 2]] = (px, py); nb[a, :2] = (px, py)
+        ob[20 + 2 * a] = (px + 0.75, py + 0.5); ob[21 + 2 * a] = (px - 0.75, py - 0.5)
+        nb[100 + 2 * a, :2] = (px - 0.5, py + 0.75); nb[101 + 2 * a, :2] = (px + 0.5, py - 0.75)
+    # agents 8..11: sqrt-rounding ties (larger d^2 at the lower index)
+    for a in range(8, 12):
+        px, py = b["x0"][a, 0], b["x0"][a, 2]
+        near, far = sqrt_tie_pair(px, py, rng)
+        ob[40 + 2 * a] = far; ob[41 + 2 * a] = near
+        near, far = sqrt_tie_pair(px, py, rng)
+        nb[130 + 2 * a, :2] = far; nb[131 + 2 * a, :2] = near
     out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], ob, nb)
-    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], ob,
-                           nb, nthreads=8)
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    np.testing.assert_array_equal(out["sel"], _oracle_sel(op, b, ob, nb, Ko, Kn))
+    r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], ob, nb, nthreads=8)
     np.testing.assert_array_equal(out["status"], r["status"])
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+
+
+def test_knn_sentinel_and_missing_rows():
+    """The reference's min_dist = 1000 / min_i = 0 start (MPC_dist.cpp:371-372): with no
+    static obstacle closer than 1000 m every static round selects obstacle 0; a neighbour
+    table with fewer finite rows than K_nbr leaves -1 slots, whose rows sit 1e6 m away (as in
+    the oracle), and the solve does not read unwritten LDS."""
+    N, C, A, Ko, Kn = 10, 2, 32, 2, 4
+    b = workload.make_batch(A, N, C, seed=12)
+    ob = np.array([[2500.0, 0.0], [0.0, -1200.0], [1001.0, 1001.0]])
+    nb = b["nbr_state"].copy()
+    nb[3:, :2] = np.nan                                       # only agents 0..2 are finite
+    nb[:3] = b["nbr_state"][:3]
+    out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], ob, nb)
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    want = _oracle_sel(op, b, ob, nb, Ko, Kn)
+    np.testing.assert_array_equal(out["sel"], want)
+    assert (out["sel"][:, :Ko] == 0).all() and (out["sel"][3:, Ko + 2:] == -1).all()
+    r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], ob, nb, nthreads=8)
+    np.testing.assert_array_equal(out["status"], r["status"])
+    np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("shards", [2, 8])
+def test_sharded_solve_matches_full_batch(shards):
+    """The multi-GPU data path on one GPU: each shard is what one rank solves after the
+    all-gather (srbnmpc.dist): its contiguous agent block with agent_offset = lo and the FULL
+    neighbour table (MPC_dist.cpp:1272-1276 rows of every agent).  Statuses, x and the
+    selected rows are bit-identical to the single-batch solve, which matches the oracle."""
+    from srbnmpc import dist as sdist
+    N, C, A, Ko, Kn = 10, 2, 1024, 3, 8
+    b = workload.make_batch(A, N, C, seed=77)
+    s = solver(N, C, Ko, Kn)
+    full = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    dev = torch.device("cuda:0")
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    nbr = T(b["nbr_state"]); obst = T(b["obstacles"])
+    parts = []
+    for r in range(shards):
+        lo, hi = sdist.shard_range(A, shards, r)
+        n = hi - lo
+        o = dict(x_qp=None, x=torch.zeros((n, s.params.nv), dtype=torch.float64, device=dev),
+                 obj=torch.zeros(n, dtype=torch.float64, device=dev),
+                 status=torch.zeros((n, 2), dtype=torch.int32, device=dev),
+                 iters=torch.zeros((n, 2), dtype=torch.int32, device=dev),
+                 sel=torch.full((n, Ko + Kn), -2, dtype=torch.int32, device=dev))
+        s.solve_device(T(b["x0"][lo:hi]), T(b["ref"][lo:hi]), T(b["foot"][lo:hi].reshape(n, -1)), obst, nbr, o,
+                       agent_offset=lo)
+        parts.append(o)
+    torch.cuda.synchronize()
+    cat = {k: np.concatenate([o[k].cpu().numpy() for o in parts]) for k in ("x", "obj", "status", "iters", "sel")}
+    for k in cat:
+        np.testing.assert_array_equal(cat[k], full[k], err_msg=k)
+    # the shard rows exclude their own global index from the neighbours
+    assert not np.any(cat["sel"][:, Ko:] == np.arange(A)[:, None])
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], b["obstacles"],
+                           b["nbr_state"], nthreads=16)
+    np.testing.assert_array_equal(cat["status"], r["status"])
+    np.testing.assert_allclose(xus(N, cat["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
 def test_qp_only_equals_qp_stage():
@@ -243,8 +323,9 @@ def test_device_api_matches_host():
                obj=torch.zeros(A, dtype=torch.float64, device=dev),
                status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
                iters=torch.zeros((A, 2), dtype=torch.int32, device=dev))
-    s.solve_device(t["x0"], t["ref"], t["foot"].reshape(A, -1), t["obstacles"], t["nbr_state"], out)
-    s.sync()
+    s.solve_device(t["x0"], t["ref"], t["foot"].reshape(A, -1), t["obstacles"], t["nbr_state"], out,
+                   stream=torch.cuda.current_stream(dev).cuda_stream)
+    torch.cuda.current_stream(dev).synchronize()
     np.testing.assert_array_equal(out["x"].cpu().numpy(), host["x"])
     np.testing.assert_array_equal(out["status"].cpu().numpy(), host["status"])
 

@@ -143,6 +143,49 @@ def test_select_obstacles_matches_bruteforce():
         assert np.all(eps[:3] == p.eps_obs) and np.all(eps[3:] == p.eps_nbr)
 
 
+def sqrt_tie_pair(px, py, rng):
+    """Two points whose squared distances to (px, py) differ (d2a < d2b) but whose sqrt
+    distances round to the same double: the reference's sqrt scan (MPC_dist.cpp:376) sees a
+    tie there and keeps the lower index, a d^2 order would not."""
+    while True:
+        ax, ay = px + rng.uniform(1, 3), py + rng.uniform(1, 3)
+        da = (px - ax) ** 2 + (py - ay) ** 2
+        by = ay
+        for _ in range(64):
+            by = np.nextafter(by, np.inf)
+            db = (px - ax) ** 2 + (py - by) ** 2
+            if db > da:
+                if np.sqrt(db) == np.sqrt(da):
+                    return (ax, ay), (ax, by)
+                break
+
+
+def test_select_idx_reference_semantics():
+    """MPC_dist.cpp:371-382: min_dist = 1000 / min_i = 0 start, strict '<' on sqrt distances."""
+    rng = np.random.default_rng(11)
+    p = oracle.params(10, 2, K_obs=2, K_nbr=2)
+    x0 = np.array([3.0, 0.1, 1.0, -0.1])
+    # every obstacle 1000 m or more away: the reference keeps index 0 in every round
+    far = np.array([[1500.0, 0.0], [3.0, 1001.5], [-998.0, 1.0]])
+    nbr = np.array([[3.5, 1.0, 0, 0], [900.0, 1.0, 0, 0], [3.0, 1.0, 0, 0]])
+    idx = oracle.select_idx(p, x0, far, nbr, 2)
+    assert idx.tolist() == [0, 0, 0, 1]            # neighbours: no distance cap
+    # one obstacle within 1000 m: it first, then the sentinel
+    near = np.r_[far, [[4.0, 1.0]]]
+    assert oracle.select_idx(p, x0, near, nbr, 2).tolist()[:2] == [3, 0]
+    # sqrt-rounding tie: the farther point (larger d^2) has the lower index and wins
+    a, b = sqrt_tie_pair(x0[0], x0[2], rng)
+    tie = np.array([b, a, [50.0, 50.0]])
+    assert oracle.select_idx(p, x0, tie, nbr, 2).tolist()[:2] == [0, 1]
+    tie2 = np.array([a, b, [50.0, 50.0]])
+    assert oracle.select_idx(p, x0, tie2, nbr, 2).tolist()[:2] == [0, 1]
+    # NaN rows are never selected; fewer finite neighbours than K_nbr -> -1
+    nan_nbr = np.array([[np.nan, 1.0, 0, 0], [3.2, 1.0, 0, 0], [3.0, 1.0, 0, 0]])
+    assert oracle.select_idx(p, x0, near, nan_nbr, 2).tolist()[2:] == [1, -1]
+    obs, _ = oracle.select_obstacles(p, x0, near, nan_nbr, 2)
+    assert (obs[:, 3] == 1e6).all()
+
+
 def test_oracle_batch_threads_deterministic():
     from srbnmpc import workload
     b = workload.make_batch(12, 10, 2, seed=5)
