@@ -108,6 +108,14 @@ typedef struct srb_ctx srb_ctx;
 int srb_ctx_create(const srb_params *p, int max_agents, int device, srb_ctx **out);
 int srb_ctx_destroy(srb_ctx *ctx);
 
+/* Waves (64-lane wavefronts) per agent's workgroup: 0 = automatic (4 while the batch has no
+ * more agents than the device has CUs, else 1, or 2 for problems whose row slots exceed five
+ * per lane), or force 1, 2 or 4.  Results are bit-identical for a given wave count; different
+ * counts sum the reduced Newton matrix in a different order (round-off differences only).
+ * srb_ctx_waves() returns the count the last launch used. */
+int srb_ctx_set_waves(srb_ctx *ctx, int nw);
+int srb_ctx_waves(srb_ctx *ctx);
+
 /* Host buffers: copies in, solves, copies out, synchronises.  n_agents <= max_agents. */
 int srb_solve_batch(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 

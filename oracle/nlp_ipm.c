@@ -21,6 +21,7 @@
 #include <math.h>
 #include <stdlib.h>
 #include <string.h>
+#include <stdio.h>
 #include "oracle.h"
 
 /* initial inequality duals: 100, the scale of the tracking weights' multipliers (against 1:
@@ -181,6 +182,8 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     }
 
     const double tol = pp->tol, th = tol / sqrt(3.0);
+    const int trace = getenv("ORC_NLP_TRACE") != NULL;     /* diagnostics: per-iteration line on stderr */
+    double tr_sigma = 0.0;
     for (int iter = 0; iter < pp->nlp_maxit; iter++) {
         rows_eval(&P, x, g, Jv, Ji);
         for (int j = 0; j < n; j++) rx[j] = -(Pd[j] * x[j] + c[j]) - q[j];
@@ -268,6 +271,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
                 for (int r = 0; r < m; r++) num += (s[r] + ap * dsv[r]) * (z[r] + ad * dz[r]);
                 double rho = num / dotv(s, z, m), mr = rho < 1 ? rho : 1;
                 double sigma = mr * mr * mr; if (sigma < 0) sigma = 0;
+                tr_sigma = sigma;
                 for (int r = 0; r < m; r++) ds[r] = -(lam[r] * lam[r]) - dsv[r] * dz[r] + sigma * mu;
             } else {
                 /* A'dy from the first block row of the Newton system,
@@ -282,6 +286,9 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             }
         }
         double ap = steplen(s, dsv, m), ad = steplen(z, dz, m);
+        if (trace)
+            fprintf(stderr, "  %2d %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e\n", iter, nrx, th * gmax, nrz, sz / m,
+                    ap, ad, delta, tr_sigma);
         if (near && (ap < ORC_NLP_BLOCKED || ad < ORC_NLP_BLOCKED)) { flag = 4; break; }
         ap = 0.99 * ap < 1.0 ? 0.99 * ap : 1.0;
         ad = 0.99 * ad < 1.0 ? 0.99 * ad : 1.0;

@@ -170,7 +170,10 @@ void orc_select_idx(const orc_params *p, const double x0[4], const double *obsta
 }
 
 /* obstacle positions per grid (static: fixed; agents: constant-velocity prediction
- * o_k = p + v Ts (k+1)) and their clearances; a row with no selection (-1) sits at 1e6 */
+ * o_k = p + v Ts (k+1)) and their clearances; a row with no selection (-1: fewer finite
+ * neighbours than K_nbr) sits 1000 m from the agent along +x, the reference's "no obstacle"
+ * distance (min_dist = 1000, MPC_dist.cpp:371): inactive, and small enough that its
+ * residual |p - o|^2 ~ 1e6 keeps full precision */
 void orc_select_obstacles(const orc_params *p, const double x0[4],
                           const double *obstacles, int n_obs,
                           const double *nbr_state, int n_all, int self_idx,
@@ -185,8 +188,8 @@ void orc_select_obstacles(const orc_params *p, const double x0[4],
         for (int k = 0; k < N; k++) {
             const double t = st ? 0.0 : p->Ts * (k + 1);
             const double *row = st ? obstacles + 2 * (size_t)bi : nbr_state + 4 * (size_t)bi;
-            obs_out[(k * K + j) * 2 + 0] = bi >= 0 ? row[0] + (st ? 0.0 : row[2] * t) : 1e6;
-            obs_out[(k * K + j) * 2 + 1] = bi >= 0 ? row[1] + (st ? 0.0 : row[3] * t) : 1e6;
+            obs_out[(k * K + j) * 2 + 0] = bi >= 0 ? row[0] + (st ? 0.0 : row[2] * t) : x0[0] + 1000.0;
+            obs_out[(k * K + j) * 2 + 1] = bi >= 0 ? row[1] + (st ? 0.0 : row[3] * t) : x0[2];
         }
     }
 }

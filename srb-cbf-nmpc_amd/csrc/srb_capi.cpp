@@ -44,9 +44,10 @@ static size_t g_lds_max = 160 * 1024;   // gfx950 LDS per CU; the device's share
 // not waves of one agent, fill the SIMDs -- except large problems (more than five row slots per
 // lane with one wave, e.g. N = 20), where one wave spills its registers and two waves per agent
 // are 1.8x faster (profiles/r01_nw_tuning.txt).  SRB_NMPC_NW = 1 | 2 | 4 overrides (tuning).
-static int wanted_waves(int n_agents, int slots)
+static int wanted_waves(int n_agents, int slots, int ctx_nw)
 {
     static const int forced = [] { const char *e = std::getenv("SRB_NMPC_NW"); return e ? std::atoi(e) : 0; }();
+    if (ctx_nw == 1 || ctx_nw == 2 || ctx_nw == 4) return ctx_nw;
     if (forced == 1 || forced == 2 || forced == 4) return forced;
     if (g_cu_count > 0 && n_agents <= g_cu_count) return 4;
     return (slots > 5 * 64) ? 2 : 1;
@@ -95,6 +96,7 @@ struct srb_ctx {
     float knn_ms, solve_ms;
     bool timed;
     int last_nw;
+    int nw;                        // waves per agent forced by srb_ctx_set_waves (0: automatic)
 };
 
 extern "C" void srb_params_default(srb_params *p, int N, int C)
@@ -221,7 +223,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     if (rc) return rc;
     srb_ctx *c = new srb_ctx();
     c->p = *p; c->max_agents = max_agents; c->device = device;
-    c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false;
+    c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false; c->nw = 0; c->last_nw = 0;
     const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -275,7 +277,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
     if (k.K_nbr > others) k.K_nbr = others > 0 ? others : 0;
-    const srb_instance *in = pick_instance(k, wanted_waves(n_agents, srb_slots(k.N, k.C, k.K_obs + k.K_nbr)));
+    const srb_instance *in = pick_instance(k, wanted_waves(n_agents, srb_slots(k.N, k.C, k.K_obs + k.K_nbr), c->nw));
     if (!in) return fail(SRB_ERR_SIZE, "no kernel instance covers this problem");
     const size_t lds = (size_t)srb_lds_doubles(k, in->nzl, in->nw) * sizeof(double);
     c->last_nw = in->nw;
@@ -298,6 +300,16 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
 }
+
+extern "C" int srb_ctx_set_waves(srb_ctx *c, int nw)
+{
+    if (!c) return fail(SRB_ERR_ARG, "null ctx");
+    if (nw != 0 && nw != 1 && nw != 2 && nw != 4) return fail(SRB_ERR_ARG, "waves per agent: 0 (automatic), 1, 2 or 4");
+    c->nw = nw;
+    return SRB_OK;
+}
+
+extern "C" int srb_ctx_waves(srb_ctx *c) { return c ? c->last_nw : 0; }
 
 extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch *dev_io, void *stream)
 {

@@ -30,10 +30,14 @@ struct SrbKParams {
 // threads, see srb_kernels.hip).  The host launches the first fitting instance of this list
 // with NW = 4 for small batches (one agent per CU, all four SIMDs) and NW = 1 otherwise
 // (srb_capi.cpp).
+#ifdef SRB_DEV_INSTANCES          // register-tuning builds of a few instances (make dev)
+#define SRB_KERNEL_INSTANCES(X) SRB_DEV_INSTANCES(X)
+#else
 #define SRB_KERNEL_INSTANCES(X) \
     X(8, 1, 1) X(16, 1, 1) X(12, 3, 1) X(12, 4, 1) X(16, 4, 1) X(24, 5, 1) X(24, 8, 1) X(32, 4, 1) X(32, 8, 1) \
     X(8, 1, 4) X(12, 1, 4) X(16, 1, 4) X(16, 2, 4) X(32, 2, 4) \
     X(12, 2, 2) X(16, 2, 2) X(24, 4, 2) X(24, 2, 4)
+#endif
 static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K; }
 
 static inline int srb_r4(int x) { return (x + 3) & ~3; }
@@ -49,7 +53,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int red = (NW > 1) ? 8 * 4 * NW : 0;
     const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
     return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
-           srb_r4(NK) + (K + 1) + red + part
+           srb_r4(NK) + (K + 1) + red + part + srb_slots(N, C, K)
 #ifdef SRB_STAMPS
            + 64
 #endif

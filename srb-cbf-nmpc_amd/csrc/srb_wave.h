@@ -7,6 +7,9 @@
 #ifndef WAVE
 #define WAVE 64
 #endif
+#ifndef SRB_USE_DPP     // DPP row_newbcast broadcasts in the reduced solve (0: readlane / LDS forms)
+#define SRB_USE_DPP 1
+#endif
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
@@ -129,6 +132,19 @@ __device__ __forceinline__ double rcp_d(double x)
 }
 __device__ __forceinline__ int rnd4(int x) { return (x + 3) & ~3; }
 
+// value of lane k of this lane's 16-lane row: one v_mov_b64_dpp row_newbcast:k (gfx90a+),
+// a VALU result the next instruction can consume -- no SGPR round trip as with readlane.
+// k must fold to a constant (unrolled loops).
+__device__ __forceinline__ double bc16(double v, int k)
+{
+    switch (k) {
+#define SRB_BC(K) case K: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xf, 0xf, false);
+    SRB_BC(0) SRB_BC(1) SRB_BC(2) SRB_BC(3) SRB_BC(4) SRB_BC(5) SRB_BC(6) SRB_BC(7)
+    SRB_BC(8) SRB_BC(9) SRB_BC(10) SRB_BC(11) SRB_BC(12) SRB_BC(13) SRB_BC(14) default: SRB_BC(15)
+#undef SRB_BC
+    }
+}
+
 // --------------------------------------------------------------------------- Gauss-Jordan
 // In-place inverse of the nz x nz SPD matrix held one row per lane (lane i: A[0..NZL)),
 // rows/columns >= nz padded with the identity.  Step k broadcasts the pivot row by
@@ -138,8 +154,12 @@ __device__ __forceinline__ int rnd4(int x) { return (x + 3) & ~3; }
 // order, so pivot <= 0 <=> not positive definite; regularise != 0 applies iSWIFT's dynamic
 // pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7).  Returns 0 on success.
 template <int NZL>
+__device__ __forceinline__ int gj_invert_dpp(double (&A)[NZL], int lane, int regularise);
+
+template <int NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
+    if constexpr (NZL <= 16 && SRB_USE_DPP) return gj_invert_dpp<NZL>(A, lane, regularise);
     // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
     // elimination is one basic block: the scheduler overlaps step k's row updates with the
     // broadcast of row k+1, whose entries are updated first.
@@ -160,6 +180,39 @@ __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int
         for (int jj = 0; jj < NZL; jj++) {
             const int j = (k + 1 + jj) % NZL;           // next pivot row's entries first
             if (j != k) A[j] = fma(-f, rk[j], A[j]);
+        }
+        A[k] = me ? 1.0 : -f;
+        cs = me ? inv : cs;
+    }
+#pragma unroll
+    for (int j = 0; j < NZL; j++) A[j] *= cs;
+    return fail;
+}
+
+// NZL <= 16: the matrix is replicated in each 16-lane row of the wave (lane l holds matrix
+// row l & 15) and step k broadcasts the pivot row by DPP row_newbcast:k -- one VALU move per
+// entry that the row update consumes directly, so a step's critical path is the pivot's
+// broadcast, reciprocal and multiplier, not the v_readlane -> SGPR -> VALU latency.  Same
+// arithmetic as the readlane form above (bit-identical results).
+template <int NZL>
+__device__ __forceinline__ int gj_invert_dpp(double (&A)[NZL], int lane, int regularise)
+{
+    static_assert(NZL <= 16, "row_newbcast reaches within 16 lanes");
+    const int r = lane & 15;
+    int fail = 0;
+    double cs = 1.0;
+#pragma unroll
+    for (int k = 0; k < NZL; k++) {
+        double piv = bc16(A[k], k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        fail |= !(piv > 0.0);
+        const double inv = rcp_d(piv);
+        const bool me = r == k;
+        const double f = me ? 0.0 : A[k] * inv;
+#pragma unroll
+        for (int jj = 0; jj < NZL; jj++) {
+            const int j = (k + 1 + jj) % NZL;           // next pivot row's entries first
+            if (j != k) A[j] = fma(-f, bc16(A[j], k), A[j]);
         }
         A[k] = me ? 1.0 : -f;
         cs = me ? inv : cs;

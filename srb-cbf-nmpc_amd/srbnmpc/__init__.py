@@ -79,6 +79,8 @@ def lib():
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch)]
         L.srb_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_void_p]
         L.srb_sync.argtypes = [ctypes.c_void_p]
+        L.srb_ctx_set_waves.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.srb_ctx_waves.argtypes = [ctypes.c_void_p]
         L.srb_hl_plan.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.srb_prepare_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Prep), ctypes.c_void_p]
         L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
@@ -234,6 +236,14 @@ class BatchSolver:
 
     def sync(self):
         _check(lib().srb_sync(self._h))
+
+    def set_waves(self, nw: int = 0):
+        """Waves per agent (0 automatic, 1, 2, 4; srb_ctx_set_waves)."""
+        _check(lib().srb_ctx_set_waves(self._h, int(nw)))
+
+    def waves(self) -> int:
+        """Waves per agent of the last launch."""
+        return lib().srb_ctx_waves(self._h)
 
     def last_kernel_ms(self):
         a = ctypes.c_float(); b = ctypes.c_float()

@@ -224,10 +224,17 @@ def test_knn_matches_bruteforce(Ko, Kn):
     ob = b["obstacles"].copy()
     # agents 0..7 at exact coordinates with exact-distance ties at mirrored positions
     for a in range(8):
-        px, py = 2.0 + a, 1.0 - 0.25 * a
+        # translate agent a's whole problem (state, reference, footholds) to the nearest
+        # quarter-metre point, where the mirrored offsets below give bit-equal distances
+        px, py = np.round(b["x0"][a, [0, 2]] * 4) / 4
+        dx, dy = px - b["x0"][a, 0], py - b["x0"][a, 2]
+        b["x0"][a, 0] += dx; b["x0"][a, 2] += dy
         b["x0"][a, [0, 2]] = (px, py); nb[a, :2] = (px, py)
-        ob[20 + 2 * a] = (px + 0.75, py + 0.5); ob[21 + 2 * a] = (px - 0.75, py - 0.5)
-        nb[100 + 2 * a, :2] = (px - 0.5, py + 0.75); nb[101 + 2 * a, :2] = (px + 0.5, py - 0.75)
+        b["ref"][a, 0::4] += dx; b["ref"][a, 2::4] += dy
+        b["foot"][a, :, 0] += dx; b["foot"][a, :, 1] += dy
+        # (clearances d^2 = 3.25 and 7.3125 stay above eps = 1.9 / 2.2: feasible instances)
+        ob[20 + 2 * a] = (px + 1.5, py + 1.0); ob[21 + 2 * a] = (px - 1.5, py - 1.0)
+        nb[100 + 2 * a, :2] = (px - 1.5, py + 2.25); nb[101 + 2 * a, :2] = (px + 1.5, py - 2.25)
     # agents 8..11: sqrt-rounding ties (larger d^2 at the lower index)
     for a in range(8, 12):
         px, py = b["x0"][a, 0], b["x0"][a, 2]
@@ -246,8 +253,8 @@ def test_knn_matches_bruteforce(Ko, Kn):
 def test_knn_sentinel_and_missing_rows():
     """The reference's min_dist = 1000 / min_i = 0 start (MPC_dist.cpp:371-372): with no
     static obstacle closer than 1000 m every static round selects obstacle 0; a neighbour
-    table with fewer finite rows than K_nbr leaves -1 slots, whose rows sit 1e6 m away (as in
-    the oracle), and the solve does not read unwritten LDS."""
+    table with fewer finite rows than K_nbr leaves -1 slots, whose rows sit 1000 m from the
+    agent (as in the oracle), and the solve does not read unwritten LDS."""
     N, C, A, Ko, Kn = 10, 2, 32, 2, 4
     b = workload.make_batch(A, N, C, seed=12)
     ob = np.array([[2500.0, 0.0], [0.0, -1200.0], [1001.0, 1001.0]])
@@ -258,40 +265,51 @@ def test_knn_sentinel_and_missing_rows():
     op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
     want = _oracle_sel(op, b, ob, nb, Ko, Kn)
     np.testing.assert_array_equal(out["sel"], want)
-    assert (out["sel"][:, :Ko] == 0).all() and (out["sel"][3:, Ko + 2:] == -1).all()
+    # agents 3.. see the three finite rows 0..2, agents 0..2 the other two
+    assert (out["sel"][:, :Ko] == 0).all() and (out["sel"][3:, Ko + 3] == -1).all()
+    assert (out["sel"][:3, Ko + 2:] == -1).all() and (out["sel"][3:, Ko:Ko + 3] >= 0).all()
     r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], ob, nb, nthreads=8)
     np.testing.assert_array_equal(out["status"], r["status"])
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
-@pytest.mark.parametrize("shards", [2, 8])
-def test_sharded_solve_matches_full_batch(shards):
+@pytest.mark.parametrize("shards,nw", [(2, 0), (8, 1), (8, 4)])
+def test_sharded_solve_matches_full_batch(shards, nw):
     """The multi-GPU data path on one GPU: each shard is what one rank solves after the
     all-gather (srbnmpc.dist): its contiguous agent block with agent_offset = lo and the FULL
     neighbour table (MPC_dist.cpp:1272-1276 rows of every agent).  Statuses, x and the
-    selected rows are bit-identical to the single-batch solve, which matches the oracle."""
+    selected rows are bit-identical to the single-batch solve with the same waves per agent
+    (nw; 0 = the automatic choice, the same for 512- and 1024-agent batches), which matches
+    the oracle."""
     from srbnmpc import dist as sdist
     N, C, A, Ko, Kn = 10, 2, 1024, 3, 8
     b = workload.make_batch(A, N, C, seed=77)
-    s = solver(N, C, Ko, Kn)
+    s = srbnmpc.BatchSolver(srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn), A)
+    s.set_waves(nw)
     full = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    nw_full = s.waves()
     dev = torch.device("cuda:0")
     T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
     nbr = T(b["nbr_state"]); obst = T(b["obstacles"])
-    parts = []
+    parts, keep = [], []
     for r in range(shards):
         lo, hi = sdist.shard_range(A, shards, r)
         n = hi - lo
+        ins = (T(b["x0"][lo:hi]), T(b["ref"][lo:hi]), T(b["foot"][lo:hi].reshape(n, -1)))
+        keep.append(ins)                      # inputs stay allocated until the launches have run
         o = dict(x_qp=None, x=torch.zeros((n, s.params.nv), dtype=torch.float64, device=dev),
                  obj=torch.zeros(n, dtype=torch.float64, device=dev),
                  status=torch.zeros((n, 2), dtype=torch.int32, device=dev),
                  iters=torch.zeros((n, 2), dtype=torch.int32, device=dev),
                  sel=torch.full((n, Ko + Kn), -2, dtype=torch.int32, device=dev))
-        s.solve_device(T(b["x0"][lo:hi]), T(b["ref"][lo:hi]), T(b["foot"][lo:hi].reshape(n, -1)), obst, nbr, o,
-                       agent_offset=lo)
+        s.solve_device(*ins, obst, nbr, o, agent_offset=lo)
         parts.append(o)
     torch.cuda.synchronize()
+    assert s.waves() == nw_full
+    s.close()
     cat = {k: np.concatenate([o[k].cpu().numpy() for o in parts]) for k in ("x", "obj", "status", "iters", "sel")}
+    bad = np.where((cat["status"] != full["status"]).any(1) | (cat["x"] != full["x"]).any(1))[0]
+    assert bad.size == 0, (bad[:10], cat["status"][bad[:5]], full["status"][bad[:5]])
     for k in cat:
         np.testing.assert_array_equal(cat[k], full[k], err_msg=k)
     # the shard rows exclude their own global index from the neighbours

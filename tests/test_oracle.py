@@ -143,12 +143,12 @@ def test_select_obstacles_matches_bruteforce():
         assert np.all(eps[:3] == p.eps_obs) and np.all(eps[3:] == p.eps_nbr)
 
 
-def sqrt_tie_pair(px, py, rng):
+def sqrt_tie_pair(px, py, rng, lo=1.5, hi=3.0):
     """Two points whose squared distances to (px, py) differ (d2a < d2b) but whose sqrt
     distances round to the same double: the reference's sqrt scan (MPC_dist.cpp:376) sees a
     tie there and keeps the lower index, a d^2 order would not."""
     while True:
-        ax, ay = px + rng.uniform(1, 3), py + rng.uniform(1, 3)
+        ax, ay = px + rng.uniform(lo, hi), py + rng.uniform(lo, hi)
         da = (px - ax) ** 2 + (py - ay) ** 2
         by = ay
         for _ in range(64):
@@ -183,7 +183,7 @@ def test_select_idx_reference_semantics():
     nan_nbr = np.array([[np.nan, 1.0, 0, 0], [3.2, 1.0, 0, 0], [3.0, 1.0, 0, 0]])
     assert oracle.select_idx(p, x0, near, nan_nbr, 2).tolist()[2:] == [1, -1]
     obs, _ = oracle.select_obstacles(p, x0, near, nan_nbr, 2)
-    assert (obs[:, 3] == 1e6).all()
+    assert (obs[:, 3] == [x0[0] + 1000.0, x0[2]]).all()
 
 
 def test_oracle_batch_threads_deterministic():

@@ -8,7 +8,7 @@ mkdir -p gpurun_out
 export TMPDIR=/tmp
 make -s -C oracle all || exit 1
 if [ -z "$1" ]; then
-  timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread > gpurun_out/pytest_gpu.log 2>&1; rc=$?
+  timeout -k 10 900 python -u -m pytest tests -x -v -m gpu --timeout 300 --timeout-method thread ${PYTEST_K:+-k "$PYTEST_K"} > gpurun_out/pytest_gpu.log 2>&1; rc=$?
   tail -4 gpurun_out/pytest_gpu.log
   [ $rc -eq 0 ] || { grep -E "Error|assert|FAILED" gpurun_out/pytest_gpu.log | head -30; exit $rc; }
   timeout -k 10 180 python -c "import __graft_entry__ as g; g.smoke()" > gpurun_out/smoke.log 2>&1 || { cat gpurun_out/smoke.log; exit 1; }
@@ -37,3 +37,5 @@ for a in "10 2 3 0 64" "10 2 3 8 1024"; do
   cat "gpurun_out/stamps_${a// /_}.log"
 done
 find gpurun_out -name "*stats*.csv" | sort
+[ -x tools/ubench/gj_bench ] && timeout -k 10 60 tools/ubench/gj_bench
+[ -f srb-cbf-nmpc_amd/srbnmpc/libsrbnmpc_nlpdbg.so ] && timeout -k 10 60 python tools/far_trace.py 5
