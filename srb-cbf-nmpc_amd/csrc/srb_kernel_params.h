@@ -30,6 +30,9 @@ struct SrbKParams {
 // threads, see srb_kernels.hip).  The host launches the first fitting instance of this list
 // with NW = 4 for small batches (one agent per CU, all four SIMDs) and NW = 1 otherwise
 // (srb_capi.cpp).
+#ifndef SRB_WPE                 // extra kernel attribute of the solve instances (register-tuning builds)
+#define SRB_WPE
+#endif
 #ifdef SRB_DEV_INSTANCES          // register-tuning builds of a few instances (make dev)
 #define SRB_KERNEL_INSTANCES(X) SRB_DEV_INSTANCES(X)
 #else
@@ -42,6 +45,7 @@ static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * 
 
 static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
+
 // doubles of dynamic LDS one agent needs for instance bound NZL; must match the carve in
 // nmpc_agent (srb_kernels.hip)
 static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
@@ -53,7 +57,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int red = (NW > 1) ? 8 * 4 * NW : 0;
     const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
     return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
-           srb_r4(NK) + (K + 1) + red + part + srb_slots(N, C, K)
+           srb_r4(NK) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64
 #endif

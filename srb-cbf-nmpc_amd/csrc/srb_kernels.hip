@@ -292,25 +292,17 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         // rows replicated per 16-lane row: the three vector broadcasts are DPP moves, no LDS
         // round trip or barrier
         const int i = lane & 15;
-        double hr[NZL], gv[NZL];
-#pragma unroll
-        for (int j = 0; j < NZL; j++) { hr[j] = Hs[i * LDH + j]; gv[j] = g[j]; }
-        const double gi = (i < nz) ? g[i] : 0.0;
+        const double gi = (i < nz) ? g[i] : 0.0;         // g is zero beyond nz
         double y0 = 0.0;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) y0 = fma(M[j], gv[j], y0);
-        double yb[NZL];
-#pragma unroll
-        for (int j = 0; j < NZL; j++) yb[j] = bc16(y0, j);
+        for (int j = 0; j < NZL; j++) y0 = fma(M[j], bc16(gi, j), y0);
         double rr = gi;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) rr = fma(-hr[j], yb[j], rr);
+        for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y0, j), rr);
         if (i >= nz) rr = 0.0;
-#pragma unroll
-        for (int j = 0; j < NZL; j++) yb[j] = bc16(rr, j);
         double y1 = y0;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) y1 = fma(M[j], yb[j], y1);
+        for (int j = 0; j < NZL; j++) y1 = fma(M[j], bc16(rr, j), y1);
 #pragma unroll
         for (int j = 0; j < NZL; j++) res[j] = bc16(y1, j);
         return;
@@ -370,95 +362,53 @@ __device__ __forceinline__ int lambda_basis(const double *F, int C, int t, doubl
 // --------------------------------------------------------------------------- slots
 // Every inequality row of the problem belongs to a SLOT: a bound pair on one scalar
 // function f of x (row 0: f <= h0, row 1: -f <= h1; a single row has row 1 off) whose
-// Jacobian, reduced by Z, is one term row of R.  Slot s is worked by lane s % (64 NW) (trip
-// s / (64 NW)) for the whole solve.  Kinds, in slot order:
+// Jacobian, reduced by Z, is one term row of R.  Slot s lives in registers of lane s % 64
+// (trip s / 64) for the whole solve.  Kinds, in slot order:
 //   VAR  s in [0, n):            f = x_v (v = s), box +-1e3 on X/U, [0, 1] on lambda, none on
-//                                the slack; also carries rx_v; term row v (Z row)
+//                                the slack; also carries rx_v, P_v, c_v; term row v (Z row)
 //   COP  [n, n + 2(N-1)):        f = p_i - u_{i+1}, +-mu h / sqrt 2; term row M_e
 //   VEL  [.., + 2N) (NLP):       f = xdot_k / ydot_k, +-vsat; adds into term row v
 //   OBS  [.., + N K) (NLP):      f = -|p_k - o_kj|^2 - s, single row <= -eps_j; term row M_o
 // so residuals, Newton rows, step lengths and updates are one straight-line code path.
-//
-// Registers hold only the iterate of a slot (s, z, the last direction ds, dz, the
-// reciprocals 1/s, 1/z of the current iteration, rx and J dx); everything constant -- kind,
-// indices, term row, bounds, weights, masks -- is decoded at each use from one packed LDS
-// word per slot (SlotDesc), and the complementarity right-hand side (dsT, r3) is recomputed
-// where it is needed.  The LDS read is opaque to the compiler, so none of it is hoisted into
-// registers that would stay live across the iteration.
 enum { K_NONE = 0, K_VAR = 1, K_COP = 2, K_VEL = 3, K_OBS = 4 };
 
 struct Slot {
-    double s[2], z[2], iz[2], is[2], dz[2], ds[2];
-    double rx;          // VAR: dual residual component
-    double jd;          // J dx of the latest Newton solve (setup phases: f(x))
+    double s[2], z[2], iz[2], is[2], dz[2], ds[2], dsT[2], r3[2];
+    double h[2];        // row bounds
+    double a0, a1, rx;  // VAR: P_v, c_v ; OBS: o_x, o_y
+    double jd;          // J dx of the latest Newton solve (VAR: dx_v)
+    double m[2];        // 1.0 / 0.0: row active in the current stage (arithmetic masks keep
+                        // per-lane flags in VGPRs instead of long-lived SGPR lane masks)
+    int i0, i1, r;      // xs indices of f, term row
+    int wr;             // row this slot stores W / CF to (a scratch entry for VEL / unused slots)
+    int kind;
 };
 
-// packed descriptor: x = kind | st << 3 | r << 4 ; y = i0 | i1 << 16
-//   (st: OBS row of a static obstacle / VAR lambda entry; r: term row; i0, i1: xs indices of f)
-struct SlotDesc {
-    int kind, st, r, i0, i1;
-};
-__device__ __forceinline__ SlotDesc slot_desc(const int2 *sd, int sl, int S)
+// kind read through an opaque copy: comparisons on it are recomputed at each use instead
+// of being hoisted into lane masks that stay live across the whole iteration
+__device__ __forceinline__ int kind_of(const Slot &q)
 {
-    int2 v = make_int2(K_NONE, 0);
-    if (sl < S) v = sd[sl];
-    asm volatile("" : "+v"(v.x), "+v"(v.y));
-    SlotDesc d;
-    d.kind = v.x & 7; d.st = (v.x >> 3) & 1; d.r = v.x >> 4;
-    d.i0 = v.y & 0xffff; d.i1 = v.y >> 16;
-    return d;
-}
-
-// slot constants decoded from the descriptor and the uniform problem data
-struct SlotK {
-    double h0, h1, m0, m1;    // bounds and stage masks (1.0 / 0.0: arithmetic, no per-lane flags)
-    double a0, a1;            // VAR: P_v, c_v ; OBS: o_x, o_y
-    int wr;                   // row this slot stores W / CF to (scratch entry TT for VEL / unused)
-};
-__device__ __forceinline__ SlotK slot_k(const SlotDesc &d, const SrbKParams &prm, bool nl, const double *ref,
-                                        const double *obs, const double *eps, int N, int n, int K, int sO, int sl, int TT)
-{
-    SlotK k;
-    const bool var = d.kind == K_VAR, cop = d.kind == K_COP, vel = d.kind == K_VEL, ob = d.kind == K_OBS;
-    const int v = d.i0;
-    const bool isX = v < 4 * N, isU = !isX && v < 6 * N;
-    const double pv = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : d.st ? 0.0 : prm.Sw;
-    const int o = sl - sO;
-    k.a0 = var ? pv : ob ? obs[ob ? 2 * o : 0] : 0.0;
-    k.a1 = var ? (isX ? -pv * ref[isX ? v : 0] : 0.0) : ob ? obs[ob ? 2 * o + 1 : 0] : 0.0;
-    k.h0 = var ? (d.st ? 1.0 : prm.box) : cop ? prm.fr : vel ? prm.vsat : ob ? -eps[d.st ? 0 : K] : 0.0;
-    k.h1 = var ? (d.st ? 0.0 : prm.box) : cop ? prm.fr : vel ? prm.vsat : 0.0;
-    const bool lin = (var && v < n - 1) || cop;
-    k.m0 = (lin || (nl && (vel || ob))) ? 1.0 : 0.0;
-    k.m1 = (lin || (nl && vel)) ? 1.0 : 0.0;
-    k.wr = (var || cop || ob) ? d.r : TT;
+    int k = q.kind;
+    asm volatile("" : "+v"(k));
     return k;
 }
 
-__device__ __forceinline__ double slot_f(const SlotDesc &d, const SlotK &k, const double *xs, double s_var)
+__device__ __forceinline__ double slot_f(const Slot &q, const double *xs, double s_var)
 {
-    const double x0 = xs[d.i0], x1 = xs[d.i1];
-    const double dx = x0 - k.a0, dy = x1 - k.a1;
-    return (d.kind == K_OBS) ? -(dx * dx + dy * dy) - s_var : (d.kind == K_COP) ? x0 - x1 : x0;
+    const double x0 = xs[q.i0], x1 = xs[q.i1];
+    const int k = kind_of(q);
+    const double dx = x0 - q.a0, dy = x1 - q.a1;
+    return (k == K_OBS) ? -(dx * dx + dy * dy) - s_var : (k == K_COP) ? x0 - x1 : x0;
 }
 
-// complementarity target of row r in pass `corr` (predictor: corr = false, smu = 0):
-//   dsT = -s z (- ds dz) + smu, and r3 = rz - dsT / z with rz = h - s -+ f
-__device__ __forceinline__ void slot_rhs(const Slot &q, const SlotK &k, double f, int r, bool corr, double smu,
-                                         double &dsT, double &r3)
-{
-    double t = -q.s[r] * q.z[r];
-    if (corr) t = fma(-q.ds[r], q.dz[r], t);
-    dsT = t + smu;
-    const double rz = r ? (k.h1 - q.s[1] + f) : (k.h0 - q.s[0] - f);
-    r3 = fma(-dsT, q.iz[r], rz);
-}
+
 
 // --------------------------------------------------------------------------- main kernel
 // NZL: register bound on nz (one reduced-matrix row per lane); TS: slot trips per thread;
-// NW: wavefronts per agent.  With NW > 1 the row slots and the term-row passes are split
-// across the waves and combined through LDS; the reduced-system factorisation and solves run
-// redundantly in every wave (identical data, identical results, no communication).
+// NW: wavefronts per agent (1, or 4 = one per SIMD of a CU for small batches).  With NW > 1
+// the row slots and the term-row passes are split across the waves and combined through LDS;
+// the reduced-system factorisation and solves run redundantly in every wave (identical data,
+// identical results, no communication).
 template <int NZL, int TS, int NW>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
@@ -472,7 +422,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDR = NZL + 1, LDH = NZM + 1;
     constexpr int NTH = 64 * NW;                        // threads per agent
-    const int tid = threadIdx.x, lane = tid & 63;
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
     const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz;
     const int NK = N * K, NE = 2 * (N - 1);
     const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N);
@@ -497,12 +447,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double *ref = p; p += 4 * N;
     double *foot = p; p += 2 * C * N;
     double *obs = p; p += 2 * NK + 2;
-    double *eps = p; p += K + 1;                        // eps[0]: static obstacles, eps[K]: agents
+    double *eps = p; p += K + 1;
     double *zo = p; p += NK4;                           // obstacle duals (per-grid sums)
     int *sel = (int *)p; p += (K + 1);
     double *red = p; p += (NW > 1) ? 8 * 4 * NW : 0;      // cross-wave reduction scratch, 8 sites
     double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   // partial Gram / rhs
-    int2 *sd = (int2 *)p; p += S;                       // slot descriptors
 #ifdef SRB_STAMPS
     unsigned long long *stamp_lds = (unsigned long long *)p; p += SRB_NSTAMP;
     if (tid < 64) stamp_lds[tid] = 0;
@@ -516,27 +465,6 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     for (int i = tid; i < 2 * C * N; i += NTH) foot[i] = footg[(size_t)agent * 2 * C * N + i];
     for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0;     // tables, matrices, vectors, xs, xb
     for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0;
-    // obstacle positions are filled at the NLP stage; until then the OBS slots' f must stay
-    // finite (their masks are 0, and 0 * NaN would poison the QP residual norms)
-    for (int i = tid; i < 2 * NK + 2; i += NTH) obs[i] = 0.0;
-    if (tid == 0) { eps[0] = prm.eps_obs; eps[K] = prm.eps_nbr; }
-    // slot descriptors
-    for (int sl = tid; sl < S; sl += NTH) {
-        int kind = K_NONE, st = 0, r = 0, i0 = 0, i1 = 0;
-        if (sl < sE) {                                   // VAR
-            kind = K_VAR; i0 = i1 = sl; r = TL.zr(sl); st = (sl >= 6 * N && sl < n - 1);
-        } else if (sl < sV) {                            // COP
-            const int e = sl - sE, i = e >> 1, d = e & 1;
-            kind = K_COP; i0 = 4 * i + 2 * d; i1 = 4 * N + 2 * (i + 1) + d; r = rC + e;
-        } else if (sl < sO) {                            // VEL
-            const int tt = sl - sV, comp = (tt < N) ? 1 : 3, k = tt % N;
-            kind = K_VEL; i0 = i1 = 4 * k + comp; r = 4 * k + comp;
-        } else {                                         // OBS (positions filled at the NLP stage)
-            const int o = sl - sO, k = o / K;
-            kind = K_OBS; i0 = 4 * k; i1 = 4 * k + 2; r = rO + o; st = (o % K) < prm.K_obs;
-        }
-        sd[sl] = make_int2(kind | st << 3 | r << 4, i0 | i1 << 16);
-    }
     SYNC();
 
     // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
@@ -582,14 +510,35 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     }
     for (int v = tid; v < n; v += NTH) xs[v] = xb[v];
 
-    // ---- slot state
+    // ---- slot constants
     Slot Q[TS];
 #pragma unroll
     for (int t = 0; t < TS; t++) {
         Slot &q = Q[t];
-        q.rx = 0.0; q.jd = 0.0;
+        const int sl = tid + NTH * t;
+        q.kind = K_NONE; q.i0 = q.i1 = 0; q.r = 0; q.h[0] = q.h[1] = 0.0; q.a0 = q.a1 = 0.0; q.rx = 0.0; q.jd = 0.0;
+        q.m[0] = q.m[1] = 0.0; q.wr = TT;
+        if (sl < sE) {                                   // VAR
+            const int v = sl;
+            const bool isX = v < 4 * N, isU = !isX && v < 6 * N, isL = !isX && !isU && v < n - 1;
+            q.kind = K_VAR; q.i0 = q.i1 = v; q.r = TL.zr(v);
+            q.a0 = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : isL ? 0.0 : prm.Sw;
+            q.a1 = isX ? -q.a0 * ref[v] : 0.0;
+            q.h[0] = isL ? 1.0 : prm.box; q.h[1] = isL ? 0.0 : prm.box;
+        } else if (sl < sV) {                            // COP
+            const int e = sl - sE, i = e >> 1, d = e & 1;
+            q.kind = K_COP; q.i0 = 4 * i + 2 * d; q.i1 = 4 * N + 2 * (i + 1) + d; q.r = rC + e;
+            q.h[0] = q.h[1] = prm.fr;
+        } else if (sl < sO) {                            // VEL
+            const int tt = sl - sV, comp = (tt < N) ? 1 : 3, k = tt % N;
+            q.kind = K_VEL; q.i0 = q.i1 = 4 * k + comp; q.r = 4 * k + comp;
+            q.h[0] = q.h[1] = prm.vsat;
+        } else if (sl < S) {                             // OBS (positions filled at the NLP stage)
+            const int o = sl - sO, k = o / K;
+            q.kind = K_OBS; q.i0 = 4 * k; q.i1 = 4 * k + 2; q.r = rO + o;
+        }
 #pragma unroll
-        for (int r = 0; r < 2; r++) { q.s[r] = q.z[r] = 1.0; q.iz[r] = q.is[r] = 1.0; q.dz[r] = q.ds[r] = 0.0; }
+        for (int r = 0; r < 2; r++) { q.s[r] = q.z[r] = 1.0; q.iz[r] = q.is[r] = 1.0; q.dz[r] = q.ds[r] = q.dsT[r] = q.r3[r] = 0.0; }
     }
     double Mi[NZL];                                          // inverse of the reduced Newton matrix (row = lane)
     double dxi[NZL];                                         // Newton direction in xi (uniform)
@@ -597,10 +546,6 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     for (int j = 0; j < NZL; j++) { Mi[j] = (mrow<NZL>(lane) == j) ? 1.0 : 0.0; dxi[j] = 0.0; }
     SYNC();
     STAMP_END(0);
-
-    // per-slot decode at a use site: d (descriptor), k (constants) of trip t in stage nl
-#define SLOT_AT(t, nl) const int sl_ = tid + NTH * (t); const SlotDesc d = slot_desc(sd, sl_, S); \
-    const SlotK k = slot_k(d, prm, nl, ref, obs, eps, N, n, K, sO, sl_, TT)
 
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
@@ -614,19 +559,28 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
         const int cnt = ((nl ? rO + NK4 : rO) + 16 * NW - 1) / (16 * NW) * (16 * NW);   // term rows (zero-padded)
         STAMP_BEGIN();
+        // stage activity of each row
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            Slot &q = Q[t];
+            const bool lin = (q.kind == K_VAR && q.i0 < n - 1) || q.kind == K_COP;
+            q.m[0] = (lin || (nl && (q.kind == K_VEL || q.kind == K_OBS))) ? 1.0 : 0.0;
+            q.m[1] = (lin || (nl && q.kind == K_VEL)) ? 1.0 : 0.0;
+            q.wr = (q.kind == K_VAR || q.kind == K_COP || q.kind == K_OBS) ? q.r : TT;
+        }
         if (!nl) {
             // ---------------- QP stage setup: kkt_initialize (Auxilary.c:680-755) ----------------
             // [P A' G'; A 0 0; G 0 -I] [x; y; z] = [-c; b; h]:  (Z'(P + G'G)Z) xi = -Z'(P xbar + c) + Z'G'(h - G xbar)
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
-                    SLOT_AT(t, false);
-                    const double f = slot_f(d, k, xs, 0.0);
-                    const double w0 = k.m0 * (k.h0 - f), w1 = k.m1 * (k.h1 + f);
-                    const bool var = d.kind == K_VAR;
-                    const double wgt = (var ? k.a0 : 0.0) + k.m0 + k.m1;
-                    const double cfv = (var ? -k.a1 - k.a0 * f : 0.0) + (w0 - w1);
-                    if (d.kind == K_VAR || d.kind == K_COP) { W[d.r] = wgt; CF[d.r] = cfv; }
+                    Slot &q = Q[t];
+                    const double f = slot_f(q, xs, 0.0);
+                    const double w0 = q.m[0] * (q.h[0] - f), w1 = q.m[1] * (q.h[1] + f);
+                    const bool var = q.kind == K_VAR;
+                    const double wgt = (var ? q.a0 : 0.0) + q.m[0] + q.m[1];
+                    const double cfv = (var ? -q.a1 - q.a0 * f : 0.0) + (w0 - w1);
+                    if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
             SYNC();
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
@@ -643,12 +597,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    SLOT_AT(t, false);
-                    const double f = slot_f(d, k, xs, 0.0) + row_dot<NZL>(R + d.r * LDR, dxi);
+                    const double f = slot_f(q, xs, 0.0) + row_dot<NZL>(R + q.r * LDR, dxi);
                     q.jd = f;                                 // f(x) for the shift below
-                    const double z0 = k.h0 - f, z1 = k.h1 + f;
-                    if (k.m0 != 0.0) { mn = fmin(mn, z0); mx = fmax(mx, z0); }
-                    if (k.m1 != 0.0) { mn = fmin(mn, z1); mx = fmax(mx, z1); }
+                    const double z0 = q.h[0] - f, z1 = q.h[1] + f;
+                    if (q.m[0] != 0.0) { mn = fmin(mn, z0); mx = fmax(mx, z0); }
+                    if (q.m[1] != 0.0) { mn = fmin(mn, z1); mx = fmax(mx, z1); }
                 }
             double rv[2] = {-mn, mx};
             wred_x<2, 3u, NW>(rv, red + 0 * 4 * NW, tid);
@@ -659,11 +612,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    SLOT_AT(t, false);
-                    const double f = q.jd, z0 = k.h0 - f, z1 = k.h1 + f;
-                    q.s[0] = (k.m0 != 0.0) ? z0 + ssh : 1.0; q.z[0] = (k.m0 != 0.0) ? -z0 + zsh : 1.0;
-                    q.s[1] = (k.m1 != 0.0) ? z1 + ssh : 1.0; q.z[1] = (k.m1 != 0.0) ? -z1 + zsh : 1.0;
-                    if (d.kind == K_VAR) xs[d.i0] = f;
+                    const double f = q.jd, z0 = q.h[0] - f, z1 = q.h[1] + f;
+                    q.s[0] = (q.m[0] != 0.0) ? z0 + ssh : 1.0; q.z[0] = (q.m[0] != 0.0) ? -z0 + zsh : 1.0;
+                    q.s[1] = (q.m[1] != 0.0) ? z1 + ssh : 1.0; q.z[1] = (q.m[1] != 0.0) ? -z1 + zsh : 1.0;
+                    if (q.kind == K_VAR) xs[q.i0] = f;
                     q.rx = 0.0;      // = G'(dz_init - z) = -(1+za) G'1 = 0: every G row comes in a +- pair
                 }
             SYNC();
@@ -683,27 +635,31 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const bool st = j < prm.K_obs;
                 const int bi = sel[j];
                 if (tid < N) {                                // no selection (-1): a row 1000 m along +x, as the oracle
-                    const int kk = tid;
-                    const double tt = st ? 0.0 : prm.Ts * (kk + 1);
+                    const int k = tid;
+                    const double tt = st ? 0.0 : prm.Ts * (k + 1);
                     const size_t bj = (bi >= 0) ? bi : 0;     // row 0 exists whenever K_obs / K_nbr > 0
                     const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj;
-                    obs[2 * (kk * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0;
-                    obs[2 * (kk * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2];
+                    obs[2 * (k * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0;
+                    obs[2 * (k * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2];
                 }
+                if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr;
             }
             SYNC();
-            // slacks: shifted h - g(x) over every NLP row; duals SRB_NLP_Z0
+            // slacks: shifted h - g(x) over every NLP row; duals 1
             const double s_var = xs[n - 1];
             double mn = 1e300;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    SLOT_AT(t, true);
-                    const double f = slot_f(d, k, xs, s_var);
+                    if (q.kind == K_OBS) {
+                        const int o = tid + NTH * t - sO;
+                        q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K];
+                    }
+                    const double f = slot_f(q, xs, s_var);
                     q.jd = f;
-                    if (k.m0 != 0.0) mn = fmin(mn, k.h0 - f);
-                    if (k.m1 != 0.0) mn = fmin(mn, k.h1 + f);
+                    if (q.m[0] != 0.0) mn = fmin(mn, q.h[0] - f);
+                    if (q.m[1] != 0.0) mn = fmin(mn, q.h[1] + f);
                 }
             {
                 double rv[1] = {-mn};
@@ -715,22 +671,21 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    SLOT_AT(t, true);
                     const double f = q.jd;
-                    q.s[0] = (k.m0 != 0.0) ? k.h0 - f + ssh : 1.0;
-                    q.s[1] = (k.m1 != 0.0) ? k.h1 + f + ssh : 1.0;
+                    q.s[0] = (q.m[0] != 0.0) ? q.h[0] - f + ssh : 1.0;
+                    q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
                     q.z[0] = q.z[1] = SRB_NLP_Z0;
-                    if (d.kind == K_OBS) {                     // M_o = J_o Z at the current x
-                        const double jx = -2.0 * (xs[d.i0] - k.a0), jy = -2.0 * (xs[d.i1] - k.a1);
+                    if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x
+                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
 #pragma unroll
                         for (int a = 0; a < NZL; a++)
-                            R[d.r * LDR + a] = fma(jx, R[d.i0 * LDR + a], jy * R[d.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
                     }
                     // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = z0: J'1 vanishes on every
                     // +- pair, leaving the obstacle rows
-                    if (d.kind == K_VAR) { W[d.r] = 1.0; CF[d.r] = fma(k.a0, f, k.a1); }
-                    else if (d.kind == K_COP) { W[d.r] = 0.0; CF[d.r] = 0.0; }
-                    else if (d.kind == K_OBS) { W[d.r] = 0.0; CF[d.r] = SRB_NLP_Z0; }
+                    if (q.kind == K_VAR) { W[q.r] = 1.0; CF[q.r] = fma(q.a0, f, q.a1); }
+                    else if (q.kind == K_COP) { W[q.r] = 0.0; CF[q.r] = 0.0; }
+                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = SRB_NLP_Z0; }
                 }
             SYNC();
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, ZZ, vg, nz, tid, part);
@@ -742,8 +697,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    const SlotDesc d = slot_desc(sd, tid + NTH * t, S);
-                    q.rx = (d.kind == K_VAR) ? -row_dot<NZL>(R + d.r * LDR, dxi) : 0.0;
+                    q.rx = (q.kind == K_VAR) ? -row_dot<NZL>(R + q.r * LDR, dxi) : 0.0;
                 }
             SYNC();
             STAMP_END(2);
@@ -760,27 +714,29 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // ---- residuals (computeresiduals, Auxilary.c:524-553), norms, reciprocals
             const double s_var = xs[n - 1];
             double nrx = 0.0, nrz = 0.0, sz = 0.0, gm = 1.0;
+            double fv[TS];
 #pragma unroll
             for (int t = 0; t < TS; t++) {
+                fv[t] = 0.0;
                 if (t < nts) {
                     Slot &q = Q[t];
-                    SLOT_AT(t, nl);
-                    const double f = slot_f(d, k, xs, s_var);
-                    if (d.kind == K_VAR) {
+                    const double f = slot_f(q, xs, s_var);
+                    fv[t] = f;
+                    if (kind_of(q) == K_VAR) {
                         nrx = fma(q.rx, q.rx, nrx);
-                        gm = fmax(gm, fabs(fma(k.a0, f, k.a1)));
+                        gm = fmax(gm, fabs(fma(q.a0, f, q.a1)));
                     }
-                    const double rz0 = k.h0 - q.s[0] - f, rz1 = k.h1 - q.s[1] + f;
-                    nrz = fma(k.m0 * rz0, rz0, fma(k.m1 * rz1, rz1, nrz));
-                    sz = fma(k.m0 * q.s[0], q.z[0], fma(k.m1 * q.s[1], q.z[1], sz));
+                    const double rz0 = q.h[0] - q.s[0] - f, rz1 = q.h[1] - q.s[1] + f;
+                    nrz = fma(q.m[0] * rz0, rz0, fma(q.m[1] * rz1, rz1, nrz));
+                    sz = fma(q.m[0] * q.s[0], q.z[0], fma(q.m[1] * q.s[1], q.z[1], sz));
 #pragma unroll
                     for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
-                    if (nl && d.kind == K_OBS) {              // re-linearise: M_o = J_o(x) Z
-                        const double jx = -2.0 * (xs[d.i0] - k.a0), jy = -2.0 * (xs[d.i1] - k.a1);
+                    if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z
+                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
 #pragma unroll
                         for (int a = 0; a < NZL; a++)
-                            R[d.r * LDR + a] = fma(jx, R[d.i0 * LDR + a], jy * R[d.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
-                        zo[d.r - rO] = q.z[0];
+                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                        zo[q.r - rO] = q.z[0];
                     }
                 }
             }
@@ -804,8 +760,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             bool acc = false;
             const bool pc = nl || (sigma > sigma_d);
             double delta = 0.0;
-            // right-hand side of pass (0 predictor, 1 corrector / centring): coefficient of term
-            // row r = rx + J'(om r3)
+            // right-hand side of pass (0 predictor, 1 corrector / centring):
+            //   dsT, r3 = rz - dsT / z, w = om r3, coefficient of term row r = rx + J'w
             auto set_rhs = [&](int pass) {
                 const double smu = (pass == 0) ? 0.0 : (pc ? sigma * mu : sigma_d * mu);
                 const bool corr = pass == 1 && pc;
@@ -814,62 +770,55 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++) {
                     cfs[t] = 0.0;
                     if (t < nts) {
-                        const Slot &q = Q[t];
-                        SLOT_AT(t, nl);
-                        const double f = slot_f(d, k, xs, s_var);
-                        double cf = (d.kind == K_VAR) ? q.rx : 0.0;
+                        Slot &q = Q[t];
+                        const double f = fv[t];
+                        double cf = (kind_of(q) == K_VAR) ? q.rx : 0.0;
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
-                            double dsT, r3;
-                            slot_rhs(q, k, f, r, corr, smu, dsT, r3);
-                            cf = fma((r ? -k.m1 : k.m0) * q.z[r] * q.is[r], r3, cf);
+                            double dsT = -q.s[r] * q.z[r];
+                            if (corr) dsT -= q.ds[r] * q.dz[r];
+                            dsT += smu;
+                            q.dsT[r] = dsT;
+                            const double rz = r ? (q.h[1] - q.s[1] + f) : (q.h[0] - q.s[0] - f);
+                            q.r3[r] = fma(-dsT, q.iz[r], rz);
+                            cf = fma((r ? -q.m[1] : q.m[0]) * q.z[r] * q.is[r], q.r3[r], cf);
                         }
                         cfs[t] = cf;
-                        CF[k.wr] = cf;
+                        CF[q.wr] = cf;
                     }
                 }
                 if (NW > 1) SYNC();             // other waves' plain stores land before the VEL adds
                 if (nl)
 #pragma unroll
                     for (int t = 0; t < TS; t++)
-                        if (t < nts) {
-                            const SlotDesc d = slot_desc(sd, tid + NTH * t, S);
-                            if (d.kind == K_VEL)
-                                __hip_atomic_fetch_add(&CF[d.r], cfs[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
+                        if (t < nts && kind_of(Q[t]) == K_VEL)
+                            __hip_atomic_fetch_add(&CF[Q[t].r], cfs[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             };
             if (pc) {
                 // ---- weights W^-1 = z/s (updatekktmatrix, Auxilary.c:197-205), Lagrangian
                 //      Hessian -2 sum_j z_kj on (x_k, y_k) (NLP), and the predictor right-hand
                 //      side; one pass over the term rows assembles Z'HZ and Z'(rx + J'w)
                 SYNC();
-                double wv[TS];
 #pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    wv[t] = 0.0;
+                for (int t = 0; t < TS; t++)
                     if (t < nts) {
-                        const Slot &q = Q[t];
-                        SLOT_AT(t, nl);
-                        const double om = fma(k.m0 * q.z[0], q.is[0], k.m1 * q.z[1] * q.is[1]);
+                        Slot &q = Q[t];
+                        const double om = fma(q.m[0] * q.z[0], q.is[0], q.m[1] * q.z[1] * q.is[1]);
                         double hs = 0.0;
-                        if (nl && d.kind == K_VAR && d.i0 < 4 * N && !(d.i0 & 1)) {
-                            const int kk = d.i0 >> 2;
-                            for (int j = 0; j < K; j++) hs += zo[kk * K + j];
+                        if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
+                            const int k = q.i0 >> 2;
+                            for (int j = 0; j < K; j++) hs += zo[k * K + j];
                             hs *= -2.0;
                         }
-                        W[k.wr] = om + ((d.kind == K_VAR) ? k.a0 + hs : 0.0);
-                        wv[t] = q.z[0] * q.is[0] + q.z[1] * q.is[1];
+                        W[q.wr] = om + ((kind_of(q) == K_VAR) ? q.a0 + hs : 0.0);
                     }
-                }
                 if (NW > 1) SYNC();
                 if (nl)
 #pragma unroll
                     for (int t = 0; t < TS; t++)
-                        if (t < nts) {
-                            const SlotDesc d = slot_desc(sd, tid + NTH * t, S);
-                            if (d.kind == K_VEL)
-                                __hip_atomic_fetch_add(&W[d.r], wv[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        }
+                        if (t < nts && kind_of(Q[t]) == K_VEL)
+                            __hip_atomic_fetch_add(&W[Q[t].r], Q[t].z[0] * Q[t].is[0] + Q[t].z[1] * Q[t].is[1], __ATOMIC_RELAXED,
+                                                   __HIP_MEMORY_SCOPE_WORKGROUP);
                 set_rhs(0);
                 SYNC();
                 gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
@@ -914,24 +863,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 la_solve<NZL>(Mi, Hsv, vg, vy, vr, vd, dxi, nz, lane);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
-                const double smu = (pass == 0) ? 0.0 : (pc ? sigma * mu : sigma_d * mu);
-                const bool corr = pass == 1 && pc;
                 double mxs = 0.0, mxz = 0.0;
 #pragma unroll
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        SLOT_AT(t, nl);
-                        const double f = slot_f(d, k, xs, s_var);
-                        q.jd = row_dot<NZL>(R + d.r * LDR, dxi);
-                        double dsT[2], r3[2];
-#pragma unroll
-                        for (int r = 0; r < 2; r++) slot_rhs(q, k, f, r, corr, smu, dsT[r], r3[r]);
+                        q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
-                            const double m = r ? k.m1 : k.m0;
-                            q.dz[r] = m * q.z[r] * q.is[r] * fma(r ? -1.0 : 1.0, q.jd, -r3[r]);
-                            q.ds[r] = m * fma(-q.s[r], q.dz[r], dsT[r]) * q.iz[r];
+                            q.dz[r] = q.m[r] * q.z[r] * q.is[r] * fma(r ? -1.0 : 1.0, q.jd, -q.r3[r]);
+                            q.ds[r] = q.m[r] * fma(-q.s[r], q.dz[r], q.dsT[r]) * q.iz[r];
                             mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
                         }
                     }
@@ -951,9 +892,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     for (int t = 0; t < TS; t++)
                         if (t < nts) {
                             const Slot &q = Q[t];
-                            SLOT_AT(t, nl);
-                            num = fma(k.m0 * fma(ap, q.ds[0], q.s[0]), fma(ad, q.dz[0], q.z[0]), num);
-                            num = fma(k.m1 * fma(ap, q.ds[1], q.s[1]), fma(ad, q.dz[1], q.z[1]), num);
+                            num = fma(q.m[0] * fma(ap, q.ds[0], q.s[0]), fma(ad, q.dz[0], q.z[0]), num);
+                            num = fma(q.m[1] * fma(ap, q.ds[1], q.s[1]), fma(ad, q.dz[1], q.z[1]), num);
                         }
                     {
                         double rv[1] = {num};
@@ -971,18 +911,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 NLPDBG(iter, 4, ap); NLPDBG(iter, 5, ad); NLPDBG(iter, 6, delta); NLPDBG(iter, 7, sigma);
                 // rx' = (1-ad) rx + (ad-ap) P dx + ad (hess + delta) dx - (J(x') - J(x))' z'
                 // (hess from the old obstacle duals in zo, the Jacobian change from the new ones)
-                double hso[TS], fo[TS];
+                double hso[TS];
 #pragma unroll
                 for (int t = 0; t < TS; t++) {
-                    hso[t] = 0.0; fo[t] = 0.0;
+                    hso[t] = 0.0;
                     if (t < nts) {
                         Slot &q = Q[t];
-                        const SlotDesc d = slot_desc(sd, tid + NTH * t, S);
-                        if (nl && d.kind == K_VAR && d.i0 < 4 * N && !(d.i0 & 1)) {
-                            const int kk = d.i0 >> 2;
-                            for (int j = 0; j < K; j++) hso[t] += zo[kk * K + j];
+                        if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
+                            const int k = q.i0 >> 2;
+                            for (int j = 0; j < K; j++) hso[t] += zo[k * K + j];
                         }
-                        fo[t] = xs[d.i0];
 #pragma unroll
                         for (int r = 0; r < 2; r++) { q.s[r] = fma(ap, q.ds[r], q.s[r]); q.z[r] = fma(ad, q.dz[r], q.z[r]); }
                     }
@@ -992,12 +930,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        SLOT_AT(t, nl);
-                        if (nl && d.kind == K_OBS) zo[d.r - rO] = q.z[0];
-                        if (d.kind == K_VAR) {
-                            q.rx = (1.0 - ad) * q.rx + ((ad - ap) * k.a0) * q.jd;
+                        if (nl && kind_of(q) == K_OBS) zo[q.r - rO] = q.z[0];
+                        if (kind_of(q) == K_VAR) {
+                            q.rx = (1.0 - ad) * q.rx + ((ad - ap) * q.a0) * q.jd;
                             if (nl) q.rx = fma(ad * (delta - 2.0 * hso[t]), q.jd, q.rx);
-                            xs[d.i0] = fma(ap, q.jd, fo[t]);
+                            xs[q.i0] = fma(ap, q.jd, fv[t]);
                         }
                     }
                 SYNC();
@@ -1006,11 +943,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     for (int t = 0; t < TS; t++)
                         if (t < nts) {
                             Slot &q = Q[t];
-                            const SlotDesc d = slot_desc(sd, tid + NTH * t, S);
-                            if (d.kind == K_VAR && d.i0 < 4 * N && !(d.i0 & 1)) {   // +2 ap dx sum_j z'_kj on (x_k, y_k)
-                                const int kk = d.i0 >> 2;
+                            if (kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {   // +2 ap dx sum_j z'_kj on (x_k, y_k)
+                                const int k = q.i0 >> 2;
                                 double hs_new = 0.0;
-                                for (int j = 0; j < K; j++) hs_new += zo[kk * K + j];
+                                for (int j = 0; j < K; j++) hs_new += zo[k * K + j];
                                 q.rx = fma(2.0 * ap * hs_new, q.jd, q.rx);
                             }
                         }
@@ -1029,14 +965,13 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double f = 0.0;
 #pragma unroll
     for (int t = 0; t < TS; t++) {
-        SLOT_AT(t, true);
-        if (d.kind == K_VAR) {
-            const double xv = xs[d.i0];
-            x_out[(size_t)agent * n + d.i0] = xv;
-            f += fma(0.5 * k.a0 * xv, xv, k.a1 * xv);
+        const Slot &q = Q[t];
+        if (q.kind == K_VAR) {
+            const double xv = xs[q.i0];
+            x_out[(size_t)agent * n + q.i0] = xv;
+            f += fma(0.5 * q.a0 * xv, xv, q.a1 * xv);
         }
     }
-#undef SLOT_AT
     {
         double rv[1] = {f};
         wred_x<1, 0u, NW>(rv, red + 6 * 4 * NW, tid);
@@ -1062,7 +997,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 }
 
 #define SRB_NMPC_KERNEL(NZL, TS, NW)                                                                           \
-    extern "C" __global__ void __launch_bounds__(64 * NW) srb_nmpc_kernel_##NZL##_##TS##_##NW(                \
+    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE srb_nmpc_kernel_##NZL##_##TS##_##NW(        \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \

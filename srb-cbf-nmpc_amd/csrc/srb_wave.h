@@ -153,13 +153,16 @@ __device__ __forceinline__ double bc16(double v, int k)
 // step is one multiplier and one FMA per entry.  The pivots are those of LDL' in natural
 // order, so pivot <= 0 <=> not positive definite; regularise != 0 applies iSWIFT's dynamic
 // pivot regularisation (ldl.c:320-321: |D_kk| <= 1e-14 -> 1e-7).  Returns 0 on success.
-template <int NZL>
-__device__ __forceinline__ int gj_invert_dpp(double (&A)[NZL], int lane, int regularise);
-
+// Rows may be replicated: with NZL <= 16 (and SRB_USE_DPP) every 16-lane row of the wave holds
+// the whole matrix (lane l: matrix row l & 15) for the DPP solves that follow (la_solve); the
+// broadcasts read the first copy, and each copy applies the same operations (bit-identical).
+// A DPP row_newbcast form of this elimination (gj_invert_dpp) measured slower on MI355X: 3546
+// against 3062 cycles for NZL = 12 (tools/ubench/gj_bench.hip), since readlane broadcasts land
+// in SGPRs that the row updates read for free while the DPP copies cost a VALU move each.
 template <int NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
-    if constexpr (NZL <= 16 && SRB_USE_DPP) return gj_invert_dpp<NZL>(A, lane, regularise);
+    if constexpr (NZL <= 16 && SRB_USE_DPP) lane &= 15;
     // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
     // elimination is one basic block: the scheduler overlaps step k's row updates with the
     // broadcast of row k+1, whose entries are updated first.

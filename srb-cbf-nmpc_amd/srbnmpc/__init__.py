@@ -19,7 +19,8 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "libsrbnmpc.so")
+# SRBNMPC_LIB names an alternative build in this directory (diagnostic A/B runs only)
+LIB_PATH = os.path.join(_HERE, os.environ.get("SRBNMPC_LIB", "libsrbnmpc.so"))
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
