@@ -242,6 +242,7 @@ def main():
     ap.add_argument("--agents", type=int, default=0, help="agents per GPU (override)")
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
+    ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py); default profiles/r02_pmc_traffic_c<config>.json")
     args = ap.parse_args()
@@ -284,6 +285,7 @@ def main():
                status=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
                iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev))
     solver = srbnmpc.BatchSolver(p, n_loc, local_rank)
+    solver.set_waves(args.waves)
     # one explicit stream for the collective, both kernels and the timing events (the C ABI
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)
@@ -360,7 +362,7 @@ def main():
                      "cycles_per_iter_note": "solve-kernel HIP-event time x 2.4 GHz / IPM iterations (QP + NLP) of "
                                              "the slowest agent: the critical-path cost of one iteration; per-phase "
                                              "split in profiles/r02_*_stamps.txt",
-                     "kernel": "srb_nmpc_kernel", "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
+                     "kernel": "srb_nmpc_kernel", "waves_per_agent": solver.waves(), "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
                      "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
                                    "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
                                    "agent), neither MFMA- nor HBM-throughput-bound",

@@ -27,8 +27,15 @@
 /* initial inequality duals: 100, the scale of the tracking weights' multipliers (against 1:
  * 20-25 % fewer NLP iterations on the bench/test workloads, profiles/r01_nlp_z0_scan.txt) */
 #define ORC_NLP_Z0 100.0
-/* a step shorter than this from a near-optimal iterate ends the NLP as ACCEPTABLE (4) */
-#define ORC_NLP_BLOCKED 0.05
+/* OPTIMAL also needs the last primal step max|ap dx| below this: the residual tests alone
+ * (dual residual scaled by max(1, |Q x + f|_inf)) left 73 of 2048 N = 20 solves 1e-4..5e-4
+ * from the optimum along flat directions; with the step test every one is within 2.1e-5
+ * (profiles/r02_nlp_exit.txt) */
+#define ORC_NLP_DXTOL 3e-5
+/* ... and after this many near-optimal iterates (primal and complementarity tests met, dual
+ * residual within 100x of its threshold) without meeting both, the solve is at its round-off
+ * floor: ACCEPTABLE (4) at the current iterate */
+#define ORC_NLP_NEARWAIT 4
 
 typedef struct {
     int n, p, mq, K, N, mo, mv, m;
@@ -183,6 +190,16 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
 
     const double tol = pp->tol, th = tol / sqrt(3.0);
     const int trace = getenv("ORC_NLP_TRACE") != NULL;     /* diagnostics: per-iteration line on stderr */
+    /* diagnostics: ORC_NLP_EXIT="fx fmu acc" scales the dual-residual threshold, the
+     * complementarity threshold and the ACCEPTABLE window (exploration of exit rules only) */
+    double fx = 1.0, fmu = 1.0, facc = 100.0, fdx = ORC_NLP_DXTOL;
+    if (getenv("ORC_NLP_EXIT")) sscanf(getenv("ORC_NLP_EXIT"), "%lf %lf %lf %lf", &fx, &fmu, &facc, &fdx);
+    double dxlast = 1e300;                                  /* max |ap dx| of the last update */
+    int npassed = 0;                                        /* near-optimal iterates so far */
+    int saved = 0, restore = 0;                             /* last near-optimal iterate since the residual tests passed */
+    double *xsave = malloc(sizeof(double) * n);
+    int nearwait = ORC_NLP_NEARWAIT;
+    if (getenv("ORC_NLP_NEARWAIT")) nearwait = atoi(getenv("ORC_NLP_NEARWAIT"));
     double tr_sigma = 0.0;
     for (int iter = 0; iter < pp->nlp_maxit; iter++) {
         rows_eval(&P, x, g, Jv, Ji);
@@ -197,11 +214,17 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
          * QP stage keeps iSWIFT's absolute test): max(1, ||Q x + f||_inf) */
         double gmax = 1.0;
         for (int j = 0; j < n; j++) { double gj = fabs(Pd[j] * x[j] + c[j]); if (gj > gmax) gmax = gj; }
-        if (nrx < th * gmax && nrz < th && nry < th && sz / m < tol) { flag = 0; break; }
+        const int pass = nrx < fx * th * gmax && nrz < th && nry < th && sz / m < fmu * tol;
+        if (pass && dxlast < fdx) { flag = 0; break; }
         /* near the optimum: primal and complementarity met, dual residual within 100x of its
          * threshold.  An inertia shift or a blocked step from here is the condensed system's
          * round-off (W = z/s ~ 1e14 swamps the soft curvature), not progress: ACCEPTABLE (4) */
-        const int near = nrz < th && nry < th && sz / m < tol && nrx < 100.0 * th * gmax;
+        const int near = nrz < th && nry < th && sz / m < fmu * tol && nrx < facc * fx * th * gmax;
+        /* a solve that passed the residual tests and then left the near-optimal region is past
+         * its round-off floor: ACCEPTABLE at the last near-optimal iterate */
+        if (saved && !near) { restore = 1; flag = 4; break; }
+        if (near && (saved || pass)) { memcpy(xsave, x, sizeof(double) * n); saved = 1; }
+        if (near && ++npassed >= nearwait) { flag = 4; break; }
         for (int r = 0; r < m; r++) { lam[r] = sqrt(s[r] * z[r]); wgt[r] = s[r] / z[r]; }
         double mu = dotv(lam, lam, m) / m;
 
@@ -245,7 +268,6 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             delta = (delta == 0.0) ? dstart : delta * 10.0;
         }
         if (!ok) { flag = 1; break; }
-        if (near && delta != 0.0) { flag = 4; break; }
         /* full-space KKT [H + delta I, A'; A, 0] */
         memset(K, 0, sizeof(double) * dim * dim);
         for (int i = 0; i < n; i++) { for (int j = 0; j < n; j++) K[i * dim + j] = Hl[i * n + j]; K[i * dim + i] += delta; }
@@ -289,15 +311,17 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         if (trace)
             fprintf(stderr, "  %2d %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e\n", iter, nrx, th * gmax, nrz, sz / m,
                     ap, ad, delta, tr_sigma);
-        if (near && (ap < ORC_NLP_BLOCKED || ad < ORC_NLP_BLOCKED)) { flag = 4; break; }
         ap = 0.99 * ap < 1.0 ? 0.99 * ap : 1.0;
         ad = 0.99 * ad < 1.0 ? 0.99 * ad : 1.0;
-        for (int j = 0; j < n; j++) { x[j] += ap * dx[j]; q[j] += ad * dq[j]; }
+        dxlast = 0.0;
+        for (int j = 0; j < n; j++) { x[j] += ap * dx[j]; q[j] += ad * dq[j]; dxlast = fmax(dxlast, fabs(ap * dx[j])); }
         for (int r = 0; r < m; r++) { s[r] += ap * dsv[r]; z[r] += ad * dz[r]; }
         it++;
     }
+    if (restore || (flag == 2 && saved)) { memcpy(x, xsave, sizeof(double) * n); flag = 4; }
     memcpy(x_out, x, sizeof(double) * n);
     if (iters_out) *iters_out = it;
+    free(xsave);
     free(P.gnz); free(P.gval); free(hh); free(x); free(q); free(s); free(z); free(g); free(Jv); free(Ji);
     free(rx); free(ry); free(rz); free(lam); free(wgt); free(ds); free(dsv); free(dz); free(r3); free(K); free(Hl);
     free(rhs); free(dx); free(dq); free(hdiag); free(Z); free(Hr); free(HZ); free(piv);

@@ -11,9 +11,12 @@
 // NLP from 10.4-11.4 to 8.0-8.6 iterations on average and from 13-18 to 9-13 at most
 // (profiles/r01_nlp_z0_scan.txt) against z = 1.
 #define SRB_NLP_Z0 100.0
-// NLP stage: a step (primal or dual) shorter than this from a near-optimal iterate ends the
-// solve as ACCEPTABLE, status 4 (oracle ORC_NLP_BLOCKED)
-#define SRB_NLP_BLOCKED 0.05
+// NLP stage: OPTIMAL also needs the last primal step max |ap dx| below this (oracle
+// ORC_NLP_DXTOL): the residual tests alone left 3.6 % of N = 20 solves 1e-4..5e-4 from the
+// optimum along flat directions (profiles/r02_nlp_exit.txt); after SRB_NLP_NEARWAIT
+// near-optimal iterates without meeting both, the solve is at its round-off floor: ACCEPTABLE
+#define SRB_NLP_DXTOL 3e-5
+#define SRB_NLP_NEARWAIT 4
 
 struct SrbKParams {
     int N, C, K_obs, K_nbr;
@@ -54,9 +57,9 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
     const int q = 16 * NW;
     const int TT = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + srb_r4(NK) + q - 1) / q * q;
-    const int red = (NW > 1) ? 8 * 4 * NW : 0;
+    const int red = (NW > 1) ? 8 * 8 * NW : 0;
     const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 2 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
+    return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
            srb_r4(NK) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64

@@ -444,13 +444,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM;
     double *xs = p; p += n4;                            // current x
     double *xb = p; p += n4;                            // xbar
+    double *xsv = p; p += n4;                           // NLP: last near-optimal iterate (restored at the round-off floor)
     double *ref = p; p += 4 * N;
     double *foot = p; p += 2 * C * N;
     double *obs = p; p += 2 * NK + 2;
     double *eps = p; p += K + 1;
     double *zo = p; p += NK4;                           // obstacle duals (per-grid sums)
     int *sel = (int *)p; p += (K + 1);
-    double *red = p; p += (NW > 1) ? 8 * 4 * NW : 0;      // cross-wave reduction scratch, 8 sites
+    double *red = p; p += (NW > 1) ? 8 * 8 * NW : 0;      // cross-wave reduction scratch, 8 sites of <= 8 values
     double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   // partial Gram / rhs
 #ifdef SRB_STAMPS
     unsigned long long *stamp_lds = (unsigned long long *)p; p += SRB_NSTAMP;
@@ -604,7 +605,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.m[1] != 0.0) { mn = fmin(mn, z1); mx = fmax(mx, z1); }
                 }
             double rv[2] = {-mn, mx};
-            wred_x<2, 3u, NW>(rv, red + 0 * 4 * NW, tid);
+            wred_x<2, 3u, NW>(rv, red + 0 * 8 * NW, tid);
             mn = -rv[0]; mx = rv[1];
             const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn, zsh = (mx < 0) ? 0.0 : 1.0 + mx;
             SYNC();                                           // every lane has read xs = xbar
@@ -663,7 +664,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 }
             {
                 double rv[1] = {-mn};
-                wred_x<1, 1u, NW>(rv, red + 1 * 4 * NW, tid);
+                wred_x<1, 1u, NW>(rv, red + 1 * 8 * NW, tid);
                 mn = -rv[0];
             }
             const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn;
@@ -709,6 +710,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double sigma_d = 0.0;
         int flag = 2, it = 0;
         const double inv_m = 1.0 / (double)mrows;
+        double dxl = 1e300;              // this lane's max |ap dx| over its variable slots, last update
+        int npassed = 0;                 // NLP: near-optimal iterates so far
+        bool saved = false, restore = false;   // NLP: xsv holds the last near-optimal iterate since the residual tests passed
         for (int iter = 0; iter < maxit; iter++) {
             STAMP_BEGIN();
             // ---- residuals (computeresiduals, Auxilary.c:524-553), norms, reciprocals
@@ -740,10 +744,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     }
                 }
             }
+            double dxm;
             {
-                double rv[4] = {nrx, nrz, sz, gm};
-                wred_x<4, 8u, NW>(rv, red + 2 * 4 * NW, tid);
-                nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3];
+                double rv[5] = {nrx, nrz, sz, gm, dxl};
+                wred_x<5, 24u, NW>(rv, red + 2 * 8 * NW, tid);
+                nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3]; dxm = rv[4];
             }
             const double mu = sz * inv_m;
             STAMP_END(3);
@@ -751,13 +756,21 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
             const double thx = nl ? th * gm : th;
             NLPDBG(iter, 0, nrx); NLPDBG(iter, 1, thx); NLPDBG(iter, 2, nrz); NLPDBG(iter, 3, sz * inv_m);
-            if (nrx < thx && nrz < th && sz * inv_m < tol) { flag = 0; break; }
+            const bool pass = nrx < thx && nrz < th && sz * inv_m < tol;
+            if (pass && (!nl || dxm < SRB_NLP_DXTOL)) { flag = 0; break; }
             // NLP near the optimum (primal and complementarity met, dual residual within 100x):
             // an inertia shift or a blocked step from here is round-off of the condensed
             // system (W = z/s ~ 1e14 swamps the soft curvature in Z'HZ), not progress -> exit
             // ACCEPTABLE (4) at this iterate (oracle/nlp_ipm.c, the same rule)
             const bool near = nl && nrz < th && sz * inv_m < tol && nrx < 100.0 * thx;
-            bool acc = false;
+            // a solve that passed the residual tests and then left the near-optimal region is
+            // past its round-off floor: ACCEPTABLE at the last near-optimal iterate (oracle, same rule)
+            if (nl && saved && !near) { restore = true; flag = 4; break; }
+            if (near && (saved || pass)) {         // each thread copies the variables it owns
+                for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
+                saved = true;
+            }
+            if (near && ++npassed >= SRB_NLP_NEARWAIT) { flag = 4; break; }
             const bool pc = nl || (sigma > sigma_d);
             double delta = 0.0;
             // right-hand side of pass (0 predictor, 1 corrector / centring):
@@ -844,7 +857,6 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 }
                 STAMP_END(5);
                 if (!ok) { flag = 1; break; }
-                if (near && delta != 0.0) { flag = 4; break; }
             }
             const double *Hsv = (delta != 0.0) ? HS : H0;
 
@@ -879,7 +891,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 // findsteplength (Auxilary.c:271-294): 1 / max(-dv / v), 1 when no dv < 0
                 {
                     double rv[2] = {mxs, mxz};
-                    wred_x<2, 3u, NW>(rv, red + (3 + 2 * pass) * 4 * NW, tid);
+                    wred_x<2, 3u, NW>(rv, red + (3 + 2 * pass) * 8 * NW, tid);
                     mxs = rv[0]; mxz = rv[1];
                 }
                 ap = (mxs > 0.0) ? 1.0 / mxs : 1.0;
@@ -897,17 +909,17 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                     {
                         double rv[1] = {num};
-                        wred_x<1, 0u, NW>(rv, red + 4 * 4 * NW, tid);
+                        wred_x<1, 0u, NW>(rv, red + 4 * 8 * NW, tid);
                         num = rv[0];
                     }
                     const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
                     sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
                     continue;
                 }
-                if (near && (ap < SRB_NLP_BLOCKED || ad < SRB_NLP_BLOCKED)) { acc = true; break; }
                 // ---- update (Prime.c:208-216): step 0.99 alpha capped at 1
                 ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
                 ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
+                dxl = 0.0;
                 NLPDBG(iter, 4, ap); NLPDBG(iter, 5, ad); NLPDBG(iter, 6, delta); NLPDBG(iter, 7, sigma);
                 // rx' = (1-ad) rx + (ad-ap) P dx + ad (hess + delta) dx - (J(x') - J(x))' z'
                 // (hess from the old obstacle duals in zo, the Jacobian change from the new ones)
@@ -932,6 +944,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         Slot &q = Q[t];
                         if (nl && kind_of(q) == K_OBS) zo[q.r - rO] = q.z[0];
                         if (kind_of(q) == K_VAR) {
+                            dxl = fmax(dxl, fabs(ap * q.jd));
                             q.rx = (1.0 - ad) * q.rx + ((ad - ap) * q.a0) * q.jd;
                             if (nl) q.rx = fma(ad * (delta - 2.0 * hso[t]), q.jd, q.rx);
                             xs[q.i0] = fma(ap, q.jd, fv[t]);
@@ -952,8 +965,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                 STAMP_END(14);
             }
-            if (acc) { flag = 4; break; }
             it++;
+        }
+        if (nl && (restore || (flag == 2 && saved))) {
+            for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];     // owner threads, as saved
+            flag = 4;
         }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
     }
@@ -974,7 +990,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     }
     {
         double rv[1] = {f};
-        wred_x<1, 0u, NW>(rv, red + 6 * 4 * NW, tid);
+        wred_x<1, 0u, NW>(rv, red + 6 * 8 * NW, tid);
         f = rv[0];
     }
     // ---- fitComTrajectory_eventbase (MPC_dist.cpp:784-855) as an epilogue: alpha_COM (4 x 5)

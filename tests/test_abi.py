@@ -31,7 +31,8 @@ def test_library_contains_gfx950_code_object():
     assert b"gfx950" in data
     import re
     hdr = open(os.path.join(ROOT, "srb-cbf-nmpc_amd", "csrc", "srb_kernel_params.h")).read()
-    inst = re.findall(r"X\((\d+), (\d+), (\d+)\)", hdr.split("#define SRB_KERNEL_INSTANCES(X)")[1].split("\n\n")[0])
+    # the product list (the #else branch; SRB_DEV_INSTANCES builds only a few for register reports)
+    inst = re.findall(r"X\((\d+), (\d+), (\d+)\)", hdr.split("#define SRB_KERNEL_INSTANCES(X) \\")[1].split("#endif")[0])
     assert len(inst) >= 4 and any(nw == "4" for _, _, nw in inst)
     for nzl, ts, nw in inst:                  # every register-bound instance is in the code object
         assert f"srb_nmpc_kernel_{nzl}_{ts}_{nw}".encode() in data
