@@ -27,6 +27,8 @@
 /* initial inequality duals: 100, the scale of the tracking weights' multipliers (against 1:
  * 20-25 % fewer NLP iterations on the bench/test workloads, profiles/r01_nlp_z0_scan.txt) */
 #define ORC_NLP_Z0 100.0
+/* a step shorter than this from a near-optimal iterate ends the NLP as ACCEPTABLE (4) */
+#define ORC_NLP_BLOCKED 0.05
 /* OPTIMAL also needs the last primal step max|ap dx| below this: the residual tests alone
  * (dual residual scaled by max(1, |Q x + f|_inf)) left 73 of 2048 N = 20 solves 1e-4..5e-4
  * from the optimum along flat directions; with the step test every one is within 2.1e-5
@@ -268,6 +270,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
             delta = (delta == 0.0) ? dstart : delta * 10.0;
         }
         if (!ok) { flag = 1; break; }
+        if (near && delta != 0.0) { flag = 4; break; }
         /* full-space KKT [H + delta I, A'; A, 0] */
         memset(K, 0, sizeof(double) * dim * dim);
         for (int i = 0; i < n; i++) { for (int j = 0; j < n; j++) K[i * dim + j] = Hl[i * n + j]; K[i * dim + i] += delta; }
@@ -311,6 +314,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         if (trace)
             fprintf(stderr, "  %2d %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e %10.3e\n", iter, nrx, th * gmax, nrz, sz / m,
                     ap, ad, delta, tr_sigma);
+        if (near && (ap < ORC_NLP_BLOCKED || ad < ORC_NLP_BLOCKED)) { flag = 4; break; }
         ap = 0.99 * ap < 1.0 ? 0.99 * ap : 1.0;
         ad = 0.99 * ad < 1.0 ? 0.99 * ad : 1.0;
         dxlast = 0.0;

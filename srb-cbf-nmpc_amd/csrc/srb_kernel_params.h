@@ -11,6 +11,9 @@
 // NLP from 10.4-11.4 to 8.0-8.6 iterations on average and from 13-18 to 9-13 at most
 // (profiles/r01_nlp_z0_scan.txt) against z = 1.
 #define SRB_NLP_Z0 100.0
+// NLP stage: a step (primal or dual) shorter than this from a near-optimal iterate ends the
+// solve as ACCEPTABLE, status 4 (oracle ORC_NLP_BLOCKED)
+#define SRB_NLP_BLOCKED 0.05
 // NLP stage: OPTIMAL also needs the last primal step max |ap dx| below this (oracle
 // ORC_NLP_DXTOL): the residual tests alone left 3.6 % of N = 20 solves 1e-4..5e-4 from the
 // optimum along flat directions (profiles/r02_nlp_exit.txt); after SRB_NLP_NEARWAIT

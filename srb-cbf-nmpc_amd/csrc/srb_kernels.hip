@@ -771,6 +771,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 saved = true;
             }
             if (near && ++npassed >= SRB_NLP_NEARWAIT) { flag = 4; break; }
+            bool acc = false;
             const bool pc = nl || (sigma > sigma_d);
             double delta = 0.0;
             // right-hand side of pass (0 predictor, 1 corrector / centring):
@@ -857,6 +858,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 }
                 STAMP_END(5);
                 if (!ok) { flag = 1; break; }
+                if (near && delta != 0.0) { flag = 4; break; }
             }
             const double *Hsv = (delta != 0.0) ? HS : H0;
 
@@ -916,6 +918,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     sigma = mr * mr * mr; if (sigma < sigma_d) sigma = sigma_d;
                     continue;
                 }
+                if (near && (ap < SRB_NLP_BLOCKED || ad < SRB_NLP_BLOCKED)) { acc = true; break; }
                 // ---- update (Prime.c:208-216): step 0.99 alpha capped at 1
                 ap = (0.99 * ap < 1.0) ? 0.99 * ap : 1.0;
                 ad = (0.99 * ad < 1.0) ? 0.99 * ad : 1.0;
@@ -965,6 +968,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                 STAMP_END(14);
             }
+            if (acc) { flag = 4; break; }
             it++;
         }
         if (nl && (restore || (flag == 2 && saved))) {
