@@ -243,6 +243,9 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
+    ap.add_argument("--emulate-shards", type=int, default=1,
+                    help="diagnostic: solve rank 0's shard of a swarm this many GPUs wide on one GPU (the whole "
+                         "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py); default profiles/r02_pmc_traffic_c<config>.json")
     args = ap.parse_args()
@@ -264,11 +267,13 @@ def main():
     cfg = dict(CONFIGS[args.config])
     A_local = args.agents or cfg["agents"]
     A_total = A_local * world
+    if args.emulate_shards > 1 and world == 1:
+        A_total = A_local * args.emulate_shards
     N, C = cfg["N"], cfg["C"]
     p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
     # the whole swarm is generated identically on every rank; each rank keeps its shard
     b = workload.make_batch(A_total, N, C, seed=1234)
-    lo, hi = sdist.shard_range(A_total, world, rank)
+    lo, hi = sdist.shard_range(A_total, max(world, args.emulate_shards), rank)
     sh = {k: (v[lo:hi] if k not in ("obstacles", "nbr_state") else v) for k, v in b.items()}
     t = {k: torch.as_tensor(np.ascontiguousarray(v).reshape(v.shape[0], -1), dtype=torch.float64, device=dev)
          for k, v in sh.items()}
@@ -296,7 +301,7 @@ def main():
     def step():
         nb = exchange(nbr_local) if exchange is not None else nbr_all
         solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nb, out, agent_offset=lo,
-                            stream=stream.cuda_stream, alpha_buf=alpha_buf)
+                            stream=stream.cuda_stream, alpha_buf=alpha_buf, obstacles_version=1)
 
     for _ in range(args.warmup):
         step()
@@ -328,7 +333,7 @@ def main():
         dist.all_gather(gl, lat)
         per_step = torch.cat(gl).cpu().numpy()
     ms_per_step = elapsed * 1e3 / args.steps
-    value = A_total * args.steps / elapsed
+    value = (hi - lo) * world * args.steps / elapsed if args.emulate_shards > 1 else A_total * args.steps / elapsed
 
     status = out["status"].cpu().numpy(); iters = out["iters"].cpu().numpy()
     solve_ms = float(np.median([k[1] for k in kern]))
@@ -351,7 +356,9 @@ def main():
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
         "vs_baseline": None, "dtype": "f64", "data": "synthetic",
         "config": {"workload": cfg["name"], "agents_per_gpu": A_local, "agents_total": A_total, "horizon": N,
-                   "contacts": C, "K_obs": cfg["K_obs"], "K_nbr": cfg["K_nbr"], "parallelism": f"agents sharded x{world}"},
+                   "contacts": C, "K_obs": cfg["K_obs"], "K_nbr": cfg["K_nbr"], "parallelism": f"agents sharded x{world}",
+                   "emulated_shards": args.emulate_shards, "n_obs": int(sh["obstacles"].shape[0]),
+                   "nbr_rows": int(A_total if cfg["K_nbr"] else 0)},
         "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
         "optimal_frac": float((status == 0).all(1).mean()),
         "acceptable_frac": float(((status[:, 0] == 0) & (status[:, 1] == 4)).mean()),

@@ -100,6 +100,9 @@ typedef struct srb_batch {
     const double *alpha_buf;
     double *alpha;
     int *sel;
+    int obstacles_version;   /* != 0: the obstacle table is unchanged since the last call that passed
+                                this version, pointer and n_obs (the reference's Pobs_real is set once,
+                                MPC_dist::setPobs_real): its selection grid is reused; 0: rebuilt */
 } srb_batch;
 
 typedef struct srb_ctx srb_ctx;
@@ -123,10 +126,10 @@ int srb_solve_batch(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 
 /* Device buffers (all pointers in `dev_io` are device pointers), asynchronous on
- * `stream` (a hipStream_t).  NULL = the context's own stream, which is NOT ordered against
- * any other stream: the caller must then make the inputs visible (and the outputs free)
- * before the call, e.g. by a device synchronisation.  Pass the stream that produced the
- * inputs instead (the Python layer passes torch's current stream).  Call srb_sync(). */
+ * `stream` (a hipStream_t; NULL = the HIP null stream, which orders against every blocking
+ * stream, as the CUDA/HIP convention has it).  Pass the stream that produced the inputs (the
+ * Python layer passes torch's current stream, whose default is that null stream).  Call
+ * srb_sync() or synchronise the stream. */
 int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
 int srb_sync(srb_ctx *ctx);
 
@@ -161,7 +164,8 @@ int srb_prepare_batch_device(srb_ctx *ctx, int n_agents, const srb_prep *dev_io,
 
 /*
  * HL reference planner (generateReferenceTrajectory, MPC_dist.cpp:930-1104; SURVEY.md 8(f)
- * row 3) on HIP device `device`, host buffers, synchronous.  NA agents (1..1024) starting at
+ * row 3) on HIP device `device`, host buffers, synchronous.  NA agents (1..2^20; up to 1024 in
+ * one persistent workgroup, more -- one coupled swarm -- as one launch per step) starting at
  * Pstart [NA][2], planner obstacles Pobs [n_obs][2] (n_obs <= 2048), `loop` steps (reference:
  * 100000).  Outputs Pr_refined_ / Prd_refined_ as column-major 2NA x (loop / 40) arrays (the
  * layout setReferenceTrajectory / srb_prep take).  Returns 0 or a negative error code.
@@ -243,7 +247,7 @@ int srb_ll_ctx_create(const srb_ll_params *p, int max_agents, int device, srb_ll
 int srb_ll_ctx_destroy(srb_ll_ctx *ctx);
 /* host buffers: copies in, solves, copies out, synchronises */
 int srb_ll_calc_torque(srb_ll_ctx *ctx, int n_agents, const srb_ll_io *host_io);
-/* device buffers, asynchronous on `stream` (NULL = the context's stream); call srb_ll_sync() */
+/* device buffers, asynchronous on `stream` (NULL = the HIP null stream); call srb_ll_sync() */
 int srb_ll_calc_torque_device(srb_ll_ctx *ctx, int n_agents, const srb_ll_io *dev_io, void *stream);
 int srb_ll_sync(srb_ll_ctx *ctx);
 /* HIP-event time of the last srb_ll_calc_torque[_device] kernel on its stream (ms) */

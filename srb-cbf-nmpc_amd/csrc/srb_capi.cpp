@@ -26,9 +26,15 @@ SRB_KERNEL_INSTANCES(DECL_NMPC)
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
                               double *, const int *);
+struct SrbGrid;
 extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const double *obstacles, int n_obs,
                                           const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
-                                          int *sel_out);
+                                          int *sel_out, const SrbGrid *gob, const int *oob, const double2 *pob,
+                                          const int *iob, const SrbGrid *gnb, const int *onb, const double2 *pnb,
+                                          const int *inb);
+extern "C" __global__ void srb_grid_build_kernel(const double *tab0, int stride0, int n0, SrbGrid *g0, int *off0,
+                                                 double2 *spos0, int *sidx0, const double *tab1, int stride1, int n1,
+                                                 SrbGrid *g1, int *off1, double2 *spos1, int *sidx1);
 struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; };
 #define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
@@ -97,7 +103,29 @@ struct srb_ctx {
     bool timed;
     int last_nw;
     int nw;                        // waves per agent forced by srb_ctx_set_waves (0: automatic)
+    // selection grids (table 0: static obstacles, 1: neighbour snapshot), rebuilt per launch
+    struct grid_buf { void *g; int *off; double2 *spos; int *sidx; size_t cap; } grid[2];
+    const double *grid_src;        // obstacle table, row count and version the obstacle grid was built from
+    int grid_n, grid_ver;
 };
+
+// device buffers of selection grid t for a table of n rows (grown on demand)
+static int grid_reserve(srb_ctx *c, int t, size_t n)
+{
+    srb_ctx::grid_buf &b = c->grid[t];
+    if (!b.g) {
+        HIPCHK(hipMalloc(&b.g, 64));
+        HIPCHK(hipMalloc(&b.off, (SRB_GRID_CELLS + 1) * sizeof(int)));
+    }
+    if (n > b.cap) {
+        if (b.spos) HIPCHK(hipFree(b.spos));
+        if (b.sidx) HIPCHK(hipFree(b.sidx));
+        HIPCHK(hipMalloc(&b.spos, n * sizeof(double2)));
+        HIPCHK(hipMalloc(&b.sidx, n * sizeof(int)));
+        b.cap = n;
+    }
+    return SRB_OK;
+}
 
 extern "C" void srb_params_default(srb_params *p, int N, int C)
 {
@@ -224,6 +252,8 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     srb_ctx *c = new srb_ctx();
     c->p = *p; c->max_agents = max_agents; c->device = device;
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false; c->nw = 0; c->last_nw = 0;
+    for (auto &g : c->grid) g = srb_ctx::grid_buf{nullptr, nullptr, nullptr, nullptr, 0};
+    c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -252,6 +282,9 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
                     c->abuf, c->alpha, c->sel};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
+    for (auto &g : c->grid)
+        for (void *b : {g.g, (void *)g.off, (void *)g.spos, (void *)g.sidx})
+            if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
     (void)hipStreamDestroy(c->stream);
     delete c;
@@ -288,8 +321,27 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
     int *sel = d->sel ? d->sel : c->sel;
     if (use_nlp && k.K_obs + k.K_nbr > 0) {
+        // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
+        // with the arena) get a uniform grid so each agent scans only the cells around it
+        static const int min_rows = [] { const char *e = std::getenv("SRB_GRID_MIN_ROWS"); return e ? std::atoi(e) : SRB_GRID_MIN_ROWS; }();
+        const bool go = k.K_obs > 0 && n_obs >= min_rows, gn = k.K_nbr > 0 && n_all >= min_rows;
+        if (go) { int rc = grid_reserve(c, 0, n_obs); if (rc) return rc; }
+        if (gn) { int rc = grid_reserve(c, 1, n_all); if (rc) return rc; }
+        const srb_ctx::grid_buf &G0 = c->grid[0], &G1 = c->grid[1];
+        // a static obstacle table (same version, pointer and size) keeps its grid
+        const bool go_build = go && !(d->obstacles_version != 0 && d->obstacles_version == c->grid_ver &&
+                                      d->obstacles == c->grid_src && n_obs == c->grid_n);
+        if (go_build || gn) {
+            hipLaunchKernelGGL(srb_grid_build_kernel, dim3(2), dim3(1024), 0, s,
+                               d->obstacles, 2, n_obs, go_build ? (SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
+                               d->nbr_state, 4, n_all, gn ? (SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
+            HIPCHK(hipGetLastError());
+        }
+        if (go_build) { c->grid_src = d->obstacles; c->grid_n = n_obs; c->grid_ver = d->obstacles_version; }
         hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, d->x0, d->obstacles, n_obs,
-                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, sel);
+                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, sel,
+                           go ? (const SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
+                           gn ? (const SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
@@ -314,7 +366,7 @@ extern "C" int srb_ctx_waves(srb_ctx *c) { return c ? c->last_nw : 0; }
 extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch *dev_io, void *stream)
 {
     if (!c || !dev_io) return fail(SRB_ERR_ARG, "null argument");
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;          // NULL: the HIP null stream (ordered with blocking streams)
     return launch(c, n_agents, dev_io, s, c->p.use_nlp);
 }
 
@@ -334,7 +386,7 @@ extern "C" int srb_prepare_batch_device(srb_ctx *c, int n_agents, const srb_prep
         return fail(SRB_ERR_ARG, "missing buffer");
     if (d->n_rows < 2 || d->T < 1) return fail(SRB_ERR_ARG, "empty HL path");
     HIPCHK(hipSetDevice(c->device));
-    hipStream_t s = stream ? (hipStream_t)stream : c->stream;
+    hipStream_t s = (hipStream_t)stream;          // NULL: the HIP null stream (ordered with blocking streams)
     hipLaunchKernelGGL(srb_prepare_kernel, dim3((n_agents + 255) / 256), dim3(256), 0, s, n_agents, c->p.N, c->p.C,
                        d->n_rows, d->T, d->agent_offset, d->Pr, d->Prd, d->agent_id, d->gait_domain, d->contact,
                        d->toe, d->start, d->q, d->dq, d->x0, d->ref, d->foot, d->last_state, d->status);
@@ -345,10 +397,18 @@ extern "C" int srb_prepare_batch_device(srb_ctx *c, int n_agents, const srb_prep
 extern "C" __global__ void srb_hlplan_kernel(int NA, const double *Pstart, const double *Pobs, int n_obs, int loop,
                                              double *Pr, double *Prd);
 
+extern "C" __global__ void srb_hlplan_step_kernel(int NA, int i, int loop, const double *Pobs, int n_obs,
+                                                  const double *pos_cur, double *pos_next, double *st, double *Pr,
+                                                  double *Prd);
+
+// swarms up to this many agents run as one persistent workgroup (srb_hlplan_kernel); larger ones
+// one launch per step over NA / 64 workgroups (srb_hlplan_step_kernel); SRB_HL_STEP=1 forces the latter
+#define SRB_HL_ONE_WG 1024
+
 extern "C" int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr,
                            double *Prd)
 {
-    if (NA < 1 || NA > 1024) return fail(SRB_ERR_SIZE, "HL planner: 1 <= NA <= 1024 (one workgroup)");
+    if (NA < 1 || NA > (1 << 20)) return fail(SRB_ERR_SIZE, "HL planner: 1 <= NA <= 2^20");
     if (n_obs < 0 || n_obs > 2048 || (n_obs > 0 && !Pobs)) return fail(SRB_ERR_ARG, "HL planner: bad obstacle table");
     if (loop < 80 || !Pstart || !Pr || !Prd) return fail(SRB_ERR_ARG, "HL planner: bad arguments (loop >= 80)");
     int ndev = 0;
@@ -370,12 +430,35 @@ extern "C" int srb_hl_plan(int device, int NA, const double *Pstart, const doubl
         chk(hipMemcpy(dPs, Pstart, 2 * NA * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
         if (n_obs > 0) chk(hipMemcpy(dOb, Pobs, n_obs * 2 * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
     }
-    if (rc == SRB_OK) {
+    static const bool force_step = [] { const char *e = std::getenv("SRB_HL_STEP"); return e && std::atoi(e) == 1; }();
+    if (rc == SRB_OK && NA <= SRB_HL_ONE_WG && !force_step) {
         const int threads = ((NA + 63) / 64) * 64;
         const size_t lds = (4 * (size_t)NA + 2 * (size_t)n_obs) * sizeof(double);
         hipLaunchKernelGGL(srb_hlplan_kernel, dim3(1), dim3(threads), lds, 0, NA, dPs, dOb, n_obs, loop, dPr, dPrd);
         chk(hipGetLastError(), "srb_hlplan_kernel");
         chk(hipDeviceSynchronize(), "srb_hlplan_kernel");
+    } else if (rc == SRB_OK) {
+        // one coupled swarm across the chip: positions double-buffered in global memory
+        double *pos[2] = {nullptr, nullptr}, *st = nullptr;
+        chk(hipMalloc(&pos[0], 2 * (size_t)NA * sizeof(double)), "hipMalloc");
+        chk(hipMalloc(&pos[1], 2 * (size_t)NA * sizeof(double)), "hipMalloc");
+        chk(hipMalloc(&st, 4 * (size_t)NA * sizeof(double)), "hipMalloc");
+        if (rc == SRB_OK) {
+            double *h = (double *)std::calloc(4 * (size_t)NA, sizeof(double));
+            for (int a = 0; a < NA; a++) { h[4 * a] = Pstart[2 * a]; h[4 * a + 1] = Pstart[2 * a + 1]; }
+            chk(hipMemcpy(st, h, 4 * (size_t)NA * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+            chk(hipMemcpy(pos[0], Pstart, 2 * (size_t)NA * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
+            std::free(h);
+        }
+        const int blocks = (NA + 63) / 64;
+        for (int i = 0; i <= loop && rc == SRB_OK; i++) {
+            hipLaunchKernelGGL(srb_hlplan_step_kernel, dim3(blocks), dim3(64), 0, 0, NA, i, loop, dOb, n_obs, pos[i & 1],
+                               pos[(i & 1) ^ 1], st, dPr, dPrd);
+            if ((i & 1023) == 0) chk(hipGetLastError(), "srb_hlplan_step_kernel");
+        }
+        chk(hipDeviceSynchronize(), "srb_hlplan_step_kernel");
+        for (void *b : {(void *)pos[0], (void *)pos[1], (void *)st})
+            if (b) (void)hipFree(b);
     }
     if (rc == SRB_OK) {
         chk(hipMemcpy(Pr, dPr, out, hipMemcpyDeviceToHost), "hipMemcpy");
@@ -451,6 +534,7 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
         d.nbr_state = c->nbr;
     }
     d.sel = nullptr;                       // the context's scratch; copied out below when asked for
+    d.obstacles_version = 0;               // staged copy: rebuilt every call
     int rc = launch(c, n_agents, &d, s, use_nlp);
     if (rc) return rc;
     if (h->sel && use_nlp) {

@@ -1038,13 +1038,16 @@ SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
 // Obstacle and neighbour selection (MPC_dist.cpp:371-396, generalised to K): one workgroup per
 // agent, the K_obs nearest static obstacles (with the reference's 1000 m sentinel) and the
 // K_nbr nearest other agents to the agent's own CoM, indices to sel_out[agent][K_obs + K_nbr]
-// (-1: no neighbour row).  A kernel of its own
-// rather than a phase of the solve: there the scan ran at the solve kernel's occupancy, one
-// or two waves per CU, and took a quarter of the solve (profiles/r01_c3_stamps.txt).
+// (-1: no neighbour row).  A kernel of its own rather than a phase of the solve: there the
+// scan ran at the solve kernel's occupancy, one or two waves per CU, and took a quarter of
+// the solve (profiles/r01_c3_stamps.txt).  Tables of SRB_GRID_MIN_ROWS rows or more come with
+// a uniform grid (srb_grid_build_kernel) and only the cells around the agent are scanned.
 extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(int n_agents,
                 const double *__restrict__ x0g, const double *__restrict__ obstacles, int n_obs,
                 const double *__restrict__ nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
-                int *__restrict__ sel_out)
+                int *__restrict__ sel_out, const SrbGrid *__restrict__ gob, const int *__restrict__ oob,
+                const double2 *__restrict__ pob, const int *__restrict__ iob, const SrbGrid *__restrict__ gnb,
+                const int *__restrict__ onb, const double2 *__restrict__ pnb, const int *__restrict__ inb)
 {
     __shared__ double wd_lds[SRB_KNN_WAVES];
     __shared__ int wi_lds[SRB_KNN_WAVES];
@@ -1052,8 +1055,100 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
     if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
     const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
     int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);
-    if (K_obs > 0) knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds);
+    if (K_obs > 0)
+        knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds, gob, oob, pob, iob);
     if (K_nbr > 0)
         knn_select<SRB_KNN_WAVES>(tid, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, 0, sel + K_obs, wd_lds,
-                                  wi_lds);
+                                  wi_lds, gnb, onb, pnb, inb);
+}
+
+// Uniform grid over one table per workgroup (block 0: table 0, block 1: table 1), rebuilt every
+// launch (the neighbour snapshot moves every cycle): bounds of the finite rows, about two rows
+// per cell (at most SRB_GRID_CELLS cells), counts by LDS atomics, one exclusive scan, scatter of
+// the rows into cell order.  One workgroup of 1024 threads per table: a few microseconds for the
+// tens of thousands of rows of an 8-GPU swarm, against a brute-force scan per agent.
+__device__ __forceinline__ int grid_cell(double x, double y, double x0, double y0, double inv_h, int nx, int ny)
+{
+    const int cx = min(max((int)((x - x0) * inv_h), 0), nx - 1);
+    const int cy = min(max((int)((y - y0) * inv_h), 0), ny - 1);
+    return cy * nx + cx;
+}
+
+extern "C" __global__ void __launch_bounds__(1024) srb_grid_build_kernel(
+    const double *__restrict__ tab0, int stride0, int n0, SrbGrid *g0, int *off0, double2 *spos0, int *sidx0,
+    const double *__restrict__ tab1, int stride1, int n1, SrbGrid *g1, int *off1, double2 *spos1, int *sidx1)
+{
+    __shared__ int cnt[SRB_GRID_CELLS];
+    __shared__ double red[4][16];
+    __shared__ int part[1024];
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
+    const double *tab = blockIdx.x ? tab1 : tab0;
+    const int stride = blockIdx.x ? stride1 : stride0, n = blockIdx.x ? n1 : n0;
+    SrbGrid *g = blockIdx.x ? g1 : g0;
+    int *off = blockIdx.x ? off1 : off0;
+    double2 *spos = blockIdx.x ? spos1 : spos0;
+    int *sidx = blockIdx.x ? sidx1 : sidx0;
+    if (!g) return;
+    // bounds of the finite rows
+    double mnx = __builtin_inf(), mny = __builtin_inf(), mxx = -__builtin_inf(), mxy = -__builtin_inf();
+    for (int i = tid; i < n; i += 1024) {
+        const double x = tab[(size_t)stride * i], y = tab[(size_t)stride * i + 1];
+        if (isfinite(x) && isfinite(y)) { mnx = fmin(mnx, x); mny = fmin(mny, y); mxx = fmax(mxx, x); mxy = fmax(mxy, y); }
+    }
+    mnx = wmin(mnx); mny = wmin(mny); mxx = wmax(mxx); mxy = wmax(mxy);
+    if (lane == 0) { red[0][wv] = mnx; red[1][wv] = mny; red[2][wv] = mxx; red[3][wv] = mxy; }
+    __syncthreads();
+    mnx = red[0][0]; mny = red[1][0]; mxx = red[2][0]; mxy = red[3][0];
+    for (int w = 1; w < 16; w++) {
+        mnx = fmin(mnx, red[0][w]); mny = fmin(mny, red[1][w]); mxx = fmax(mxx, red[2][w]); mxy = fmax(mxy, red[3][w]);
+    }
+    if (!(mnx <= mxx)) {                           // no finite row: selection falls back to the scan
+        if (tid == 0) g->ok = 0;
+        return;
+    }
+    const double W = mxx - mnx, H = mxy - mny;
+    const int target = min(max(n / 2, 1), SRB_GRID_CELLS);
+    double h = sqrt(fmax(W * H, 1e-300) / target);
+    if (!(h > 0.0) || !isfinite(h)) h = 1.0;
+    h = fmax(h, fmax(W, H) / 4096.0);             // keeps nx, ny in range
+    int nx = (int)(W / h) + 1, ny = (int)(H / h) + 1;
+    while ((long long)nx * ny > SRB_GRID_CELLS) { h *= 1.25; nx = (int)(W / h) + 1; ny = (int)(H / h) + 1; }
+    const double inv_h = 1.0 / h;
+    const int C = nx * ny;
+    for (int c = tid; c < C; c += 1024) cnt[c] = 0;
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const double x = tab[(size_t)stride * i], y = tab[(size_t)stride * i + 1];
+        if (isfinite(x) && isfinite(y)) atomicAdd(&cnt[grid_cell(x, y, mnx, mny, inv_h, nx, ny)], 1);
+    }
+    __syncthreads();
+    // exclusive scan: per-thread chunk sums, a scan of the 1024 partials, chunk-local offsets
+    const int chunk = (C + 1023) / 1024, c0 = tid * chunk, c1 = min(c0 + chunk, C);
+    int sum = 0;
+    for (int c = c0; c < c1; c++) sum += cnt[c];
+    part[tid] = sum;
+    __syncthreads();
+    for (int o = 1; o < 1024; o <<= 1) {
+        const int v = (tid >= o) ? part[tid - o] : 0;
+        __syncthreads();
+        part[tid] += v;
+        __syncthreads();
+    }
+    int run = part[tid] - sum;                     // exclusive prefix of this chunk
+    for (int c = c0; c < c1; c++) { const int v = cnt[c]; cnt[c] = run; off[c] = run; run += v; }
+    if (tid == 1023) off[C] = part[1023];
+    __syncthreads();
+    for (int i = tid; i < n; i += 1024) {
+        const double x = tab[(size_t)stride * i], y = tab[(size_t)stride * i + 1];
+        if (isfinite(x) && isfinite(y)) {
+            const int at = atomicAdd(&cnt[grid_cell(x, y, mnx, mny, inv_h, nx, ny)], 1);
+            spos[at] = make_double2(x, y);
+            sidx[at] = i;
+        }
+    }
+    if (tid == 0) {
+        SrbGrid r;
+        r.x0 = mnx; r.y0 = mny; r.inv_h = inv_h; r.h = h; r.nx = nx; r.ny = ny; r.n = part[1023]; r.ok = 1;
+        *g = r;
+    }
 }

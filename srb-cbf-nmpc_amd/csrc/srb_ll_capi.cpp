@@ -162,7 +162,7 @@ extern "C" int srb_ll_calc_torque_device(srb_ll_ctx *c, int n_agents, const srb_
     LLCHK(hipSetDevice(c->device));
     SrbLLDev k = to_dev(d);
     if (!k.x) k.x = c->outb[7];   // x is optional: the context's buffer absorbs it
-    return ll_launch(c, n_agents, k, stream ? (hipStream_t)stream : c->stream);
+    return ll_launch(c, n_agents, k, (hipStream_t)stream);      // NULL: the HIP null stream
 }
 
 extern "C" int srb_ll_calc_torque(srb_ll_ctx *c, int n_agents, const srb_ll_io *h)

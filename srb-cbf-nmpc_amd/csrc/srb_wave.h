@@ -246,22 +246,50 @@ __device__ __forceinline__ void wargmin(double &d, int &idx)
     d = a; idx = (int)i32[0]; lexmin(d, idx, b, (int)i32[1]);
 }
 
+// Uniform grid over the rows of a table (SURVEY 8(a) row a10 at swarm scale): built on the
+// device each launch by srb_grid_build_kernel for tables of SRB_GRID_MIN_ROWS rows or more.
+// Cells row-major (cy * nx + cx), rows of finite coordinates sorted by cell (the order inside
+// a cell is arbitrary -- the selection order below is exact whatever it is).
+struct SrbGrid {
+    double x0, y0, inv_h, h;       // origin and cell size
+    int nx, ny, n;                 // cells per axis, rows in the grid
+    int ok;                        // 0: not built (brute-force scan)
+};
+
+// per-lane insertion of candidate (cd = sqrt distance, ci = row) into the sorted top-K
+// (bd, bi), ordered lexicographically by (distance, index)
+template <int KM>
+__device__ __forceinline__ void knn_insert(double (&bd)[KM], int (&bi)[KM], double cd, int ci, int K)
+{
+#pragma unroll
+    for (int j = 0; j < KM; j++) {
+        const bool lt = (j < K) && (cd < bd[j] || (cd == bd[j] && ci < bi[j]));
+        const double td = bd[j]; const int ti = bi[j];
+        bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
+        cd = lt ? td : cd; ci = lt ? ti : ci;
+    }
+}
+
 // K nearest rows of a table (row i at tab[stride*i], x at +0, y at +1) to (px, py),
 // ascending in (sqrt distance, index) -- the order of the reference's strict-'<' scan over
 // sqrt(pow(dx,2)+pow(dy,2)) (MPC_dist.cpp:373-382; two rows whose squared distances differ
 // but round to the same sqrt keep index order, as there) -- excluding row `self`; indices to
 // sel[0..K).  cap != 0 applies the reference's min_dist = 1000 / min_i = 0 start: a round
 // whose winner is not closer than 1000 m selects row 0.  NaN rows are never selected.
-// KW waves (one workgroup) scan the table once: lane l of wave w visits rows l + 64 (w + KW t)
-// in increasing index and keeps a sorted top-K of them (a strict '<' keeps the lower index on
-// ties); then K rounds pop the global order: a wave argmin over the lane heads, the KW wave
-// winners through LDS (wd_lds, wi_lds: KW entries each), the owning lane drops its head.
-// The sqrt is taken only for rows that can enter a lane's list: d^2 above its K-th entry's
-// squared key by more than a relative 1e-14 cannot round to a smaller or equal sqrt.
+// KW waves (one workgroup) gather candidates -- every row (brute force), or with a grid the
+// rows of the cells around the query that must hold the K nearest -- and each lane keeps a
+// sorted top-K of its candidates; then K rounds pop the global order: a wave argmin over the
+// lane heads, the KW wave winners through LDS (wd_lds, wi_lds: KW + 1 entries each), the
+// owning lane drops its head.  The sqrt is taken only for rows that can enter a lane's list:
+// d^2 above its K-th entry's squared key by more than a relative 1e-14 cannot round to a
+// smaller sqrt.
 template <int KW, int KM>
 __device__ __forceinline__ void knn_select_k(int tid, double px, double py, const double *__restrict__ tab,
                                            int stride, int n_rows, int self, int K, int cap, int *sel,
-                                           double *wd_lds, int *wi_lds)
+                                           double *wd_lds, int *wi_lds, const SrbGrid *grid = nullptr,
+                                           const int *__restrict__ cell_off = nullptr,
+                                           const double2 *__restrict__ spos = nullptr,
+                                           const int *__restrict__ sidx = nullptr)
 {
 #pragma clang fp contract(off)
     const int lane = tid & 63, wv = tid >> 6;
@@ -269,34 +297,69 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
 #pragma unroll
     for (int j = 0; j < KM; j++) { bd[j] = __builtin_inf(); bi[j] = 0x7fffffff; }
     double wq = __builtin_inf();                   // filter bound on d^2 (K-th key squared, padded)
-    // KNN_U rows per lane per batch: all their loads are issued before the first is used
-    constexpr int KNN_U = 4, STEP = 64 * KW;
-    for (int i0 = tid; i0 < n_rows; i0 += KNN_U * STEP) {
-        double tx[KNN_U], ty[KNN_U];
+    constexpr int STEP = 64 * KW;
+    auto offer = [&](double tx, double ty, int i) {
+        const double dx = px - tx, dy = py - ty;
+        const double d2 = dx * dx + dy * dy;
+        if (i == self || !(d2 <= wq)) return;
+        knn_insert<KM>(bd, bi, sqrt(d2), i, K);
 #pragma unroll
-        for (int u = 0; u < KNN_U; u++) {
-            const int i = i0 + u * STEP;
-            const bool in = i < n_rows;
-            tx[u] = in ? tab[(size_t)stride * i] : 0.0;
-            ty[u] = in ? tab[(size_t)stride * i + 1] : 0.0;
+        for (int j = 0; j < KM; j++)
+            if (j == K - 1) wq = bd[j] * bd[j] * (1.0 + 1e-14);
+    };
+    // ---- grid search: the smallest Chebyshev ring r0 of cells around the query cell holding
+    // K candidates bounds the K-th distance by (r0 + 1) sqrt(2) h, so every row closer than
+    // that lies in the ring R = ceil((r0 + 1) sqrt 2) + 1; queries far outside the grid (or a
+    // grid that cannot supply K rows) fall back to the brute-force scan
+    bool done = false;
+    if (grid && grid->ok) {
+        const SrbGrid g = *grid;
+        const double fx = floor((px - g.x0) * g.inv_h), fy = floor((py - g.y0) * g.inv_h);
+        const int keff = K + (self >= 0 ? 1 : 0);
+        if (g.n >= keff && fx > -64.0 && fy > -64.0 && fx < g.nx + 64.0 && fy < g.ny + 64.0) {
+            const int cx = (int)fx, cy = (int)fy, rmax = max(g.nx, g.ny) + 64;
+            auto rows_in = [&](int r, int y) -> int {        // rows of cell-row y within x-range of ring r
+                const int xl = max(cx - r, 0), xr = min(cx + r, g.nx - 1);
+                if (y < 0 || y >= g.ny || xl > xr) return 0;
+                return cell_off[y * g.nx + xr + 1] - cell_off[y * g.nx + xl];
+            };
+            int r0 = 0;
+            for (; r0 < rmax; r0++) {                        // uniform: every thread computes the same count
+                int cnt = 0;
+                for (int y = cy - r0 + lane; y <= cy + r0; y += 64) cnt += rows_in(r0, y);
+                for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
+                if (cnt >= keff) break;
+            }
+            if (r0 < rmax) {
+                const int R = (int)ceil((r0 + 1) * 1.4142135623730951) + 1;
+                for (int y = max(cy - R, 0); y <= min(cy + R, g.ny - 1); y++) {
+                    const int xl = max(cx - R, 0), xr = min(cx + R, g.nx - 1);
+                    if (xl > xr) continue;
+                    const int a = cell_off[y * g.nx + xl], b = cell_off[y * g.nx + xr + 1];
+                    for (int i = a + tid; i < b; i += STEP) {
+                        const double2 q = spos[i];
+                        offer(q.x, q.y, sidx[i]);
+                    }
+                }
+                done = true;
+            }
         }
+    }
+    if (!done) {
+        // ---- brute force: KNN_U rows per lane per batch, all loads issued before the first use
+        constexpr int KNN_U = 4;
+        for (int i0 = tid; i0 < n_rows; i0 += KNN_U * STEP) {
+            double tx[KNN_U], ty[KNN_U];
 #pragma unroll
-        for (int u = 0; u < KNN_U; u++) {
-            const int i = i0 + u * STEP;
-            const double dx = px - tx[u], dy = py - ty[u];
-            const double d2 = dx * dx + dy * dy;
-            if (i >= n_rows || i == self || !(d2 <= wq)) continue;
-            double cd = sqrt(d2); int ci = i;
-#pragma unroll
-            for (int j = 0; j < KM; j++) {
-                const bool lt = (j < K) && (cd < bd[j]);
-                const double td = bd[j]; const int ti = bi[j];
-                bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
-                cd = lt ? td : cd; ci = lt ? ti : ci;
+            for (int u = 0; u < KNN_U; u++) {
+                const int i = i0 + u * STEP;
+                const bool in = i < n_rows;
+                tx[u] = in ? tab[(size_t)stride * i] : 0.0;
+                ty[u] = in ? tab[(size_t)stride * i + 1] : 0.0;
             }
 #pragma unroll
-            for (int j = 0; j < KM; j++)
-                if (j == K - 1) wq = bd[j] * bd[j] * (1.0 + 1e-14);
+            for (int u = 0; u < KNN_U; u++)
+                if (i0 + u * STEP < n_rows) offer(tx[u], ty[u], i0 + u * STEP);
         }
     }
     // round j's winner is kept by lane j and stored after the last round: a store inside the
@@ -329,9 +392,11 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
 template <int KW>
 __device__ __forceinline__ void knn_select(int tid, double px, double py, const double *__restrict__ tab,
                                            int stride, int n_rows, int self, int K, int cap, int *sel,
-                                           double *wd_lds, int *wi_lds)
+                                           double *wd_lds, int *wi_lds, const SrbGrid *grid = nullptr,
+                                           const int *cell_off = nullptr, const double2 *spos = nullptr,
+                                           const int *sidx = nullptr)
 {
-    if (K <= 4) knn_select_k<KW, 4>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
-    else if (K <= 8) knn_select_k<KW, 8>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
-    else knn_select_k<KW, SRB_KNN_MAX>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds);
+    if (K <= 4) knn_select_k<KW, 4>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds, grid, cell_off, spos, sidx);
+    else if (K <= 8) knn_select_k<KW, 8>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds, grid, cell_off, spos, sidx);
+    else knn_select_k<KW, SRB_KNN_MAX>(tid, px, py, tab, stride, n_rows, self, K, cap, sel, wd_lds, wi_lds, grid, cell_off, spos, sidx);
 }

@@ -50,7 +50,7 @@ class Batch(ctypes.Structure):
     _fields_ = [("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
                 ("n_obs", ctypes.c_int), ("n_all", ctypes.c_int), ("agent_offset", ctypes.c_int),
                 ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip),
-                ("alpha_buf", _dp), ("alpha", _dp), ("sel", _ip)]
+                ("alpha_buf", _dp), ("alpha", _dp), ("sel", _ip), ("obstacles_version", ctypes.c_int)]
 
 
 class Prep(ctypes.Structure):
@@ -184,11 +184,13 @@ class BatchSolver:
 
     # --------------------------------------------------------------- device path
     def solve_device(self, x0, ref, foot, obstacles, nbr_state, out, agent_offset: int = 0, stream=None,
-                     alpha_buf=None):
+                     alpha_buf=None, obstacles_version: int = 0):
         """All arguments torch tensors on this solver's device (float64 / int32), contiguous.
         `out` is a dict with x_qp (or None), x, obj, status, iters and, with alpha_buf [A][4],
         alpha [A][20]; an optional int32 out["sel"] [A][Ko + Kn] receives the selected rows
         (otherwise the context's scratch is used: one stream per context at a time).
+        obstacles_version != 0 marks the obstacle tensor as unchanged since the last call with
+        that version (its selection grid is reused; the reference's obstacles are static).
         Asynchronous on `stream` (a hipStream_t handle), by default torch's current stream on
         this device, so the launch is ordered after the torch work that filled the inputs."""
         def dptr(t):
@@ -207,7 +209,7 @@ class BatchSolver:
                   int(agent_offset), dptr(out.get("x_qp")), dptr(out["x"]), dptr(out["obj"]),
                   iptr(out["status"]), iptr(out["iters"]), dptr(alpha_buf),
                   dptr(out.get("alpha") if alpha_buf is not None else None),
-                  iptr(out["sel"]) if out.get("sel") is not None else None)
+                  iptr(out["sel"]) if out.get("sel") is not None else None, int(obstacles_version))
         _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), self._stream(stream)))
 
     def _stream(self, stream):

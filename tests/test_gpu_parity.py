@@ -265,6 +265,67 @@ def test_knn_matches_bruteforce(Ko, Kn):
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
+@pytest.mark.parametrize("Ko,Kn", [(3, 8), (16, 16)])
+def test_knn_grid_matches_bruteforce(Ko, Kn):
+    """Tables of SRB_GRID_MIN_ROWS (8192) rows or more go through the uniform selection grid
+    (srb_grid_build_kernel + the ring search of knn_select_k): the selected rows must be the
+    reference's scan order exactly -- exact-distance ties, sqrt-rounding ties, NaN rows, a
+    shard offset, and agents far outside the grid (brute-force fallback) included."""
+    from test_oracle import sqrt_tie_pair
+    N, C, A, n_nbr, n_obs, off = 10, 2, 384, 9000, 12000, 512
+    rng = np.random.default_rng(21)
+    b = workload.make_batch(A, N, C, seed=5)
+    big = workload.make_batch(n_nbr, N, C, seed=6, n_obs=n_obs)
+    nb = big["nbr_state"].copy(); ob = big["obstacles"].copy()
+    nb[off:off + A] = b["nbr_state"]                     # this shard's agents at rows off..off+A
+    # agents 0..7: exact ties at mirrored positions around a quarter-metre-aligned agent
+    for a in range(8):
+        px, py = np.round(b["x0"][a, [0, 2]] * 4) / 4
+        dx, dy = px - b["x0"][a, 0], py - b["x0"][a, 2]
+        b["x0"][a, [0, 2]] = (px, py); nb[off + a, :2] = (px, py)
+        b["ref"][a, 0::4] += dx; b["ref"][a, 2::4] += dy
+        b["foot"][a, :, 0] += dx; b["foot"][a, :, 1] += dy
+        ob[20 + 2 * a] = (px + 1.5, py + 1.0); ob[21 + 2 * a] = (px - 1.5, py - 1.0)
+        nb[9 + 2 * a, :2] = (px - 1.5, py + 2.25); nb[10 + 2 * a, :2] = (px + 1.5, py - 2.25)
+    for a in range(8, 12):                                 # sqrt-rounding ties
+        px, py = b["x0"][a, 0], b["x0"][a, 2]
+        near, far = sqrt_tie_pair(px, py, rng); ob[60 + 2 * a] = far; ob[61 + 2 * a] = near
+        near, far = sqrt_tie_pair(px, py, rng); nb[40 + 2 * a, :2] = far; nb[41 + 2 * a, :2] = near
+    nb[100:140, :2] = np.nan; ob[100:140] = np.nan          # rows outside every cell
+    b["x0"][20, [0, 2]] = (5000.0, -4000.0)                # far outside the grid: brute-force fallback
+    nb[off + 20, :2] = (5000.0, -4000.0)
+    out = solver(N, C, Ko, Kn).solve(b["x0"], b["ref"], b["foot"], ob, nb, agent_offset=off)
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    want = np.array([oracle.select_idx(op, b["x0"][a], ob, nb, off + a) for a in range(A)], np.int32)
+    np.testing.assert_array_equal(out["sel"], want)
+
+
+def test_knn_grid_obstacle_version_reuse():
+    """obstacles_version: an unchanged obstacle table keeps its selection grid across calls; a
+    new version rebuilds it (device API)."""
+    N, C, A, n_obs = 10, 2, 256, 10000
+    b = workload.make_batch(A, N, C, seed=8)
+    ob1 = workload.make_batch(4 * n_obs // 20, N, C, seed=9, n_obs=n_obs)["obstacles"]
+    ob2 = ob1[::-1].copy()
+    s = solver(N, C, 3, 0)
+    dev = torch.device("cuda:0")
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    x0, ref, foot, tob = T(b["x0"]), T(b["ref"]), T(b["foot"].reshape(A, -1)), T(ob1)
+    op = oracle.params(N, C, K_obs=3)
+    sels = []
+    for ver, table in ((1, ob1), (1, ob1), (2, ob2), (0, ob1)):
+        tob.copy_(T(table))
+        o = dict(x_qp=None, x=torch.zeros((A, s.params.nv), dtype=torch.float64, device=dev),
+                 obj=torch.zeros(A, dtype=torch.float64, device=dev), status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+                 iters=torch.zeros((A, 2), dtype=torch.int32, device=dev), sel=torch.zeros((A, 3), dtype=torch.int32, device=dev))
+        s.solve_device(x0, ref, foot, tob, None, o, obstacles_version=ver)
+        torch.cuda.synchronize()
+        sel = o["sel"].cpu().numpy()
+        want = np.array([oracle.select_idx(op, b["x0"][a], table) for a in range(A)], np.int32)
+        np.testing.assert_array_equal(sel, want)
+        sels.append(sel)
+
+
 def test_knn_sentinel_and_missing_rows():
     """The reference's min_dist = 1000 / min_i = 0 start (MPC_dist.cpp:371-372): with no
     static obstacle closer than 1000 m every static round selects obstacle 0; a neighbour
@@ -490,6 +551,19 @@ def test_hl_planner_bitwise_vs_oracle(NA, n_obs, loop):
     Pr, Prd = srbnmpc.hl_plan(Ps, Po, loop=loop)
     R, Rd = oracle.hl_plan(Ps, Po, loop=loop)
     assert Pr.shape == (2 * NA, loop // 40)
+    np.testing.assert_array_equal(Pr, R)
+    np.testing.assert_array_equal(Prd, Rd)
+
+
+def test_hl_planner_multi_workgroup_swarm_bitwise():
+    """A swarm beyond one workgroup (NA = 1100 > 1024): one coupled swarm, one launch per step
+    across the chip, still bit-identical to the CPU restatement."""
+    NA, n_obs, loop = 1100, 30, 160
+    rng = np.random.default_rng(11)
+    Ps = np.stack([rng.uniform(-30, 0, NA), rng.uniform(-15, 15, NA)], 1).ravel()
+    Po = np.stack([rng.uniform(0, 9, n_obs), rng.uniform(-2, 2, n_obs)], 1)
+    Pr, Prd = srbnmpc.hl_plan(Ps, Po, loop=loop)
+    R, Rd = oracle.hl_plan(Ps, Po, loop=loop)
     np.testing.assert_array_equal(Pr, R)
     np.testing.assert_array_equal(Prd, Rd)
 

@@ -10,7 +10,7 @@ import numpy as np
 import srbnmpc
 
 ap = argparse.ArgumentParser()
-ap.add_argument('--agents', default='4,256,1024')
+ap.add_argument('--agents', default='4,256,1024,4096')
 ap.add_argument('--loop', type=int, default=100000)
 ap.add_argument('--cpu-seconds', type=float, default=10.0)
 args = ap.parse_args()
