@@ -3,6 +3,9 @@
 #pragma once
 
 #define SRB_KNN_MAX 16    // nearest static obstacles / neighbours per agent (each)
+#ifndef SRB_REFINE
+#define SRB_REFINE 1      // iterative-refinement steps per reduced Newton solve
+#endif
 #define SRB_KNN_WAVES 4   // waves per agent in the selection kernel (srb_knn_kernel)
 #define SRB_GRID_CELLS 16384      // cells of the selection grid (LDS counters of srb_grid_build_kernel)
 #define SRB_GRID_MIN_ROWS 8192    // tables this long get a grid (shorter: brute-force scan)

@@ -296,13 +296,18 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         double y0 = 0.0;
 #pragma unroll
         for (int j = 0; j < NZL; j++) y0 = fma(M[j], bc16(gi, j), y0);
-        double rr = gi;
-#pragma unroll
-        for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y0, j), rr);
-        if (i >= nz) rr = 0.0;
+        // SRB_REFINE steps of iterative refinement with fp64 residuals (1 in the product build;
+        // the fp32-factor diagnostic build uses more)
         double y1 = y0;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) y1 = fma(M[j], bc16(rr, j), y1);
+        for (int it = 0; it < SRB_REFINE; it++) {
+            double rr = gi;
+#pragma unroll
+            for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y1, j), rr);
+            if (i >= nz) rr = 0.0;
+#pragma unroll
+            for (int j = 0; j < NZL; j++) y1 = fma(M[j], bc16(rr, j), y1);
+        }
 #pragma unroll
         for (int j = 0; j < NZL; j++) res[j] = bc16(y1, j);
         return;
@@ -314,16 +319,19 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
     double y0 = 0.0;
 #pragma unroll
     for (int j = 0; j < NZL; j++) y0 = fma(M[j], gv[j], y0);
-    if (lane < nz) y[lane] = y0;
-    SYNC();
-    double rr = (lane < nz) ? g[lane] : 0.0;
-#pragma unroll
-    for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
-    if (lane < nz) r[lane] = rr;
-    SYNC();
     double y1 = y0;
+    for (int it = 0; it < SRB_REFINE; it++) {
+        if (it > 0) SYNC();                      // every lane has read the previous r
+        if (lane < nz) y[lane] = y1;
+        SYNC();
+        double rr = (lane < nz) ? g[lane] : 0.0;
 #pragma unroll
-    for (int j = 0; j < NZL; j++) y1 = fma(M[j], r[j], y1);
+        for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
+        if (lane < nz) r[lane] = rr;
+        SYNC();
+#pragma unroll
+        for (int j = 0; j < NZL; j++) y1 = fma(M[j], r[j], y1);
+    }
     if (lane < nz) out[lane] = y1;
     SYNC();
 #pragma unroll

@@ -159,10 +159,49 @@ __device__ __forceinline__ double bc16(double v, int k)
 // A DPP row_newbcast form of this elimination (gj_invert_dpp) measured slower on MI355X: 3546
 // against 3062 cycles for NZL = 12 (tools/ubench/gj_bench.hip), since readlane broadcasts land
 // in SGPRs that the row updates read for free while the DPP copies cost a VALU move each.
+#ifndef SRB_KKT_FP32          // diagnostic build: reduced Newton matrix inverted in fp32 (make fp32)
+#define SRB_KKT_FP32 0
+#endif
+__device__ __forceinline__ float readlane_f(float v, int lane)
+{
+    return __int_as_float(__builtin_amdgcn_readlane(__float_as_int(v), lane));
+}
+// the fp32 form of gj_invert below (same steps), on the matrix rounded to fp32
+template <int NZL>
+__device__ __forceinline__ int gj_invert_f32(double (&Ad)[NZL], int lane, int regularise)
+{
+    float A[NZL];
+#pragma unroll
+    for (int j = 0; j < NZL; j++) A[j] = (float)Ad[j];
+    int fail = 0;
+    float cs = 1.0f;
+#pragma unroll
+    for (int k = 0; k < NZL; k++) {
+        float piv = readlane_f(A[k], k);
+        if (regularise && piv <= 1e-14f && piv == piv) piv = 1e-7f;
+        fail |= !(piv > 0.0f);
+        const float inv = 1.0f / piv;
+        float rk[NZL];
+#pragma unroll
+        for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0f : readlane_f(A[j], k);
+        const bool me = lane == k;
+        const float f = me ? 0.0f : A[k] * inv;
+#pragma unroll
+        for (int j = 0; j < NZL; j++)
+            if (j != k) A[j] = fmaf(-f, rk[j], A[j]);
+        A[k] = me ? 1.0f : -f;
+        cs = me ? inv : cs;
+    }
+#pragma unroll
+    for (int j = 0; j < NZL; j++) Ad[j] = (double)(A[j] * cs);
+    return fail;
+}
+
 template <int NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
     if constexpr (NZL <= 16 && SRB_USE_DPP) lane &= 15;
+    if constexpr (SRB_KKT_FP32) return gj_invert_f32<NZL>(A, lane, regularise);
     // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
     // elimination is one basic block: the scheduler overlaps step k's row updates with the
     // broadcast of row k+1, whose entries are updated first.
