@@ -89,6 +89,10 @@ struct SrbLLKParams {
     int dbg_agent;                    // >= 0: that agent records a per-iteration trace (srb_ll_debug_trace)
 };
 
+#ifndef SRB_LL_WPE        // waves per SIMD the low-level kernel is compiled for (min, max)
+#define SRB_LL_WPE 2, 8
+#endif
+
 // device layout of one agent (srb_ll_io, include/srbnmpc.h): column-major matrices with fixed
 // leading dimensions
 #define SRB_LL_NQ 18   // TOTAL_DOF (global_loco_opts.h:24)

@@ -81,7 +81,7 @@ __device__ unsigned long long srb_ll_stamp[16];   // s_memtime cycles per phase 
         }                                                                                            \
     } while (0)
 
-extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(2, 8))) srb_ll_kernel(SrbLLKParams prm, int n_agents, SrbLLDev io)
+extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per_eu(SRB_LL_WPE))) srb_ll_kernel(SrbLLKParams prm, int n_agents, SrbLLDev io)
 {
     __shared__ LLShared sh;
     const int agent = blockIdx.x;
