@@ -411,6 +411,23 @@ __device__ __forceinline__ double slot_f(const Slot &q, const double *xs, double
 
 
 
+// sum_j z_kj over the K obstacle rows of grid k (zo, LDS), in index order: unrolled in chunks of
+// 16 with predicated loads, so the loads of a chunk are in flight together instead of one
+// dependent load per row
+__device__ __forceinline__ double zo_sum(const double *zo, int k, int K)
+{
+    const double *z = zo + k * K;
+    double s = 0.0;
+    for (int j0 = 0; j0 < K; j0 += 16) {
+        double v[16];
+#pragma unroll
+        for (int u = 0; u < 16; u++) v[u] = (j0 + u < K) ? z[j0 + u] : 0.0;
+#pragma unroll
+        for (int u = 0; u < 16; u++) s += v[u];
+    }
+    return s;
+}
+
 // --------------------------------------------------------------------------- main kernel
 // NZL: register bound on nz (one reduced-matrix row per lane); TS: slot trips per thread;
 // NW: wavefronts per agent (1, or 4 = one per SIMD of a CU for small batches).  With NW > 1
@@ -829,7 +846,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         double hs = 0.0;
                         if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
                             const int k = q.i0 >> 2;
-                            for (int j = 0; j < K; j++) hs += zo[k * K + j];
+                            hs = zo_sum(zo, k, K);
                             hs *= -2.0;
                         }
                         W[q.wr] = om + ((kind_of(q) == K_VAR) ? q.a0 + hs : 0.0);
@@ -942,7 +959,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         Slot &q = Q[t];
                         if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
                             const int k = q.i0 >> 2;
-                            for (int j = 0; j < K; j++) hso[t] += zo[k * K + j];
+                            hso[t] = zo_sum(zo, k, K);
                         }
 #pragma unroll
                         for (int r = 0; r < 2; r++) { q.s[r] = fma(ap, q.ds[r], q.s[r]); q.z[r] = fma(ad, q.dz[r], q.z[r]); }
@@ -970,7 +987,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             if (kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {   // +2 ap dx sum_j z'_kj on (x_k, y_k)
                                 const int k = q.i0 >> 2;
                                 double hs_new = 0.0;
-                                for (int j = 0; j < K; j++) hs_new += zo[k * K + j];
+                                hs_new = zo_sum(zo, k, K);
                                 q.rx = fma(2.0 * ap * hs_new, q.jd, q.rx);
                             }
                         }
