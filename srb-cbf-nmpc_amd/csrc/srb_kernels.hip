@@ -769,6 +769,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     }
                 }
             }
+            STAMP_END(18);                                    // stamps build: residual loop | reduction
             double dxm;
             {
                 double rv[5] = {nrx, nrz, sz, gm, dxl};
@@ -858,8 +859,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         if (t < nts && kind_of(Q[t]) == K_VEL)
                             __hip_atomic_fetch_add(&W[Q[t].r], Q[t].z[0] * Q[t].is[0] + Q[t].z[1] * Q[t].is[1], __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
+                STAMP_END(16);
                 set_rhs(0);
                 SYNC();
+                STAMP_END(17);
                 gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
                 SYNC();
                 STAMP_END(4);
@@ -915,6 +918,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
                         }
                     }
+                STAMP_END(21 + pass);
                 // findsteplength (Auxilary.c:271-294): 1 / max(-dv / v), 1 when no dv < 0
                 {
                     double rv[2] = {mxs, mxz};
@@ -966,6 +970,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     }
                 }
                 SYNC();          // every lane has read the old duals and x
+                STAMP_END(19);
 #pragma unroll
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
@@ -979,6 +984,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
                     }
                 SYNC();
+                STAMP_END(20);
                 if (nl)
 #pragma unroll
                     for (int t = 0; t < TS; t++)
