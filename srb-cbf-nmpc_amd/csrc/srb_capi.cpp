@@ -323,8 +323,13 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (use_nlp && k.K_obs + k.K_nbr > 0) {
         // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
         // with the arena) get a uniform grid so each agent scans only the cells around it
-        static const int min_rows = [] { const char *e = std::getenv("SRB_GRID_MIN_ROWS"); return e ? std::atoi(e) : SRB_GRID_MIN_ROWS; }();
-        const bool go = k.K_obs > 0 && n_obs >= min_rows, gn = k.K_nbr > 0 && n_all >= min_rows;
+        // (a versioned static obstacle table builds its grid once, so it pays off at fewer rows;
+        // SRB_GRID_MIN_ROWS overrides both thresholds)
+        static const char *env_rows = std::getenv("SRB_GRID_MIN_ROWS");
+        static const int min_rows = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS;
+        static const int min_rows_static = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS_STATIC;
+        const bool go = k.K_obs > 0 && n_obs >= (d->obstacles_version != 0 ? min_rows_static : min_rows);
+        const bool gn = k.K_nbr > 0 && n_all >= min_rows;
         if (go) { int rc = grid_reserve(c, 0, n_obs); if (rc) return rc; }
         if (gn) { int rc = grid_reserve(c, 1, n_all); if (rc) return rc; }
         const srb_ctx::grid_buf &G0 = c->grid[0], &G1 = c->grid[1];

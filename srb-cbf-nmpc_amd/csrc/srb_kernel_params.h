@@ -9,6 +9,8 @@
 #define SRB_KNN_WAVES 4   // waves per agent in the selection kernel (srb_knn_kernel)
 #define SRB_GRID_CELLS 16384      // cells of the selection grid (LDS counters of srb_grid_build_kernel)
 #define SRB_GRID_MIN_ROWS 8192    // tables this long get a grid (shorter: brute-force scan)
+#define SRB_GRID_MIN_ROWS_STATIC 4096   // versioned static obstacle tables (grid built once, reused):
+                                         // configs[2]'s 5120 rows: selection 37.8 -> 31.3 us (profiles/r02_grid_threshold.txt)
 #define SRB_MAX_NZ 32     // reduced Newton system size bound: nz = N(C-1)+1 <= 32
 #define SRB_MAX_N 33      // CoM-CoP slots 2(N-1) fit one 64-lane trip
 // NLP stage: initial inequality duals (the oracle's ORC_NLP_Z0, oracle/nlp_ipm.c).  100 is the

@@ -300,10 +300,12 @@ def test_knn_grid_matches_bruteforce(Ko, Kn):
     np.testing.assert_array_equal(out["sel"], want)
 
 
-def test_knn_grid_obstacle_version_reuse():
+@pytest.mark.parametrize("n_obs", [10000, 5120])
+def test_knn_grid_obstacle_version_reuse(n_obs):
     """obstacles_version: an unchanged obstacle table keeps its selection grid across calls; a
-    new version rebuilds it (device API)."""
-    N, C, A, n_obs = 10, 2, 256, 10000
+    new version rebuilds it (device API).  5120 rows: a versioned table of fewer than
+    SRB_GRID_MIN_ROWS rows still gets the grid (SRB_GRID_MIN_ROWS_STATIC), version 0 the scan."""
+    N, C, A = 10, 2, 256
     b = workload.make_batch(A, N, C, seed=8)
     ob1 = workload.make_batch(4 * n_obs // 20, N, C, seed=9, n_obs=n_obs)["obstacles"]
     ob2 = ob1[::-1].copy()
