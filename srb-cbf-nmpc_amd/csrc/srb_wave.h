@@ -318,10 +318,11 @@ __device__ __forceinline__ void knn_insert(double (&bd)[KM], int (&bi)[KM], doub
 // KW waves (one workgroup) gather candidates -- every row (brute force), or with a grid the
 // rows of the cells around the query that must hold the K nearest -- and each lane keeps a
 // sorted top-K of its candidates; then K rounds pop the global order: a wave argmin over the
-// lane heads, the KW wave winners through LDS (wd_lds, wi_lds: KW + 1 entries each), the
-// owning lane drops its head.  The sqrt is taken only for rows that can enter a lane's list:
-// d^2 above its K-th entry's squared key by more than a relative 1e-14 cannot round to a
-// smaller sqrt.
+// lane heads, the KW wave winners through LDS (wd_lds, wi_lds: KW entries each), the owning
+// lane drops its head (measured faster than per-wave pops followed by one merge of the KW K
+// wave winners: two barriers per round cost less than K extra wave-argmin rounds).  The sqrt
+// is taken only for rows that can enter a lane's list: d^2 above its K-th entry's squared key
+// by more than a relative 1e-14 cannot round to a smaller sqrt.
 template <int KW, int KM>
 __device__ __forceinline__ void knn_select_k(int tid, double px, double py, const double *__restrict__ tab,
                                            int stride, int n_rows, int self, int K, int cap, int *sel,
@@ -362,8 +363,20 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
                 if (y < 0 || y >= g.ny || xl > xr) return 0;
                 return cell_off[y * g.nx + xr + 1] - cell_off[y * g.nx + xl];
             };
-            int r0 = 0;
-            for (; r0 < rmax; r0++) {                        // uniform: every thread computes the same count
+            // rings 0..3 in one pass (lane l < 16 counts cell row y = cy + l - r(r+1) of ring
+            // r = floor(sqrt(l))), then ring by ring from 4 if none of them holds keff rows
+            int r0 = 4;
+            {
+                const int rr = (lane < 1) ? 0 : (lane < 4) ? 1 : (lane < 9) ? 2 : (lane < 16) ? 3 : -1;
+                const int v = (rr >= 0) ? rows_in(rr, cy + lane - rr * rr - rr) : 0;
+#pragma unroll
+                for (int r = 3; r >= 0; r--) {
+                    int cr = (rr == r) ? v : 0;
+                    for (int o = 32; o > 0; o >>= 1) cr += __shfl_xor(cr, o, 64);
+                    if (cr >= keff) r0 = r;
+                }
+            }
+            for (; r0 >= 4 && r0 < rmax; r0++) {            // uniform: every thread computes the same count
                 int cnt = 0;
                 for (int y = cy - r0 + lane; y <= cy + r0; y += 64) cnt += rows_in(r0, y);
                 for (int o = 32; o > 0; o >>= 1) cnt += __shfl_xor(cnt, o, 64);
@@ -371,13 +384,30 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
             }
             if (r0 < rmax) {
                 const int R = (int)ceil((r0 + 1) * 1.4142135623730951) + 1;
-                for (int y = max(cy - R, 0); y <= min(cy + R, g.ny - 1); y++) {
-                    const int xl = max(cx - R, 0), xr = min(cx + R, g.nx - 1);
-                    if (xl > xr) continue;
-                    const int a = cell_off[y * g.nx + xl], b = cell_off[y * g.nx + xr + 1];
-                    for (int i = a + tid; i < b; i += STEP) {
-                        const double2 q = spos[i];
-                        offer(q.x, q.y, sidx[i]);
+                const int ylo = max(cy - R, 0), yhi = min(cy + R, g.ny - 1);
+                const int xl = max(cx - R, 0), xr = min(cx + R, g.nx - 1);
+                // up to 64 cell rows at a time: lane y loads its row's range [a, a + len), a wave
+                // scan numbers the candidates, and every thread takes candidates c, c + STEP, ..
+                // (segment found by a binary search over the scan), so the cell-offset loads and
+                // the row loads are two dependent round trips instead of two per cell row
+                for (int yb = ylo; xl <= xr && yb <= yhi; yb += 64) {
+                    const int y = yb + lane;
+                    int a = 0, len = 0;
+                    if (y <= yhi) { a = cell_off[y * g.nx + xl]; len = cell_off[y * g.nx + xr + 1] - a; }
+                    int inc = len;
+#pragma unroll
+                    for (int o = 1; o < 64; o <<= 1) { const int v = __shfl_up(inc, o, 64); if (lane >= o) inc += v; }
+                    const int total = __shfl(inc, 63, 64), exc = inc - len;
+                    for (int c0 = 64 * wv; c0 < total; c0 += STEP) {      // wave-uniform trip count
+                        const int c = c0 + lane;
+                        int j = 0;                                        // last lane with exc <= c
+#pragma unroll
+                        for (int st = 32; st > 0; st >>= 1) j += (__shfl(exc, j + st, 64) <= c) ? st : 0;
+                        const int i = __shfl(a, j, 64) + (c - __shfl(exc, j, 64));
+                        if (c < total) {
+                            const double2 q = spos[i];
+                            offer(q.x, q.y, sidx[i]);
+                        }
                     }
                 }
                 done = true;
