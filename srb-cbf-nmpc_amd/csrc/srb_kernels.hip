@@ -279,6 +279,27 @@ __device__ __forceinline__ void gj_load(double (&A)[NZL], const double *H, const
     }
 }
 
+// Inverse of the reduced Newton matrix (replicated layout from gj_load): gj_invert.  The
+// column-split elimination (gj_invert_split, -DSRB_GJ_SPLIT=1) is bit-identical and issues
+// fewer cross-lane moves, but measured slower on MI355X (configs[2] kernel 0.42 vs 0.40 ms,
+// configs[1] 0.244 vs 0.206 ms; profiles/r02_gj_split_ab.txt): column k reaches the other
+// rows of the wave through two permlane-swap stages on every step's critical path.
+#ifndef SRB_GJ_SPLIT
+#define SRB_GJ_SPLIT 0
+#endif
+#if SRB_GJ_SPLIT
+template <int NZL>
+__device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, int regularise)
+{
+    if constexpr (NZL <= 16 && NZL % 4 == 0 && SRB_USE_DPP && !SRB_KKT_FP32)
+        return gj_invert_split<NZL>(A, lane, regularise);
+    else
+        return gj_invert<NZL>(A, nz, lane, regularise);
+}
+#else
+#define gj_reduced gj_invert
+#endif
+
 // Newton solve in the reduced space: out = Hs^-1 g with one step of iterative refinement
 // (y = M g; y += M (g - Hs y)): the explicit inverse alone is not backward stable, and near
 // the end of an interior-point solve Hs carries barrier weights of 1e8..1e12.
@@ -612,7 +633,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
-            if (gj_invert<NZL>(Mi, nz, lane, 1) != 0) {
+            if (gj_reduced<NZL>(Mi, nz, lane, 1) != 0) {
                 qp_flag = 1;                                  // x stays xbar (last iterate is returned)
                 continue;
             }
@@ -717,7 +738,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, ZZ, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
-            gj_invert<NZL>(Mi, nz, lane, 0);
+            gj_reduced<NZL>(Mi, nz, lane, 0);
             la_solve<NZL>(Mi, ZZ, vg, vy, vr, vd, dxi, nz, lane);
 #pragma unroll
             for (int t = 0; t < TS; t++)
@@ -880,7 +901,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             for (int j = 0; j < NZL; j++) HS[lane * LDH + j] = Mi[j];
                         SYNC();
                     }
-                    const int cf = gj_invert<NZL>(Mi, nz, lane, !nl);
+                    const int cf = gj_reduced<NZL>(Mi, nz, lane, !nl);
                     if (cf == 0) { ok = 1; break; }
                     delta = (delta == 0.0) ? dstart : delta * 10.0;
                 }

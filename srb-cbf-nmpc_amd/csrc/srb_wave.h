@@ -231,6 +231,75 @@ __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int
     return fail;
 }
 
+// value of v in 16-lane row G (compile-time) of the wave, same position in the row: two
+// permlane swap stages (32-lane halves, then row pairs) with compile-time half selection
+template <int G>
+__device__ __forceinline__ double from_row(double v)
+{
+    double a, b;
+    swap_d<32>(v, a, b);                    // a: lane l & 31, b: lane (l & 31) | 32
+    const double t = (G & 2) ? b : a;
+    swap_d<16>(t, a, b);                    // a: lane l & ~16, b: lane l | 16
+    return (G & 1) ? b : a;
+}
+
+// The same elimination as gj_invert on a matrix replicated in each 16-lane row (NZL <= 16,
+// lane l: row i = l & 15), with the columns split over the four copies instead of repeated:
+// row g of the wave (g = l >> 4) updates only columns j = 4c + g, c < NZL / 4.  A step is then
+// NZL / 4 DPP row_newbcast reads of the pivot row and NZL / 4 FMAs per lane, plus one
+// cross-row fetch of column k (from_row, overlapping the pivot reciprocal), where gj_invert
+// issues 2 NZL readlanes and NZL FMAs.  Every entry sees the same operations in the same
+// order (bit-identical to gj_invert); the rows are reassembled at the end, so the result is
+// replicated exactly as gj_invert leaves it.  Callers must hold the replicated layout.
+template <int NZL>
+__device__ __forceinline__ int gj_invert_split(double (&A)[NZL], int lane, int regularise)
+{
+    static_assert(NZL <= 16 && NZL % 4 == 0, "four column groups of a 16-lane row");
+    constexpr int NC = NZL / 4;
+    const int i = lane & 15, g = lane >> 4;
+    double B[NC];
+#pragma unroll
+    for (int c = 0; c < NC; c++)
+        B[c] = (g == 0) ? A[4 * c] : (g == 1) ? A[4 * c + 1] : (g == 2) ? A[4 * c + 2] : A[4 * c + 3];
+    int fail = 0;
+    double cs = 1.0;
+#pragma unroll
+    for (int k = 0; k < NZL; k++) {
+        const int gk = k & 3, ck = k >> 2;
+        // column k of this lane's row (held by row gk of the wave), fetched while the pivot's
+        // reciprocal is formed
+        double colk;
+        switch (gk) {
+        case 0: colk = from_row<0>(B[ck]); break;
+        case 1: colk = from_row<1>(B[ck]); break;
+        case 2: colk = from_row<2>(B[ck]); break;
+        default: colk = from_row<3>(B[ck]); break;
+        }
+        double piv = readlane_d(B[ck], 16 * gk + k);
+        if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
+        fail |= !(piv > 0.0);
+        const double inv = rcp_d(piv);
+        const bool me = i == k;
+        const double f = me ? 0.0 : colk * inv;
+#pragma unroll
+        for (int cc = 0; cc < NC; cc++) {
+            const int c = (((k + 1) >> 2) + cc) % NC;       // the next pivot's column first
+            const double upd = fma(-f, bc16(B[c], k), B[c]);
+            B[c] = (c == ck && g == gk) ? (me ? 1.0 : -f) : upd;
+        }
+        cs = me ? inv : cs;
+    }
+#pragma unroll
+    for (int c = 0; c < NC; c++) {
+        const double v = B[c] * cs;
+        A[4 * c + 0] = from_row<0>(v);
+        A[4 * c + 1] = from_row<1>(v);
+        A[4 * c + 2] = from_row<2>(v);
+        A[4 * c + 3] = from_row<3>(v);
+    }
+    return fail;
+}
+
 // NZL <= 16: the matrix is replicated in each 16-lane row of the wave (lane l holds matrix
 // row l & 15) and step k broadcasts the pivot row by DPP row_newbcast:k -- one VALU move per
 // entry that the row update consumes directly, so a step's critical path is the pivot's
