@@ -100,6 +100,11 @@ struct TermLayout {
 // cnt is a multiple of 16; rows / W / CF are zero beyond every real row.
 // NW > 1: wave w takes the term rows [w cnt/NW, (w+1) cnt/NW) and the per-wave partial
 // tiles / right-hand sides are summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
+// SRB_GRAM_CHAINS = 2 (NZM = 16): alternate term groups accumulate into two MFMA chains,
+// summed at the end (a different summation order; half the dependent-MFMA chain)
+#ifndef SRB_GRAM_CHAINS
+#define SRB_GRAM_CHAINS 1
+#endif
 template <int NZL, bool RHS, int NW>
 __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt,
                                          double *H, double *g, int nz, int tid, double *part)
@@ -113,6 +118,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     double ps[NTC];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
+    d4 acc2 = d4{0.0, 0.0, 0.0, 0.0};       // second accumulator chain (SRB_GRAM_CHAINS == 2)
 #pragma unroll
     for (int t = 0; t < NTC; t++) ps[t] = 0.0;
     const int chunk = cnt / NW, tb = wv * chunk;
@@ -135,7 +141,10 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 #pragma unroll
                 for (int tc = 0; tc < NTC; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
             if constexpr (NZM == 16) {
-                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
+                if (SRB_GRAM_CHAINS == 2 && (u & 1))
+                    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc2, 0, 0, 0);
+                else
+                    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
             } else {
                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
                 acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][NTC - 1], acc[1], 0, 0, 0);
@@ -143,6 +152,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
             }
         }
     }
+    if constexpr (NZM == 16 && SRB_GRAM_CHAINS == 2) acc[0] += acc2;
     double gs[NTC];
     if (RHS)
 #pragma unroll
@@ -723,10 +733,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
                     q.z[0] = q.z[1] = SRB_NLP_Z0;
                     if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x
+                        // both Z rows are read before the first store: the store could alias
+                        // them as far as the compiler knows, and would otherwise put one LDS
+                        // round trip per entry on the path
                         const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
+                        double z0[NZL], z1[NZL];
+#pragma unroll
+                        for (int a = 0; a < NZL; a++) { z0[a] = R[q.i0 * LDR + a]; z1[a] = R[q.i1 * LDR + a]; }
 #pragma unroll
                         for (int a = 0; a < NZL; a++)
-                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                            R[q.r * LDR + a] = fma(jx, z0[a], jy * z1[a]) - (a == nz - 1 ? 1.0 : 0.0);
                     }
                     // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = z0: J'1 vanishes on every
                     // +- pair, leaving the obstacle rows
@@ -782,10 +798,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 #pragma unroll
                     for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
                     if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z
+                        // both Z rows are read before the first store: the store could alias
+                        // them as far as the compiler knows, and would otherwise put one LDS
+                        // round trip per entry on the path
                         const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
+                        double z0[NZL], z1[NZL];
+#pragma unroll
+                        for (int a = 0; a < NZL; a++) { z0[a] = R[q.i0 * LDR + a]; z1[a] = R[q.i1 * LDR + a]; }
 #pragma unroll
                         for (int a = 0; a < NZL; a++)
-                            R[q.r * LDR + a] = fma(jx, R[q.i0 * LDR + a], jy * R[q.i1 * LDR + a]) - (a == nz - 1 ? 1.0 : 0.0);
+                            R[q.r * LDR + a] = fma(jx, z0[a], jy * z1[a]) - (a == nz - 1 ? 1.0 : 0.0);
                         zo[q.r - rO] = q.z[0];
                     }
                 }
