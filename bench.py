@@ -3,6 +3,9 @@
 
     python bench.py [--gpus N --steps K --warmup W] [--config 2] [--agents A]
 
+--gpus N > 1 without a launcher starts N ranks itself (torch.distributed.run on 127.0.0.1, one
+process per GPU); under a launcher WORLD_SIZE must equal N or the run exits non-zero.
+
 One "step" = one pass of the hot path over one batch: (configs with inter-agent rows:
 all-gather of the neighbour snapshot over RCCL) + kNN + QP stage + NLP stage + Bezier fit
 (alpha_COM) for every agent of the batch, inputs resident in HBM.  Multi-GPU: one process per GPU (torchrun),
@@ -232,6 +235,54 @@ def main_ll(args, world, rank, local_rank, dev):
     ctrl.close()
 
 
+def rank_batch(config, agents_per_gpu, world, rank, seed=1234):
+    """The swarm of a `world`-GPU run of `config` and this rank's block of it: (A_total, the whole
+    batch as host arrays, lo, hi).  Every rank generates the whole swarm identically and keeps
+    agents [lo, hi); the obstacle arena and the neighbour snapshot (get_lastState rows of every
+    agent, MPC_dist.cpp:1272-1276) stay whole.  tests/test_gpu_shards.py solves exactly this."""
+    cfg = CONFIGS[config]
+    A_total = agents_per_gpu * world
+    b = workload.make_batch(A_total, cfg["N"], cfg["C"], seed=seed)
+    lo, hi = sdist.shard_range(A_total, world, rank)
+    return A_total, b, lo, hi
+
+
+def launch_ranks(n):
+    """`python bench.py --gpus N` without a launcher: run this script as N ranks (one per GPU) under
+    torch.distributed.run on 127.0.0.1, as the driver does, and return their exit status."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1", f"--nproc-per-node={n}",
+           "--master-addr", "127.0.0.1", f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    return subprocess.call(cmd)
+
+
+def plumbing(args, world, rank):
+    """The launch / barrier / max-over-ranks path of main() on CPU (gloo), without a solve: every
+    rank reports, rank 0 prints the JSON line with n_gpus = WORLD_SIZE and value null."""
+    if world > 1:
+        os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
+        dist.init_process_group("gloo", rank=rank, world_size=world)
+        dist.barrier()
+    t0 = time.perf_counter()
+    elapsed = time.perf_counter() - t0
+    seen = torch.zeros(world, dtype=torch.int64)
+    seen[rank] = 1
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        dist.all_reduce(seen)
+    print(f"bench.py rank {rank}/{world} reporting", file=sys.stderr, flush=True)
+    if rank == 0:
+        print(json.dumps({"metric": METRIC, "value": None, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
+                          "warmup": args.warmup, "plumbing": True, "ranks_reporting": int(seen.sum())}), flush=True)
+    if world > 1:
+        dist.destroy_process_group()
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--path", choices=["nmpc", "ll"], default="nmpc")
@@ -248,11 +299,24 @@ def main():
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py); default profiles/r02_pmc_traffic_c<config>.json")
+    ap.add_argument("--plumbing", action="store_true",
+                    help="CPU check of the multi-process launch only (gloo, no GPU, no solve; tests/test_bench_launch.py)")
     args = ap.parse_args()
 
+    if "WORLD_SIZE" not in os.environ and args.gpus > 1:
+        # one process per GPU: start N ranks under torch.distributed.run as CHILD processes (no
+        # GPU has been touched in this process; never exec over it) and exit with their status
+        sys.exit(launch_ranks(args.gpus))
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local_rank = int(os.environ.get("LOCAL_RANK", "0"))
+    if world != args.gpus:
+        print(f"bench.py: --gpus {args.gpus} but WORLD_SIZE={world}: refusing to report a number for another "
+              f"GPU count", file=sys.stderr)
+        sys.exit(2)
+    if args.plumbing:
+        plumbing(args, world, rank)
+        return
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
@@ -266,14 +330,9 @@ def main():
 
     cfg = dict(CONFIGS[args.config])
     A_local = args.agents or cfg["agents"]
-    A_total = A_local * world
-    if args.emulate_shards > 1 and world == 1:
-        A_total = A_local * args.emulate_shards
     N, C = cfg["N"], cfg["C"]
     p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
-    # the whole swarm is generated identically on every rank; each rank keeps its shard
-    b = workload.make_batch(A_total, N, C, seed=1234)
-    lo, hi = sdist.shard_range(A_total, max(world, args.emulate_shards), rank)
+    A_total, b, lo, hi = rank_batch(args.config, A_local, max(world, args.emulate_shards), rank)
     sh = {k: (v[lo:hi] if k not in ("obstacles", "nbr_state") else v) for k, v in b.items()}
     t = {k: torch.as_tensor(np.ascontiguousarray(v).reshape(v.shape[0], -1), dtype=torch.float64, device=dev)
          for k, v in sh.items()}
@@ -296,7 +355,8 @@ def main():
     stream = torch.cuda.Stream(dev)
     torch.cuda.set_stream(stream)
     exchange = sdist.NeighbourExchange(A_total, world, rank, dev) if cfg["K_nbr"] > 0 and world > 1 else None
-    out["sel"] = torch.zeros((n_loc, cfg["K_obs"] + cfg["K_nbr"]), dtype=torch.int32, device=dev)
+    Ko, Kn = solver.n_selected(sh["obstacles"].shape[0], A_total if cfg["K_nbr"] > 0 else 0)
+    out["sel"] = torch.zeros((n_loc, Ko + Kn), dtype=torch.int32, device=dev)
 
     def step():
         nb = exchange(nbr_local) if exchange is not None else nbr_all

@@ -33,6 +33,18 @@ extern "C" {
 #define SRB_ERR_HIP (-2)
 #define SRB_ERR_SIZE (-3)
 
+/*
+ * ABI versioning.  Every I/O struct (srb_batch, srb_prep, srb_ll_io) starts with
+ * `int struct_size`, which the caller sets to sizeof(struct) of the header it was compiled
+ * against; the library rejects any other value with SRB_ERR_ARG (srb_last_error() names
+ * the struct), so a caller built against an older or newer layout fails loudly instead of
+ * having trailing fields read from whatever follows its struct.  srb_abi_version() returns
+ * the SRB_ABI_VERSION the library was built with (bumped on any layout change).
+ *   srb_batch b = {sizeof(srb_batch)};      (C)      srb_batch b{}; b.struct_size = sizeof b;  (C++)
+ */
+#define SRB_ABI_VERSION 3
+int srb_abi_version(void);
+
 /* solver exit codes (iSWIFT GlobalOptions.h:31-34) */
 #define SRB_OPTIMAL 0
 #define SRB_KKTFAIL 1
@@ -88,11 +100,10 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *                           nbr_state; -1 = none), in the reference's scan order (sqrt distance,
  *                           lower index on ties; a static round with nothing closer than 1000 m
  *                           selects obstacle 0, as min_dist = 1000 / min_i = 0 do).  NULL = the
- *                           context's own scratch buffer, which makes the context usable from
- *                           one stream at a time; with a caller buffer per stream, calls on
- *                           different streams share nothing but read-only constants.
+ *                           context's own scratch buffer.
  */
 typedef struct srb_batch {
+    int struct_size;         /* sizeof(srb_batch) (ABI check, see SRB_ABI_VERSION) */
     const double *x0, *ref, *foot, *obstacles, *nbr_state;
     int n_obs, n_all, agent_offset;
     double *x_qp, *x, *obj;
@@ -129,7 +140,15 @@ int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
  * `stream` (a hipStream_t; NULL = the HIP null stream, which orders against every blocking
  * stream, as the CUDA/HIP convention has it).  Pass the stream that produced the inputs (the
  * Python layer passes torch's current stream, whose default is that null stream).  Call
- * srb_sync() or synchronise the stream. */
+ * srb_sync() or synchronise the stream.
+ *
+ * Ordering.  A context executes its calls in submission order, whatever stream each call
+ * names: a launch on a stream other than the previous call's first waits (hipStreamWaitEvent)
+ * for that call's work, and the host entry points (srb_solve_batch / srb_solve_qp) order
+ * after the last device launch the same way.  The context's scratch -- the selection grids
+ * and their static-table cache, the default `sel` buffer, the staging buffers and the timing
+ * events -- is therefore never used by two launches in flight.  For solves that run
+ * concurrently, use one context per stream. */
 int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
 int srb_sync(srb_ctx *ctx);
 
@@ -153,6 +172,7 @@ int srb_sync(srb_ctx *ctx);
  * contacts, 2 reference window outside the path.
  */
 typedef struct srb_prep {
+    int struct_size;         /* sizeof(srb_prep) (ABI check) */
     const double *Pr, *Prd;
     int n_rows, T, agent_offset;
     const int *agent_id, *gait_domain, *contact;
@@ -234,6 +254,7 @@ void srb_ll_params_default(srb_ll_params *p);
  *   iters    [A] int         interior-point iterations
  */
 typedef struct srb_ll_io {
+    int struct_size;         /* sizeof(srb_ll_io) (ABI check) */
     const int *ind;
     const double *q, *dq, *Dinv, *B, *H, *Jc, *dJc, *Js, *Jtoe, *Jhip, *toePos, *hipPos;
     const double *H0, *dH0, *y, *dy, *hd, *dhd, *fDes;

@@ -138,7 +138,8 @@ public:
                 throw std::runtime_error(std::string("srb_ll_ctx_create: ") + srb_last_error());
             params_ = p;
         }
-        srb_ll_io io;
+        srb_ll_io io{};
+        io.struct_size = sizeof io;          /* ABI check (SRB_ABI_VERSION) */
         io.ind = ind_.data();
         io.q = q_.data(); io.dq = dq_.data(); io.Dinv = Dinv_.data(); io.B = B_.data(); io.H = H_.data();
         io.Jc = Jc_.data(); io.dJc = dJc_.data(); io.Js = Js_.data(); io.Jtoe = Jtoe_.data(); io.Jhip = Jhip_.data();

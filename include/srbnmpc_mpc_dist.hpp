@@ -163,6 +163,7 @@ public:
         x_qp_.assign((size_t)nv, 0.0);
         double obj = 0.0;
         srb_batch b{};
+        b.struct_size = sizeof b;            /* ABI check (SRB_ABI_VERSION) */
         b.x0 = x0; b.ref = ref; b.foot = foot.data();
         b.obstacles = pobs_real_.empty() ? nullptr : pobs_real_.data();
         b.n_obs = (int)(pobs_real_.size() / 2);

@@ -129,6 +129,164 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
     Z[(size_t)(n - 1) * nz + nz - 1] = 1.0;
 }
 
+/*
+ * Active-set polish at the end of the NLP (the kernel's `polish`, srb_kernels.hip, the same
+ * rules).  Near its round-off floor the barrier system's active rows carry z/s ~ 1e14, so the
+ * interior-point iterate stops up to ~1e-4 from the optimum along soft directions.  From the
+ * final iterate, rows with s < z are taken as the active set A and the equality-constrained
+ * problem  min f(x) s.t. Aeq x = beq, g_A(x) = h_A  is solved by Newton steps on its KKT system
+ * regularised by 1/rho on the constraint block,
+ *     [H_L + rho J_A'J_A, Aeq'; Aeq, 0] dx = -(grad f + J_A'(z_A + rho c_A)),  z_A += rho (c_A + J_A dx),
+ * (H_L = Q_qp - 2 sum z_A on the obstacle positions), whose fixed point is the exact KKT point
+ * for that active set (c_A = 0).  The result replaces the iterate only if it is primal feasible
+ * (every row within ORC_POLISH_PTOL of its bound), dual feasible (z_A >= 0), the Newton
+ * iteration has converged and the reduced stationarity Z'(grad f + J_A' z_A) is at round-off
+ * level; the solve then ends OPTIMAL.  Otherwise the interior-point result stands.
+ */
+#ifndef ORC_POLISH_ON
+#define ORC_POLISH_ON 0           /* turned on together with the kernel's polish */
+#endif
+#define ORC_POLISH_RHO 1e8
+#define ORC_POLISH_IT 2           /* Newton steps per active-set pass */
+#define ORC_POLISH_PASSES 4       /* active-set passes (drop z_A < 0, add violated rows) */
+#define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
+#define ORC_POLISH_STOL 1e-9      /* |Z'(grad f + J_A' z_A)|_inf <= this * max(1, |Z' grad f|_inf, |Z'J_A'z_A|_inf) */
+
+static double g_polish_rho = ORC_POLISH_RHO;
+static double g_polish_kappa = 1e4;
+int orc_early_stats[2];
+int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */          /* exploration counters: early polish attempts failed / accepted */
+static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
+
+/* Newton steps of the regularised equality-constrained KKT for the active set `act`; returns 0
+ * on success, -1 when the reduced matrix is not positive definite */
+static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int nz, const int *act, double *xt,
+                         double *za, double *g, double *Jv, int *Ji, double *Hl, double *K, double *rhs, double *cA,
+                         double *Hr, double *HZ, int *piv, int trace)
+{
+    const int n = P->n, p = P->p, m = P->m, dim = n + p;
+    const double rho = g_polish_rho;
+    for (int it = 0; it < g_polish_it; it++) {
+        rows_eval(P, xt, g, Jv, Ji);
+        for (int r = 0; r < m; r++) cA[r] = act[r] ? g[r] - hh[r] : 0.0;
+        memset(Hl, 0, sizeof(double) * n * n);
+        for (int j = 0; j < n; j++) { Hl[j * n + j] = P->Pd[j]; rhs[j] = -(P->Pd[j] * xt[j] + P->c[j]); }
+        for (int k = 0; k < P->N; k++) {
+            double zs = 0;
+            for (int j = 0; j < P->K; j++) zs += za[P->mq + k * P->K + j];
+            Hl[(4 * k) * n + 4 * k] -= 2 * zs; Hl[(4 * k + 2) * n + 4 * k + 2] -= 2 * zs;
+        }
+        for (int r = 0; r < m; r++) {
+            if (!act[r]) continue;
+            for (int a = 0; a < 4; a++) {
+                const int ia = Ji[4 * r + a]; if (ia < 0) continue;
+                rhs[ia] -= Jv[4 * r + a] * (za[r] + rho * cA[r]);
+                for (int bb = 0; bb < 4; bb++) { const int ib = Ji[4 * r + bb]; if (ib >= 0) Hl[ia * n + ib] += rho * Jv[4 * r + a] * Jv[4 * r + bb]; }
+            }
+        }
+        /* the reduced matrix Z'(H_L + rho J_A'J_A)Z must be positive definite */
+        for (int i = 0; i < n; i++)
+            for (int a = 0; a < nz; a++) {
+                double acc = 0;
+                for (int j = 0; j < n; j++) acc += Hl[i * n + j] * Z[(size_t)j * nz + a];
+                HZ[(size_t)i * nz + a] = acc;
+            }
+        for (int a = 0; a < nz; a++)
+            for (int bb = 0; bb < nz; bb++) {
+                double acc = 0;
+                for (int i = 0; i < n; i++) acc += Z[(size_t)i * nz + a] * HZ[(size_t)i * nz + bb];
+                Hr[a * nz + bb] = acc;
+            }
+        if (orc_chol(nz, Hr)) return -1;
+        memset(K, 0, sizeof(double) * dim * dim);
+        for (int i = 0; i < n; i++) for (int j = 0; j < n; j++) K[i * dim + j] = Hl[i * n + j];
+        for (int k = 0; k < p; k++) {
+            for (int j = 0; j < n; j++) { K[(n + k) * dim + j] = P->A[(size_t)k * n + j]; K[j * dim + n + k] = P->A[(size_t)k * n + j]; }
+            rhs[n + k] = P->b[k] - dotv(P->A + (size_t)k * n, xt, n);
+        }
+        if (orc_lu(dim, K, piv)) return -1;
+        orc_lu_solve(dim, K, piv, rhs);
+        double mdx = 0.0;
+        for (int r = 0; r < m; r++) {
+            if (!act[r]) continue;
+            double jd = 0;
+            for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) jd += Jv[4 * r + t] * rhs[Ji[4 * r + t]];
+            za[r] += rho * (cA[r] + jd);
+        }
+        for (int j = 0; j < n; j++) { xt[j] += rhs[j]; mdx = fmax(mdx, fabs(rhs[j])); }
+        if (trace) fprintf(stderr, "  polish it %d: |dx| %.3e\n", it, mdx);
+    }
+    return 0;
+}
+
+/* returns 1 when the polished point is accepted (x, z replaced) */
+static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, double *x, const double *s,
+                  double *z, int trace)
+{
+    const int n = P->n, m = P->m, dim = n + P->p;
+    double *xt = malloc(sizeof(double) * n), *za = malloc(sizeof(double) * m), *g = malloc(sizeof(double) * m);
+    double *Jv = malloc(sizeof(double) * 4 * m), *Hl = malloc(sizeof(double) * n * n), *K = malloc(sizeof(double) * dim * dim);
+    double *rhs = malloc(sizeof(double) * dim), *cA = malloc(sizeof(double) * m), *v = malloc(sizeof(double) * n);
+    double *Hr = malloc(sizeof(double) * nz * nz), *HZ = malloc(sizeof(double) * (size_t)n * nz), *gr = malloc(sizeof(double) * nz);
+    int *Ji = malloc(sizeof(int) * 4 * m), *piv = malloc(sizeof(int) * dim), *act = malloc(sizeof(int) * m);
+    int ok = 0;
+    for (int r = 0; r < m; r++) { act[r] = s[r] * g_polish_kappa < z[r]; za[r] = act[r] ? z[r] : 0.0; }
+    int npass = 0;
+    for (int pass = 0; pass < g_polish_passes && !ok; pass++, npass++) {
+        memcpy(xt, x, sizeof(double) * n);
+        if (polish_newton(P, hh, Z, nz, act, xt, za, g, Jv, Ji, Hl, K, rhs, cA, Hr, HZ, piv, trace)) break;
+        rows_eval(P, xt, g, Jv, Ji);
+        double zm = 1.0, pv = -1e300, cv = 0.0, zmin = 1e300;
+        int nact = 0, changed = 0;
+        for (int r = 0; r < m; r++) {
+            pv = fmax(pv, g[r] - hh[r]);
+            if (act[r]) { nact++; zm = fmax(zm, fabs(za[r])); zmin = fmin(zmin, za[r]); cv = fmax(cv, fabs(g[r] - hh[r])); }
+        }
+        /* reduced stationarity: gradient part and multiplier part separately for the scale */
+        double gf = 0.0, gz = 0.0, res = 0.0;
+        for (int j = 0; j < n; j++) v[j] = P->Pd[j] * xt[j] + P->c[j];
+        for (int a = 0; a < nz; a++) { double acc = 0; for (int j = 0; j < n; j++) acc += Z[(size_t)j * nz + a] * v[j]; gr[a] = acc; gf = fmax(gf, fabs(acc)); }
+        for (int j = 0; j < n; j++) v[j] = 0.0;
+        for (int r = 0; r < m; r++) if (act[r]) for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) v[Ji[4 * r + t]] += Jv[4 * r + t] * za[r];
+        for (int a = 0; a < nz; a++) {
+            double acc = 0; for (int j = 0; j < n; j++) acc += Z[(size_t)j * nz + a] * v[j];
+            gz = fmax(gz, fabs(acc)); res = fmax(res, fabs(gr[a] + acc));
+        }
+        const int dual_ok = nact == 0 || zmin >= -1e-9 * zm;
+        const int stat = res <= ORC_POLISH_STOL * fmax(1.0, fmax(gf, gz));
+        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && stat;
+        if (trace)
+            fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  stat %.2e (scale %.2e)  -> %s\n",
+                    pass, nact, pv, cv, nact ? zmin : 0.0, zm, res, fmax(1.0, fmax(gf, gz)), ok ? "accepted" : "rejected");
+        if (trace > 1)
+            for (int r = 0; r < m; r++)
+                if (act[r] || g[r] - hh[r] > ORC_POLISH_PTOL)
+                    fprintf(stderr, "    row %3d (%s) act %d  s %.3e z %.3e  za %.4e  g-h %.3e\n", r,
+                            r < P->mq ? "lin" : r < P->mq + P->mo ? "obs" : "vel", act[r], s[r], z[r], za[r], g[r] - hh[r]);
+        if (ok) break;
+        /* next pass: the row with the most negative multiplier leaves the active set (one at a
+         * time: near-dependent active rows -- one obstacle at consecutive grids -- share large
+         * multipliers of both signs, and dropping all negative ones at once loses rows the
+         * solution needs), violated rows join */
+        int worst = -1;
+        for (int r = 0; r < m; r++)
+            if (act[r] && za[r] < -1e-9 * zm && (worst < 0 || za[r] < za[worst])) worst = r;
+        if (worst >= 0) { act[worst] = 0; changed = 1; }
+        for (int r = 0; r < m; r++)
+            if (!act[r] && r != worst && g[r] - hh[r] > ORC_POLISH_PTOL) { act[r] = 1; changed = 1; }
+        for (int r = 0; r < m; r++) za[r] = act[r] ? fmax(z[r], 0.0) : 0.0;
+        if (!changed) break;
+    }
+    if (ok) {
+        memcpy(x, xt, sizeof(double) * n);
+        for (int r = 0; r < m; r++) z[r] = za[r];
+    }
+    __atomic_add_fetch(&orc_polish_stats[ok ? 1 + npass : 0], 1, __ATOMIC_RELAXED);
+    free(xt); free(za); free(g); free(Jv); free(Hl); free(K); free(rhs); free(cA); free(v); free(Hr); free(HZ); free(gr);
+    free(Ji); free(piv); free(act);
+    return ok;
+}
+
 int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
                   const double *Pd, const double *c, const double *A, const double *b,
                   const double *G, const double *h,
@@ -191,7 +349,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     }
 
     const double tol = pp->tol, th = tol / sqrt(3.0);
-    const int trace = getenv("ORC_NLP_TRACE") != NULL;     /* diagnostics: per-iteration line on stderr */
+    const int trace = getenv("ORC_NLP_TRACE") ? atoi(getenv("ORC_NLP_TRACE")) + 1 : 0;   /* diagnostics on stderr (2: polish rows) */
     /* diagnostics: ORC_NLP_EXIT="fx fmu acc" scales the dual-residual threshold, the
      * complementarity threshold and the ACCEPTABLE window (exploration of exit rules only) */
     double fx = 1.0, fmu = 1.0, facc = 100.0, fdx = ORC_NLP_DXTOL;
@@ -203,6 +361,10 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     int nearwait = ORC_NLP_NEARWAIT;
     if (getenv("ORC_NLP_NEARWAIT")) nearwait = atoi(getenv("ORC_NLP_NEARWAIT"));
     double tr_sigma = 0.0;
+    double early_mu = 0.0, early_rz = 1e300;
+    int early_tried = 0, early_done = 0;
+    if (getenv("ORC_NLP_EARLY")) sscanf(getenv("ORC_NLP_EARLY"), "%lf %lf %lf", &early_mu, &early_rz, &fdx);
+    double *xe = malloc(sizeof(double) * n), *ze = malloc(sizeof(double) * m);
     for (int iter = 0; iter < pp->nlp_maxit; iter++) {
         rows_eval(&P, x, g, Jv, Ji);
         for (int j = 0; j < n; j++) rx[j] = -(Pd[j] * x[j] + c[j]) - q[j];
@@ -218,6 +380,13 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         for (int j = 0; j < n; j++) { double gj = fabs(Pd[j] * x[j] + c[j]); if (gj > gmax) gmax = gj; }
         const int pass = nrx < fx * th * gmax && nrz < th && nry < th && sz / m < fmu * tol;
         if (pass && dxlast < fdx) { flag = 0; break; }
+        /* exploration: one early polish attempt once the complementarity gap is below early_mu */
+        if (early_mu > 0 && !early_tried && sz / m < early_mu && nrz < early_rz) {
+            early_tried = 1;
+            memcpy(xe, x, sizeof(double) * n); memcpy(ze, z, sizeof(double) * m);
+            if (polish(&P, hh, Z, nz, xe, s, ze, trace)) { memcpy(x, xe, sizeof(double) * n); flag = 0; early_done = 1; __atomic_add_fetch(&orc_early_stats[1], 1, __ATOMIC_RELAXED); break; }
+            __atomic_add_fetch(&orc_early_stats[0], 1, __ATOMIC_RELAXED);
+        }
         /* near the optimum: primal and complementarity met, dual residual within 100x of its
          * threshold.  An inertia shift or a blocked step from here is the condensed system's
          * round-off (W = z/s ~ 1e14 swamps the soft curvature), not progress: ACCEPTABLE (4) */
@@ -323,6 +492,13 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         it++;
     }
     if (restore || (flag == 2 && saved)) { memcpy(x, xsave, sizeof(double) * n); flag = 4; }
+    if (getenv("ORC_POLISH_RHO")) g_polish_rho = atof(getenv("ORC_POLISH_RHO"));
+    if (getenv("ORC_POLISH_KAPPA")) g_polish_kappa = atof(getenv("ORC_POLISH_KAPPA"));
+    if (getenv("ORC_POLISH_IT")) g_polish_it = atoi(getenv("ORC_POLISH_IT"));
+    if (getenv("ORC_POLISH_PASSES")) g_polish_passes = atoi(getenv("ORC_POLISH_PASSES"));
+    const int do_polish = ORC_POLISH_ON ? getenv("ORC_NO_POLISH") == NULL : getenv("ORC_POLISH") != NULL;
+    if (do_polish && !early_done && (flag == 0 || flag == 4) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
+    free(xe); free(ze);
     memcpy(x_out, x, sizeof(double) * n);
     if (iters_out) *iters_out = it;
     free(xsave);

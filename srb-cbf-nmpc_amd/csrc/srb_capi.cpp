@@ -94,6 +94,9 @@ struct srb_ctx {
     int max_agents, device;
     hipStream_t stream;
     hipEvent_t ev[4];
+    hipEvent_t done;               // recorded after every call's work (submission-order chaining)
+    hipStream_t last;              // stream of the previous call
+    bool any;                      // a call has been submitted (done is valid)
     // device staging
     double *x0, *ref, *foot, *obstacles, *nbr, *x_qp, *x, *obj, *abuf, *alpha;
     int *status, *iters;
@@ -109,15 +112,35 @@ struct srb_ctx {
     int grid_n, grid_ver;
 };
 
-// device buffers of selection grid t for a table of n rows (grown on demand)
+// Calls on one context run in submission order (include/srbnmpc.h, "Ordering"): a call on
+// another stream than the previous one first waits for that call's work, so the context's
+// scratch (grids, the default sel buffer, staging, timing events) never serves two launches
+// in flight.
+static int order_after_last(srb_ctx *c, hipStream_t s)
+{
+    if (c->any && s != c->last) HIPCHK(hipStreamWaitEvent(s, c->done, 0));
+    return SRB_OK;
+}
+
+static int mark_done(srb_ctx *c, hipStream_t s)
+{
+    HIPCHK(hipEventRecord(c->done, s));
+    c->last = s; c->any = true;
+    return SRB_OK;
+}
+
+// device buffers of selection grid t for a table of n rows (grown on demand; the header
+// starts with ok = 0, so a grid is never read before a build has filled it)
 static int grid_reserve(srb_ctx *c, int t, size_t n)
 {
     srb_ctx::grid_buf &b = c->grid[t];
     if (!b.g) {
         HIPCHK(hipMalloc(&b.g, 64));
+        HIPCHK(hipMemset(b.g, 0, 64));
         HIPCHK(hipMalloc(&b.off, (SRB_GRID_CELLS + 1) * sizeof(int)));
     }
     if (n > b.cap) {
+        if (c->any) HIPCHK(hipEventSynchronize(c->done));   // the previous launch may still read them
         if (b.spos) HIPCHK(hipFree(b.spos));
         if (b.sidx) HIPCHK(hipFree(b.sidx));
         HIPCHK(hipMalloc(&b.spos, n * sizeof(double2)));
@@ -139,6 +162,8 @@ extern "C" void srb_params_default(srb_params *p, int N, int C)
 }
 
 extern "C" int srb_nv(const srb_params *p) { return (6 + p->C) * p->N + 1; }
+
+extern "C" int srb_abi_version(void) { return SRB_ABI_VERSION; }
 
 static void mm4(const double *X, const double *Y, double *Z)
 {
@@ -254,10 +279,12 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false; c->nw = 0; c->last_nw = 0;
     for (auto &g : c->grid) g = srb_ctx::grid_buf{nullptr, nullptr, nullptr, nullptr, 0};
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
+    c->last = nullptr; c->any = false;
     const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
+    HIPCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
     HIPCHK(hipMalloc(&c->x0, A * 4 * sizeof(double)));
     HIPCHK(hipMalloc(&c->ref, A * 4 * N * sizeof(double)));
     HIPCHK(hipMalloc(&c->foot, A * 2 * C * N * sizeof(double)));
@@ -278,6 +305,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->any) (void)hipEventSynchronize(c->done);     // the last launch may be on another stream
     void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr,
                     c->abuf, c->alpha, c->sel};
     for (void *b : bufs)
@@ -286,6 +314,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
         for (void *b : {g.g, (void *)g.off, (void *)g.spos, (void *)g.sidx})
             if (b) (void)hipFree(b);
     for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
+    (void)hipEventDestroy(c->done);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SRB_OK;
@@ -370,9 +399,16 @@ extern "C" int srb_ctx_waves(srb_ctx *c) { return c ? c->last_nw : 0; }
 
 extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch *dev_io, void *stream)
 {
+    // the layout check comes first: it needs no context (tests/test_abi.py runs it without a GPU)
+    if (dev_io && dev_io->struct_size != (int)sizeof(srb_batch))
+        return fail(SRB_ERR_ARG, "srb_batch.struct_size != sizeof(srb_batch): caller built against another ABI");
     if (!c || !dev_io) return fail(SRB_ERR_ARG, "null argument");
     hipStream_t s = (hipStream_t)stream;          // NULL: the HIP null stream (ordered with blocking streams)
-    return launch(c, n_agents, dev_io, s, c->p.use_nlp);
+    HIPCHK(hipSetDevice(c->device));
+    int rc = order_after_last(c, s);
+    if (!rc) rc = launch(c, n_agents, dev_io, s, c->p.use_nlp);
+    if (!rc && n_agents > 0) rc = mark_done(c, s);
+    return rc;
 }
 
 extern "C" __global__ void srb_prepare_kernel(int n_agents, int N, int C, int n_rows, int T, int agent_offset,
@@ -383,6 +419,9 @@ extern "C" __global__ void srb_prepare_kernel(int n_agents, int N, int C, int n_
 
 extern "C" int srb_prepare_batch_device(srb_ctx *c, int n_agents, const srb_prep *d, void *stream)
 {
+    // the layout check comes first: it needs no context (tests/test_abi.py runs it without a GPU)
+    if (d && d->struct_size != (int)sizeof(srb_prep))
+        return fail(SRB_ERR_ARG, "srb_prep.struct_size != sizeof(srb_prep): caller built against another ABI");
     if (!c || !d) return fail(SRB_ERR_ARG, "null argument");
     if (n_agents < 0) return fail(SRB_ERR_ARG, "negative n_agents");
     if (n_agents == 0) return SRB_OK;
@@ -496,6 +535,9 @@ extern "C" int srb_last_kernel_ms(srb_ctx *c, float *knn_ms, float *solve_ms)
 
 static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
 {
+    // the layout check comes first: it needs no context (tests/test_abi.py runs it without a GPU)
+    if (h && h->struct_size != (int)sizeof(srb_batch))
+        return fail(SRB_ERR_ARG, "srb_batch.struct_size != sizeof(srb_batch): caller built against another ABI");
     if (!c || !h) return fail(SRB_ERR_ARG, "null argument");
     if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
     if (n_agents == 0) return SRB_OK;
@@ -504,6 +546,7 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
     const size_t A = (size_t)n_agents;
     HIPCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
+    if (int rc0 = order_after_last(c, s)) return rc0;   // after the last device launch on this context
     if (!h->x0 || !h->ref || !h->foot || !h->x || !h->obj || !h->status || !h->iters)
         return fail(SRB_ERR_ARG, "missing buffer");
     HIPCHK(hipMemcpyAsync(c->x0, h->x0, A * 4 * sizeof(double), hipMemcpyHostToDevice, s));
@@ -541,6 +584,7 @@ static int solve_host(srb_ctx *c, int n_agents, const srb_batch *h, int use_nlp)
     d.sel = nullptr;                       // the context's scratch; copied out below when asked for
     d.obstacles_version = 0;               // staged copy: rebuilt every call
     int rc = launch(c, n_agents, &d, s, use_nlp);
+    if (!rc) rc = mark_done(c, s);
     if (rc) return rc;
     if (h->sel && use_nlp) {
         const int Ko = std::min(p->K_obs, std::max(h->n_obs, 0)), Kn = h->nbr_state ? std::min(p->K_nbr, std::max(h->n_all - 1, 0)) : 0;

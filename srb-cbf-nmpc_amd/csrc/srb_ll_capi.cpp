@@ -41,7 +41,9 @@ struct srb_ll_ctx {
     int max_agents, device;
     hipStream_t stream;
     hipEvent_t ev[2];
-    bool timed;
+    hipEvent_t done;               // recorded after every call's work (submission-order chaining)
+    hipStream_t last;              // stream of the previous call
+    bool timed, any;
     int *ind, *status, *iters;
     double *in[LL_NIN], *outb[LL_NOUT];
 };
@@ -99,6 +101,7 @@ extern "C" int srb_ll_ctx_create(const srb_ll_params *p, int max_agents, int dev
     const size_t A = (size_t)max_agents;
     LLCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
     for (int i = 0; i < 2; i++) LLCHK(hipEventCreate(&c->ev[i]));
+    LLCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
     LLCHK(hipMalloc(&c->ind, A * 4 * sizeof(int)));
     LLCHK(hipMalloc(&c->status, A * sizeof(int)));
     LLCHK(hipMalloc(&c->iters, A * sizeof(int)));
@@ -113,10 +116,12 @@ extern "C" int srb_ll_ctx_destroy(srb_ll_ctx *c)
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
     (void)hipStreamSynchronize(c->stream);
+    if (c->any) (void)hipEventSynchronize(c->done);     // the last launch may be on another stream
     (void)hipFree(c->ind); (void)hipFree(c->status); (void)hipFree(c->iters);
     for (int i = 0; i < LL_NIN; i++) (void)hipFree(c->in[i]);
     for (int i = 0; i < LL_NOUT; i++) (void)hipFree(c->outb[i]);
     for (int i = 0; i < 2; i++) (void)hipEventDestroy(c->ev[i]);
+    (void)hipEventDestroy(c->done);
     (void)hipStreamDestroy(c->stream);
     delete c;
     return SRB_OK;
@@ -135,6 +140,21 @@ static SrbLLDev to_dev(const srb_ll_io *d)
     k.tau = d->tau; k.QP_force = d->QP_force; k.ddq = d->ddq; k.dq_out = d->dq_out; k.q_out = d->q_out;
     k.V = d->V; k.dV = d->dV; k.x = d->x; k.status = d->status; k.iters = d->iters;
     return k;
+}
+
+// calls on one context run in submission order (include/srbnmpc.h, "Ordering"): a call on
+// another stream than the previous one first waits for that call's work
+static int ll_order(srb_ll_ctx *c, hipStream_t s)
+{
+    if (c->any && s != c->last) LLCHK(hipStreamWaitEvent(s, c->done, 0));
+    return SRB_OK;
+}
+
+static int ll_done(srb_ll_ctx *c, hipStream_t s)
+{
+    LLCHK(hipEventRecord(c->done, s));
+    c->last = s; c->any = true;
+    return SRB_OK;
 }
 
 static int ll_launch(srb_ll_ctx *c, int n_agents, SrbLLDev k, hipStream_t s)
@@ -156,22 +176,31 @@ static int ll_launch(srb_ll_ctx *c, int n_agents, SrbLLDev k, hipStream_t s)
 
 extern "C" int srb_ll_calc_torque_device(srb_ll_ctx *c, int n_agents, const srb_ll_io *d, void *stream)
 {
+    if (d && d->struct_size != (int)sizeof(srb_ll_io))    // layout check first (no context needed)
+        return srb_internal_fail(SRB_ERR_ARG, "srb_ll_io.struct_size != sizeof(srb_ll_io): caller built against another ABI");
     if (!c || !d) return srb_internal_fail(SRB_ERR_ARG, "null argument");
     if (n_agents < 0 || n_agents > c->max_agents) return srb_internal_fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
     if (n_agents == 0) return SRB_OK;
     LLCHK(hipSetDevice(c->device));
     SrbLLDev k = to_dev(d);
     if (!k.x) k.x = c->outb[7];   // x is optional: the context's buffer absorbs it
-    return ll_launch(c, n_agents, k, (hipStream_t)stream);      // NULL: the HIP null stream
+    hipStream_t s = (hipStream_t)stream;                         // NULL: the HIP null stream
+    int rc = ll_order(c, s);
+    if (!rc) rc = ll_launch(c, n_agents, k, s);
+    if (!rc) rc = ll_done(c, s);
+    return rc;
 }
 
 extern "C" int srb_ll_calc_torque(srb_ll_ctx *c, int n_agents, const srb_ll_io *h)
 {
+    if (h && h->struct_size != (int)sizeof(srb_ll_io))    // layout check first (no context needed)
+        return srb_internal_fail(SRB_ERR_ARG, "srb_ll_io.struct_size != sizeof(srb_ll_io): caller built against another ABI");
     if (!c || !h) return srb_internal_fail(SRB_ERR_ARG, "null argument");
     if (n_agents < 0 || n_agents > c->max_agents) return srb_internal_fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
     if (n_agents == 0) return SRB_OK;
     LLCHK(hipSetDevice(c->device));
     hipStream_t s = c->stream;
+    if (int rc0 = ll_order(c, s)) return rc0;
     const size_t A = (size_t)n_agents;
     const double *hin[LL_NIN] = {h->q, h->dq, h->Dinv, h->B, h->H, h->Jc, h->dJc, h->Js, h->Jtoe, h->Jhip,
                                  h->toePos, h->hipPos, h->H0, h->dH0, h->y, h->dy, h->hd, h->dhd, h->fDes};
@@ -186,6 +215,7 @@ extern "C" int srb_ll_calc_torque(srb_ll_ctx *c, int n_agents, const srb_ll_io *
         LLCHK(hipMemcpyAsync(c->in[i], hin[i], A * kInCount[i] * sizeof(double), hipMemcpyHostToDevice, s));
     LLCHK(hipMemcpyAsync(c->outb[0], h->tau, A * 18 * sizeof(double), hipMemcpyHostToDevice, s));   // tau is in/out
     srb_ll_io d;
+    d.struct_size = sizeof d;
     d.ind = c->ind;
     d.q = c->in[0]; d.dq = c->in[1]; d.Dinv = c->in[2]; d.B = c->in[3]; d.H = c->in[4]; d.Jc = c->in[5];
     d.dJc = c->in[6]; d.Js = c->in[7]; d.Jtoe = c->in[8]; d.Jhip = c->in[9]; d.toePos = c->in[10];
@@ -194,6 +224,7 @@ extern "C" int srb_ll_calc_torque(srb_ll_ctx *c, int n_agents, const srb_ll_io *
     d.tau = c->outb[0]; d.QP_force = c->outb[1]; d.ddq = c->outb[2]; d.dq_out = c->outb[3]; d.q_out = c->outb[4];
     d.V = c->outb[5]; d.dV = c->outb[6]; d.x = c->outb[7]; d.status = c->status; d.iters = c->iters;
     int rc = ll_launch(c, n_agents, to_dev(&d), s);
+    if (!rc) rc = ll_done(c, s);
     if (rc) return rc;
     for (int i = 0; i < LL_NOUT; i++)
         if (hout[i]) LLCHK(hipMemcpyAsync(hout[i], c->outb[i], A * kOutCount[i] * sizeof(double), hipMemcpyDeviceToHost, s));

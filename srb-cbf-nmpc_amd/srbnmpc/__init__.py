@@ -26,6 +26,7 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 
 OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
+ABI_VERSION = 3                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 
 class Params(ctypes.Structure):
@@ -46,19 +47,25 @@ class Params(ctypes.Structure):
 
 
 class Batch(ctypes.Structure):
-    """Mirror of srb_batch."""
-    _fields_ = [("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
+    """Mirror of srb_batch (struct_size is filled in by the constructor)."""
+    _fields_ = [("struct_size", ctypes.c_int), ("x0", _dp), ("ref", _dp), ("foot", _dp), ("obstacles", _dp), ("nbr_state", _dp),
                 ("n_obs", ctypes.c_int), ("n_all", ctypes.c_int), ("agent_offset", ctypes.c_int),
                 ("x_qp", _dp), ("x", _dp), ("obj", _dp), ("status", _ip), ("iters", _ip),
                 ("alpha_buf", _dp), ("alpha", _dp), ("sel", _ip), ("obstacles_version", ctypes.c_int)]
 
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(Batch), *args, **kw)
+
 
 class Prep(ctypes.Structure):
-    """Mirror of srb_prep (input assembly on the device)."""
-    _fields_ = [("Pr", _dp), ("Prd", _dp), ("n_rows", ctypes.c_int), ("T", ctypes.c_int), ("agent_offset", ctypes.c_int),
+    """Mirror of srb_prep (input assembly on the device; struct_size filled in)."""
+    _fields_ = [("struct_size", ctypes.c_int), ("Pr", _dp), ("Prd", _dp), ("n_rows", ctypes.c_int), ("T", ctypes.c_int), ("agent_offset", ctypes.c_int),
                 ("agent_id", _ip), ("gait_domain", _ip), ("contact", _ip),
                 ("toe", _dp), ("start", _dp), ("q", _dp), ("dq", _dp),
                 ("x0", _dp), ("ref", _dp), ("foot", _dp), ("last_state", _dp), ("status", _ip)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(Prep), *args, **kw)
 
 
 _lib = None
@@ -87,6 +94,8 @@ def lib():
         L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
         L.srb_fit_bezier.argtypes = [_dp, _dp, _dp]
         L.srb_last_error.restype = ctypes.c_char_p
+        if L.srb_abi_version() != ABI_VERSION:
+            raise RuntimeError(f"srbnmpc: {LIB_PATH} has ABI {L.srb_abi_version()}, these bindings {ABI_VERSION} (rebuild)")
         _lib = L
     return _lib
 
@@ -202,8 +211,12 @@ class BatchSolver:
         Ko, Kn = self.n_selected(0 if obstacles is None else obstacles.shape[0],
                                  0 if nbr_state is None else nbr_state.shape[0])
         sel = out.get("sel")
-        if sel is not None and (sel.dtype != torch_int32() or sel.numel() < A * (Ko + Kn) or not sel.is_contiguous()):
-            raise ValueError(f"out['sel'] must be a contiguous int32 tensor of at least {A} x {Ko + Kn}")
+        # the kernel writes rows of stride Ko + Kn (K clamped to the table sizes): the tensor must
+        # have exactly that row length, or its rows would be read misaligned
+        if sel is not None and (sel.dtype != torch_int32() or tuple(sel.shape) != (A, Ko + Kn) or not sel.is_contiguous()):
+            raise ValueError(f"out['sel'] must be a contiguous int32 tensor of shape ({A}, {Ko + Kn}) "
+                             f"(K_obs, K_nbr clamped to the table sizes: BatchSolver.n_selected), got "
+                             f"{tuple(sel.shape)} {sel.dtype}")
         b = Batch(dptr(x0), dptr(ref), dptr(foot), dptr(obstacles), dptr(nbr_state),
                   0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],
                   int(agent_offset), dptr(out.get("x_qp")), dptr(out["x"]), dptr(out["obj"]),

@@ -33,10 +33,13 @@ class LLParams(ctypes.Structure):
 
 class LLIO(ctypes.Structure):
     """Mirror of srb_ll_io."""
-    _fields_ = [("ind", _ip)] + [(k, _dp) for k in (
+    _fields_ = [("struct_size", ctypes.c_int), ("ind", _ip)] + [(k, _dp) for k in (
         "q", "dq", "Dinv", "B", "H", "Jc", "dJc", "Js", "Jtoe", "Jhip", "toePos", "hipPos",
         "H0", "dH0", "y", "dy", "hd", "dhd", "fDes",
         "tau", "QP_force", "ddq", "dq_out", "q_out", "V", "dV", "x")] + [("status", _ip), ("iters", _ip)]
+
+    def __init__(self, *args, **kw):
+        super().__init__(ctypes.sizeof(LLIO), *args, **kw)
 
 
 _bound = False

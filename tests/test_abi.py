@@ -150,3 +150,29 @@ def test_ll_no_silent_cpu_fallback_without_gpu():
         pytest.skip("GPU present")
     with pytest.raises(RuntimeError):
         srbnmpc.LowLevelCtrl(max_agents=4)
+
+
+def test_abi_version_and_struct_size_checks():
+    """Versioned C ABI (include/srbnmpc.h SRB_ABI_VERSION): every I/O struct starts with
+    struct_size; a caller built against another layout (an older header without the field, or a
+    shorter / longer struct) is rejected with SRB_ERR_ARG before any buffer or device is used."""
+    from srbnmpc import lowlevel
+    lib = srbnmpc.lib()
+    hdr = open(os.path.join(ROOT, "include", "srbnmpc.h")).read()
+    assert lib.srb_abi_version() == int(re.search(r"#define SRB_ABI_VERSION (\d+)", hdr).group(1)) == srbnmpc.ABI_VERSION
+    for cls, fn in ((srbnmpc.Batch, "srb_solve_batch"), (srbnmpc.Batch, "srb_solve_qp"),
+                    (srbnmpc.Batch, "srb_solve_batch_device"), (srbnmpc.Prep, "srb_prepare_batch_device"),
+                    (lowlevel.LLIO, "srb_ll_calc_torque"), (lowlevel.LLIO, "srb_ll_calc_torque_device")):
+        b = cls()
+        assert b.struct_size == ctypes.sizeof(cls)
+        f = getattr(lib if not fn.startswith("srb_ll") else lowlevel._bind(), fn)
+        args = lambda s: (None, 1, ctypes.byref(s)) + ((None,) if fn.endswith("device") else ())
+        f.argtypes = None
+        for bad in (0, ctypes.sizeof(cls) - 8, ctypes.sizeof(cls) + 8, 0x5a5a5a5a):
+            b.struct_size = bad
+            assert f(*args(b)) == -1, (fn, bad)
+            assert b"struct_size" in lib.srb_last_error(), fn
+        b.struct_size = ctypes.sizeof(cls)
+        assert f(*args(b)) == -1 and b"null argument" in lib.srb_last_error()   # passes the layout check
+    # the mirrors match the C layout: struct_size first, then the pointers 8-byte aligned
+    assert srbnmpc.Batch.x0.offset == 8 and srbnmpc.Prep.Pr.offset == 8 and lowlevel.LLIO.ind.offset == 8

@@ -1,0 +1,134 @@
+"""End-to-end parity of the 8-GPU per-rank workloads on one GPU (BASELINE configs[3] and
+configs[4]; VERDICT r02 "Next round" item 1).
+
+On an 8-GPU node every rank solves its contiguous block of the swarm against the WHOLE
+neighbour snapshot (the get_lastState() row of every agent after the all-gather,
+/root/reference/include/shared_structs.hpp:94, /root/reference/src/MPC_dist.cpp:1272-1276)
+and the whole obstacle arena.  These tests build rank 0's and rank 7's inputs exactly as
+`bench.py --config 4|5` does under torchrun (bench.rank_batch: the same generator, seed and
+shard bounds), pass them through the device entry point with agent_offset = lo, the
+selection grids (tables of 8192+ rows; the static obstacle grid kept across calls by
+obstacles_version) and check:
+
+  * the selected obstacle / neighbour rows of EVERY agent == the oracle's scan
+    (oracle.select_idx: sqrt distance, lower index on ties, MPC_dist.cpp:371-382);
+  * X, U, s of a sample of 128 agents within NLP_TOL = 1e-4 of oracle.solve_batch (the same
+    global agent index, so the agent excludes itself from its neighbours), statuses equal;
+  * size-independent properties on every agent of the shard (dynamics, u = F lambda,
+    sum lambda = 1, bounds, CoM-CoP box, velocity rows, obstacle rows d^2 + s >= eps);
+  * a second call with the kept obstacle grid is bit-identical to the first.
+"""
+import os
+import sys
+from concurrent.futures import ThreadPoolExecutor
+
+import numpy as np
+import pytest
+from conftest import ROOT
+
+import oracle
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("no GPU", allow_module_level=True)
+
+sys.path.insert(0, ROOT)
+import bench  # noqa: E402
+import srbnmpc  # noqa: E402
+
+NLP_TOL = 1e-4
+
+
+def _xus(N, x):
+    return np.concatenate([x[..., :6 * N], x[..., -1:]], -1)
+
+
+def _run_shard(config, world, rank, agents_per_gpu):
+    cfg = bench.CONFIGS[config]
+    N, C, Ko, Kn = cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"]
+    A_total, b, lo, hi = bench.rank_batch(config, agents_per_gpu, world, rank)
+    n = hi - lo
+    dev = torch.device("cuda:0")
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    x0, ref, foot = T(b["x0"][lo:hi]), T(b["ref"][lo:hi]), T(b["foot"][lo:hi].reshape(n, -1))
+    obst, nbr = T(b["obstacles"]), T(b["nbr_state"])
+    alpha_buf = torch.stack([x0[:, 0], torch.zeros_like(x0[:, 0]), x0[:, 2], torch.zeros_like(x0[:, 0])], 1).contiguous()
+    s = srbnmpc.BatchSolver(srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn), n)
+    Kos, Kns = s.n_selected(obst.shape[0], nbr.shape[0])
+    outs = []
+    for _ in range(2):                     # the second call reuses the static obstacle grid
+        o = dict(x_qp=torch.zeros((n, s.params.nv), dtype=torch.float64, device=dev),
+                 x=torch.zeros((n, s.params.nv), dtype=torch.float64, device=dev),
+                 obj=torch.zeros(n, dtype=torch.float64, device=dev),
+                 status=torch.zeros((n, 2), dtype=torch.int32, device=dev),
+                 iters=torch.zeros((n, 2), dtype=torch.int32, device=dev),
+                 alpha=torch.zeros((n, 20), dtype=torch.float64, device=dev),
+                 sel=torch.full((n, Kos + Kns), -2, dtype=torch.int32, device=dev))
+        s.solve_device(x0, ref, foot, obst, nbr, o, agent_offset=lo, alpha_buf=alpha_buf, obstacles_version=1)
+        torch.cuda.synchronize()
+        outs.append({k: v.cpu().numpy() for k, v in o.items()})
+    s.close()
+    for k in outs[0]:
+        np.testing.assert_array_equal(outs[0][k], outs[1][k], err_msg=f"grid reuse changed {k}")
+    return cfg, b, lo, hi, outs[0]
+
+
+def _oracle_one(op, b, g):
+    r = oracle.solve_batch(op, b["x0"][g:g + 1], b["ref"][g:g + 1], b["foot"][g:g + 1], b["obstacles"],
+                           b["nbr_state"], agent_offset=g, nthreads=1)
+    return {k: v[0] for k, v in r.items()}
+
+
+@pytest.mark.parametrize("config,rank", [(4, 0), (4, 7), (5, 0), (5, 7)])
+def test_rank_shard_of_8gpu_swarm_vs_oracle(config, rank):
+    """configs[3] (config 4: 8192 agents, N = 10, 1024 per rank, 40960 obstacles, 8192-row
+    snapshot) and configs[4] (config 5: 16384 agents, N = 20, 2048 per rank, 81920 obstacles,
+    16384-row snapshot) -- rank 0's and rank 7's shard."""
+    world = 8
+    agents = bench.CONFIGS[config]["agents"]
+    cfg, b, lo, hi, out = _run_shard(config, world, rank, agents)
+    N, C, Ko, Kn = cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"]
+    n = hi - lo
+    assert b["nbr_state"].shape[0] == world * agents and b["obstacles"].shape[0] >= 8192 * 5 * world // 8
+    op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+    # 1. selected rows, every agent, index for index
+    want = np.array([oracle.select_idx(op, b["x0"][lo + a], b["obstacles"], b["nbr_state"], lo + a) for a in range(n)],
+                    np.int32)
+    np.testing.assert_array_equal(out["sel"], want)
+    assert not np.any(out["sel"][:, Ko:] == (lo + np.arange(n))[:, None])        # never itself
+    # 2. a sample of 128 agents against the oracle, same global index
+    rng = np.random.default_rng(100 * config + rank)
+    smp = np.sort(rng.choice(n, 128, replace=False))
+    with ThreadPoolExecutor(16) as ex:
+        ref = list(ex.map(lambda a: _oracle_one(op, b, lo + int(a)), smp))
+    st_o = np.array([r["status"] for r in ref]); x_o = np.array([r["x"] for r in ref])
+    assert (out["status"][smp] == st_o).all(), [(int(a), out["status"][a].tolist(), s.tolist())
+                                                for a, s in zip(smp, st_o) if (out["status"][a] != s).any()]
+    e = np.abs(_xus(N, out["x"][smp]) - _xus(N, x_o)).max(1)
+    assert e.max() < NLP_TOL, (int(smp[np.argmax(e)]), float(e.max()))
+    np.testing.assert_allclose(out["x_qp"][smp][:, :6 * N], np.array([r["x_qp"] for r in ref])[:, :6 * N], atol=1e-6)
+    # 3. properties on every agent of the shard
+    st = out["status"]
+    assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
+    p = srbnmpc.default_params(N, C)
+    x = out["x"]
+    Ad, Bd = oracle.lip(oracle.params(N, C))
+    Xs, U, L, sl = srbnmpc.split(p, x)
+    prev = b["x0"][lo:hi]
+    for k in range(N):
+        assert np.abs(prev @ Ad.T + U[:, k] @ Bd.T - Xs[:, k]).max() < 1e-9          # dynamics
+        prev = Xs[:, k]
+    np.testing.assert_allclose(L.sum(-1), 1.0, atol=1e-9)
+    np.testing.assert_allclose(U, np.einsum("akdc,akc->akd", b["foot"][lo:hi], L), atol=1e-9)
+    assert L.min() > -1e-7 and L.max() < 1 + 1e-7
+    assert np.abs(Xs[:, :-1][..., [0, 2]] - U[:, 1:]).max() < p.mu * p.hcom / np.sqrt(2) + 1e-6
+    assert np.abs(Xs[..., [1, 3]]).max() < p.vsat + 1e-6
+    for a in range(n):
+        obs, eps = oracle.select_obstacles(op, b["x0"][lo + a], b["obstacles"], b["nbr_state"], lo + a)
+        d2 = ((Xs[a][:, None, [0, 2]] - obs) ** 2).sum(-1)
+        assert (d2 + sl[a] - eps[None, :]).min() > -1e-6, a
+    # 4. the fused Bezier epilogue on the shard (alpha_COM of the start buffer)
+    X = x[:, :16].reshape(n, 4, 4)
+    np.testing.assert_allclose(out["alpha"].reshape(n, 4, 5)[:, :, 4], X[:, 3], atol=1e-9)
