@@ -294,6 +294,8 @@ def main():
     ap.add_argument("--cpu-seconds", type=float, default=12.0)
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
+    ap.add_argument("--qp-init", type=int, default=1,
+                    help="QP-stage start: 1 scaled (default), 0 iSWIFT's kkt_initialize (srb_ctx_set_qp_init)")
     ap.add_argument("--emulate-shards", type=int, default=1,
                     help="diagnostic: solve rank 0's shard of a swarm this many GPUs wide on one GPU (the whole "
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
@@ -350,6 +352,7 @@ def main():
                iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev))
     solver = srbnmpc.BatchSolver(p, n_loc, local_rank)
     solver.set_waves(args.waves)
+    solver.set_qp_init(args.qp_init)
     # one explicit stream for the collective, both kernels and the timing events (the C ABI
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)
@@ -366,10 +369,11 @@ def main():
     for _ in range(args.warmup):
         step()
     torch.cuda.synchronize(dev)
-    kern = []
+    kern, pol = [], []
     for _ in range(3):            # kernel duration on the stream it runs on (HIP events in the C ABI)
         step()
         kern.append(solver.last_kernel_ms())
+        pol.append(solver.last_polish_ms())
     ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
     if world > 1:
         dist.barrier()
@@ -399,7 +403,7 @@ def main():
     solve_ms = float(np.median([k[1] for k in kern]))
     flops = executed_flops(p, iters, cfg["K_obs"] + cfg["K_nbr"])
     achieved = flops / (solve_ms * 1e-3) / 1e12
-    dense_eq = dense_equiv_flops(p, iters) / (solve_ms * 1e-3) / 1e12
+    dense_per_solve = dense_equiv_flops(p, iters) / max(1, iters.shape[0])
     cyc_iter = solve_ms * 1e-3 * SCLK_GHZ * 1e9 / max(1, int(iters.sum(1).max()))
     traffic = None
     if args.traffic_json is None:
@@ -423,6 +427,12 @@ def main():
         "optimal_frac": float((status == 0).all(1).mean()),
         "acceptable_frac": float(((status[:, 0] == 0) & (status[:, 1] == 4)).mean()),
         "iters_mean": [float(iters[:, 0].mean()), float(iters[:, 1].mean())],
+        "iters_max": [int(iters[:, 0].max()), int(iters[:, 1].max())],
+        "qp_init": args.qp_init,
+        "dense_kkt_flops_per_solve": dense_per_solve,
+        "dense_kkt_flops_note": "SURVEY.md 8(d) work-equivalence figure: (2/3) d^3 + 4 d^2 per IPM iteration of the "
+                                "unreduced dense KKT (d = nv + neq) x this batch's iterations, per solve; a "
+                                "comparison with a dense-KKT solver, not executed flops and not a rate",
         "roofline": {"bound": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
                      "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
                      "cycles_per_iter": cyc_iter,
@@ -433,7 +443,7 @@ def main():
                      "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
                                    "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
                                    "agent), neither MFMA- nor HBM-throughput-bound",
-                     "dense_equivalent_tflops": dense_eq,
+                     "polish_ms": float(np.median(pol)), "polish_kernel": "srb_polish_kernel",
                      "io_bytes_per_launch": io_bytes(p, n_loc, sh["obstacles"].shape[0], A_total if cfg["K_nbr"] else 0)},
         "cpu_baseline": None,
     }

@@ -130,6 +130,13 @@ int srb_ctx_destroy(srb_ctx *ctx);
 int srb_ctx_set_waves(srb_ctx *ctx, int nw);
 int srb_ctx_waves(srb_ctx *ctx);
 
+/* QP-stage starting point: 1 (default) the scaled start s = max(h - Gx, 0.1), z = 1/s from the
+ * least-squares x of iSWIFT's kkt_initialize (Auxilary.c:680-755); 0 iSWIFT's own shifted start
+ * (z + 1 + max(h - Gx): ~1e3 with the +-1e3 boxes of MPC_dist.cpp:317-318), which follows the
+ * genuine iSWIFT step for step (tests/test_gpu_parity.py) but needs up to twice the iterations on
+ * the slowest agents.  Both end at the QP optimum to the solver tolerance. */
+int srb_ctx_set_qp_init(srb_ctx *ctx, int mode);
+
 /* Host buffers: copies in, solves, copies out, synchronises.  n_agents <= max_agents. */
 int srb_solve_batch(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
 
@@ -197,6 +204,9 @@ int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, in
  * the stream the kernel ran on (ms): knn_ms the obstacle / neighbour selection kernel
  * (0 when nothing is selected: QP only, or K_obs = K_nbr = 0), solve_ms the solve kernel. */
 int srb_last_kernel_ms(srb_ctx *ctx, float *knn_ms, float *solve_ms);
+/* ... and of the active-set polish of the NLP result (srb_polish_kernel, launched right after the
+ * solve kernel), ms. */
+int srb_last_polish_ms(srb_ctx *ctx, float *polish_ms);
 
 /* Dynamic LDS bytes one agent's workgroup uses (for occupancy reports). */
 int srb_lds_bytes(const srb_params *p);

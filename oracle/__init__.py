@@ -33,7 +33,8 @@ class OrcParams(ctypes.Structure):
                 ("Qw", ctypes.c_double), ("Pw", ctypes.c_double), ("Rw", ctypes.c_double), ("Sw", ctypes.c_double),
                 ("box", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
                 ("vsat", ctypes.c_double), ("tol", ctypes.c_double),
-                ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int), ("use_nlp", ctypes.c_int)]
+                ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int), ("use_nlp", ctypes.c_int),
+                ("qp_init", ctypes.c_int)]
 
 
 def build(force: bool = False) -> None:

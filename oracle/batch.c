@@ -23,7 +23,7 @@ int orc_solve_agent(const orc_params *p_in, const double x0[4], const double *re
     double *G = malloc(sizeof(double) * (size_t)mq * nv), *h = malloc(sizeof(double) * mq);
     double *xq = malloc(sizeof(double) * nv);
     orc_build_qp(p, x0, ref, foot, Pd, c, A, b, G, h);
-    status[0] = orc_qp_solve(nv, mq, neq, Pd, c, A, b, G, h, p->qp_maxit, p->tol, xq, NULL, &iters[0]);
+    status[0] = orc_qp_solve_init(nv, mq, neq, Pd, c, A, b, G, h, p->qp_maxit, p->tol, p->qp_init, xq, NULL, &iters[0]);
     if (x_qp) memcpy(x_qp, xq, sizeof(double) * nv);
     status[1] = 0; iters[1] = 0;
     if (p->use_nlp) {

@@ -144,16 +144,17 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
  * level; the solve then ends OPTIMAL.  Otherwise the interior-point result stands.
  */
 #ifndef ORC_POLISH_ON
-#define ORC_POLISH_ON 0           /* turned on together with the kernel's polish */
+#define ORC_POLISH_ON 1           /* the kernel's SRB_POLISH_ON */
 #endif
 #define ORC_POLISH_RHO 1e8
-#define ORC_POLISH_IT 2           /* Newton steps per active-set pass */
-#define ORC_POLISH_PASSES 4       /* active-set passes (drop z_A < 0, add violated rows) */
+#define ORC_POLISH_IT 3           /* at most this many Newton steps per active-set pass */
+#define ORC_POLISH_PASSES 2       /* active-set passes (the most negative z_A leaves, violated rows join) */
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
-#define ORC_POLISH_STOL 1e-9      /* |Z'(grad f + J_A' z_A)|_inf <= this * max(1, |Z' grad f|_inf, |Z'J_A'z_A|_inf) */
+#define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
 
 static double g_polish_rho = ORC_POLISH_RHO;
 static double g_polish_kappa = 1e4;
+static int g_polish_zinit = 1;    /* exploration: 1 = a later pass starts from the previous pass's z_A */
 int orc_early_stats[2];
 int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */          /* exploration counters: early polish attempts failed / accepted */
 static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
@@ -162,7 +163,7 @@ static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
  * on success, -1 when the reduced matrix is not positive definite */
 static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int nz, const int *act, double *xt,
                          double *za, double *g, double *Jv, int *Ji, double *Hl, double *K, double *rhs, double *cA,
-                         double *Hr, double *HZ, int *piv, int trace)
+                         double *Hr, double *HZ, int *piv, double *lastdx, int trace)
 {
     const int n = P->n, p = P->p, m = P->m, dim = n + p;
     const double rho = g_polish_rho;
@@ -214,7 +215,10 @@ static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int 
             za[r] += rho * (cA[r] + jd);
         }
         for (int j = 0; j < n; j++) { xt[j] += rhs[j]; mdx = fmax(mdx, fabs(rhs[j])); }
+        *lastdx = mdx;
+        __atomic_add_fetch(&orc_polish_stats[15], 1, __ATOMIC_RELAXED);
         if (trace) fprintf(stderr, "  polish it %d: |dx| %.3e\n", it, mdx);
+        if (mdx <= ORC_POLISH_DXTOL) break;            /* converged: no further step */
     }
     return 0;
 }
@@ -234,7 +238,8 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
     int npass = 0;
     for (int pass = 0; pass < g_polish_passes && !ok; pass++, npass++) {
         memcpy(xt, x, sizeof(double) * n);
-        if (polish_newton(P, hh, Z, nz, act, xt, za, g, Jv, Ji, Hl, K, rhs, cA, Hr, HZ, piv, trace)) break;
+        double lastdx = 1e300;
+        if (polish_newton(P, hh, Z, nz, act, xt, za, g, Jv, Ji, Hl, K, rhs, cA, Hr, HZ, piv, &lastdx, trace)) break;
         rows_eval(P, xt, g, Jv, Ji);
         double zm = 1.0, pv = -1e300, cv = 0.0, zmin = 1e300;
         int nact = 0, changed = 0;
@@ -253,11 +258,13 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
             gz = fmax(gz, fabs(acc)); res = fmax(res, fabs(gr[a] + acc));
         }
         const int dual_ok = nact == 0 || zmin >= -1e-9 * zm;
-        const int stat = res <= ORC_POLISH_STOL * fmax(1.0, fmax(gf, gz));
-        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && stat;
+        /* converged Newton iteration (the last correction) stands for stationarity: the step solves
+         * grad f + H dx + J_A' z_A+ = 0, so at x + dx the reduced gradient of the Lagrangian is
+         * O(|H| |dx|); `res` (the reduced stationarity itself) is reported by the trace only */
+        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL;
         if (trace)
-            fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  stat %.2e (scale %.2e)  -> %s\n",
-                    pass, nact, pv, cv, nact ? zmin : 0.0, zm, res, fmax(1.0, fmax(gf, gz)), ok ? "accepted" : "rejected");
+            fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  last dx %.2e  stat %.2e (scale %.2e)  -> %s\n",
+                    pass, nact, pv, cv, nact ? zmin : 0.0, zm, lastdx, res, fmax(1.0, fmax(gf, gz)), ok ? "accepted" : "rejected");
         if (trace > 1)
             for (int r = 0; r < m; r++)
                 if (act[r] || g[r] - hh[r] > ORC_POLISH_PTOL)
@@ -274,7 +281,7 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
         if (worst >= 0) { act[worst] = 0; changed = 1; }
         for (int r = 0; r < m; r++)
             if (!act[r] && r != worst && g[r] - hh[r] > ORC_POLISH_PTOL) { act[r] = 1; changed = 1; }
-        for (int r = 0; r < m; r++) za[r] = act[r] ? fmax(z[r], 0.0) : 0.0;
+        for (int r = 0; r < m; r++) za[r] = act[r] ? (g_polish_zinit ? fmax(za[r], 0.0) : fmax(z[r], 0.0)) : 0.0;
         if (!changed) break;
     }
     if (ok) {
@@ -329,11 +336,16 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
 
     memcpy(x, x_init, sizeof(double) * n);
     rows_eval(&P, x, g, Jv, Ji);
-    {   /* slacks: iSWIFT-style shift of h - g(x); duals ORC_NLP_Z0 (the kernel's SRB_NLP_Z0) */
+    {   /* slacks: iSWIFT-style shift of h - g(x); duals below */
         double mn = hh[0] - g[0];
         for (int r = 1; r < m; r++) if (hh[r] - g[r] < mn) mn = hh[r] - g[r];
         double ap = -mn;
         for (int r = 0; r < m; r++) { s[r] = (ap < 0) ? hh[r] - g[r] : hh[r] - g[r] + (1 + ap); z[r] = ORC_NLP_Z0; }
+        /* duals z_r = ORC_NLP_Z0 / s_r (round 3; the kernel's SRB_NLP_Z0, the same rule): every row
+         * starts at complementarity Z0 instead of z = Z0 on rows whose slack is far from the
+         * bound (the +-1e3 boxes); on the bench batches the NLP needs 8.1 / 8.5 iterations on
+         * average against 8.9 / 9.3 (N = 10 / 20) and at most 12 / 13 against 13 / 17 */
+        for (int r = 0; r < m; r++) z[r] = ORC_NLP_Z0 / s[r];
     }
     {   /* q = A'y, y = argmin |A'y + (Px + c + J'z)|  ->  (A A') y = -A v */
         double *v = malloc(sizeof(double) * n), *AAt = malloc(sizeof(double) * (p ? p * p : 1)), *yy = malloc(sizeof(double) * (p + 1));
@@ -493,11 +505,12 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     }
     if (restore || (flag == 2 && saved)) { memcpy(x, xsave, sizeof(double) * n); flag = 4; }
     if (getenv("ORC_POLISH_RHO")) g_polish_rho = atof(getenv("ORC_POLISH_RHO"));
+    if (getenv("ORC_POLISH_ZINIT")) g_polish_zinit = atoi(getenv("ORC_POLISH_ZINIT"));
     if (getenv("ORC_POLISH_KAPPA")) g_polish_kappa = atof(getenv("ORC_POLISH_KAPPA"));
     if (getenv("ORC_POLISH_IT")) g_polish_it = atoi(getenv("ORC_POLISH_IT"));
     if (getenv("ORC_POLISH_PASSES")) g_polish_passes = atoi(getenv("ORC_POLISH_PASSES"));
     const int do_polish = ORC_POLISH_ON ? getenv("ORC_NO_POLISH") == NULL : getenv("ORC_POLISH") != NULL;
-    if (do_polish && !early_done && (flag == 0 || flag == 4) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
+    if (do_polish && !early_done && (flag == 0 || flag == 4 || flag == 2) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
     free(xe); free(ze);
     memcpy(x_out, x, sizeof(double) * n);
     if (iters_out) *iters_out = it;

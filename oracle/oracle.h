@@ -39,6 +39,7 @@ typedef struct orc_params {
     double tol;                         /* 1e-6                    (GlobalOptions.h:24-25)    */
     int qp_maxit, nlp_maxit;            /* 25 (GlobalOptions.h:23), 50                        */
     int use_nlp;                        /* MPC_dist::use_snopt                                */
+    int qp_init;                        /* QP starting point: 1 scaled (the kernel's default), 0 iSWIFT's kkt_initialize */
 } orc_params;
 
 void orc_params_default(orc_params *p, int N, int C);
@@ -77,6 +78,10 @@ void orc_select_obstacles(const orc_params *p, const double x0[4],
                           double *obs_out, double *eps_out);
 
 /* iSWIFT algorithm restated (Prime.c:127-230, Auxilary.c); returns 0..3 exit code. */
+/* qp_init: 0 = iSWIFT's kkt_initialize (Auxilary.c:680-755), 1 = scaled start (qp_ipm.c) */
+int orc_qp_solve_init(int n, int m, int p, const double *Pd, const double *c, const double *A, const double *b,
+                      const double *G, const double *h, int maxit, double tol, int qp_init, double *x_out, double *q_out,
+                      int *iters_out);
 int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
                  const double *A, const double *b, const double *G, const double *h,
                  int maxit, double tol, double *x_out, double *q_out, int *iters_out);

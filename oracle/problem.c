@@ -23,6 +23,7 @@ void orc_params_default(orc_params *p, int N, int C)
     p->qp_maxit = 25;                    /* GlobalOptions.h:23 */
     p->nlp_maxit = 50;
     p->use_nlp = 1;
+    p->qp_init = 1;                      /* scaled QP start (qp_ipm.c); 0 = iSWIFT's kkt_initialize */
 }
 
 int orc_nv(const orc_params *p) { return (6 + p->C) * p->N + 1; }

@@ -14,6 +14,7 @@
  * P + G'W^-1 G is O(mu) and A H^-1 A' loses definiteness to round-off near convergence.)
  */
 #include <math.h>
+#include <stdio.h>
 #include <stdlib.h>
 #include <string.h>
 #include "oracle.h"
@@ -138,7 +139,7 @@ static double steplen(const double *v, const double *dv, int m)
 static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf, const double *c,
                          const double *A, const double *b, const double *G, const double *h,
                          int maxit, double tol, double *x_out, double *q_out, int *iters_out, int no_trap,
-                         int *trapped)
+                         int *trapped, int qp_init)
 {
     kktws w;
     ws_init(&w, n, m, p, Pd, A, G);
@@ -165,6 +166,14 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
         double ap = -mn, ad = mx;
         for (int r = 0; r < m; r++) s[r] = (ap < 0) ? zi[r] : zi[r] + (1 + ap);
         for (int r = 0; r < m; r++) z[r] = (ad < 0) ? -zi[r] : -zi[r] + (1 + ad);
+        /* scaled start (qp_init = 1, the kernel's default): the same x, s_r = max(h_r - (Gx)_r, 0.1),
+         * z_r = 1 / s_r.  iSWIFT shifts every z by 1 + max_r(h - Gx)_r, which the +-1e3 boxes on X
+         * and U (MPC_dist.cpp:317-318) make ~1e3: mu starts near 5e4, the dual steps stay blocked
+         * (alpha_d 0.01-0.1) for many iterations, and the slowest bench agents need 18-19; from the
+         * scaled start the same QPs take at most 9 and end within 4e-8 of iSWIFT's point
+         * (DESIGN.md 3).  iSWIFT's start stays available (qp_init = 0) for step-for-step checks. */
+        if (qp_init == 1)
+            for (int r = 0; r < m; r++) { s[r] = fmax(zi[r], 0.1); z[r] = 1.0 / s[r]; }
     }
 
     double sigma = 100.0;                  /* options->sigma = SIGMA (GlobalOptions.h:26) */
@@ -219,6 +228,9 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
         kkt_solve(&w, wgt, rx, ry, r3, dx, dy, dz);           /* kktsolve_2 */
         for (int r = 0; r < m; r++) dsv[r] = (ds[r] - s[r] * dz[r]) / z[r];
         alpha_p = steplen(s, dsv, m); alpha_d = steplen(z, dz, m);
+        if (getenv("ORC_QP_TRACE"))
+            fprintf(stderr, "  qp %2d  |rx| %.2e |rz| %.2e |ry| %.2e  mu %.2e  ap %.3f ad %.3f sigma %.2e\n", i, norm2(rx, n),
+                    norm2(rz, m), norm2(ry, p), dot(s, z, m) / m, alpha_p, alpha_d, sigma);
         alpha_p = 0.99 * alpha_p < 1.0 ? 0.99 * alpha_p : 1.0;
         alpha_d = 0.99 * alpha_d < 1.0 ? 0.99 * alpha_d : 1.0;
         for (int j = 0; j < n; j++) x[j] += dx[j] * alpha_p;
@@ -239,11 +251,18 @@ done:
     return flag;
 }
 
+int orc_qp_solve_init(int n, int m, int p, const double *Pd, const double *c, const double *A, const double *b,
+                      const double *G, const double *h, int maxit, double tol, int qp_init, double *x_out, double *q_out,
+                      int *iters_out)
+{
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, qp_init);
+}
+
 int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
                  const double *A, const double *b, const double *G, const double *h,
                  int maxit, double tol, double *x_out, double *q_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, 0);
 }
 
 /* iSWIFT with the sigma <= sigma_d branch (Prime.c:193-196) disabled.  The step-length rule keeps
@@ -255,7 +274,7 @@ int orc_qp_solve_nt(int n, int m, int p, const double *Pd, const double *c,
                     const double *A, const double *b, const double *G, const double *h,
                     int maxit, double tol, double *x_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 1, NULL);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 1, NULL, 0);
 }
 
 /* iSWIFT semantics, reporting whether the sigma <= sigma_d branch was taken */
@@ -264,7 +283,7 @@ int orc_qp_solve_trap(int n, int m, int p, const double *Pd, const double *c,
                       int maxit, double tol, double *x_out, int *iters_out, int *trapped)
 {
     *trapped = 0;
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, trapped);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, trapped, 0);
 }
 
 /* general (full, symmetric) P -- used for iSWIFT's own test QP (Matrices_small.h) */
@@ -272,5 +291,5 @@ int orc_qp_solve_full(int n, int m, int p, const double *P, const double *c,
                       const double *A, const double *b, const double *G, const double *h,
                       int maxit, double tol, double *x_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, NULL);
+    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, NULL, 0);
 }

@@ -19,13 +19,20 @@
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
-        const double *alpha_buf, double *alpha_out, const int *sel_g);
+        const double *alpha_buf, double *alpha_out, const int *sel_g, float *zpol_g, int zstride);            \
+    extern "C" __global__ void srb_polish_kernel_##NZL##_##TS##_##NW(                                         \
+        SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
+        const double *obstacles, const double *nbr_state, double *x_out, double *obj_out, int *status_out,     \
+        const double *alpha_buf, double *alpha_out, const int *sel_g, const float *zpol_g, int zstride);
 SRB_KERNEL_INSTANCES(DECL_NMPC)
 #undef DECL_NMPC
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
-                              double *, const int *);
+                              double *, const int *, float *, int);
+typedef void (*srb_polish_fn)(SrbKParams, int, const double *, const double *, const double *, const double *,
+                              const double *, double *, double *, int *, const double *, double *, const int *,
+                              const float *, int);
 struct SrbGrid;
 extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const double *obstacles, int n_obs,
                                           const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
@@ -35,8 +42,8 @@ extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const
 extern "C" __global__ void srb_grid_build_kernel(const double *tab0, int stride0, int n0, SrbGrid *g0, int *off0,
                                                  double2 *spos0, int *sidx0, const double *tab1, int stride1, int n1,
                                                  SrbGrid *g1, int *off1, double2 *spos1, int *sidx1);
-struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; };
-#define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW},
+struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; srb_polish_fn polish; };
+#define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW, srb_polish_kernel_##NZL##_##TS##_##NW},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 #undef ENTRY_NMPC
 
@@ -106,6 +113,10 @@ struct srb_ctx {
     bool timed;
     int last_nw;
     int nw;                        // waves per agent forced by srb_ctx_set_waves (0: automatic)
+    int qp_init;                   // QP starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT
+    float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
+    int zstride;
+    float polish_ms;
     // selection grids (table 0: static obstacles, 1: neighbour snapshot), rebuilt per launch
     struct grid_buf { void *g; int *off; double2 *spos; int *sidx; size_t cap; } grid[2];
     const double *grid_src;        // obstacle table, row count and version the obstacle grid was built from
@@ -280,6 +291,8 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     for (auto &g : c->grid) g = srb_ctx::grid_buf{nullptr, nullptr, nullptr, nullptr, 0};
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
+    c->qp_init = 1; c->polish_ms = 0.0f;
+    c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
     HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
@@ -296,6 +309,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
     HIPCHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
     HIPCHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
+    HIPCHK(hipMalloc(&c->zpol, A * (size_t)c->zstride * sizeof(float)));
     *out = c;
     return SRB_OK;
 }
@@ -307,7 +321,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     (void)hipStreamSynchronize(c->stream);
     if (c->any) (void)hipEventSynchronize(c->done);     // the last launch may be on another stream
     void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr,
-                    c->abuf, c->alpha, c->sel};
+                    c->abuf, c->alpha, c->sel, c->zpol};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
     for (auto &g : c->grid)
@@ -335,6 +349,9 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (use_nlp && p->K_nbr > 0 && d->nbr_state && (d->agent_offset < 0 || d->agent_offset + n_agents > d->n_all))
         return fail(SRB_ERR_ARG, "agent_offset out of range of the neighbour table");
     SrbKParams k = make_kparams(p, use_nlp);
+    k.qp_init = c->qp_init;
+    static const double rho_env = [] { const char *e = std::getenv("SRB_POLISH_RHO"); return e ? std::atof(e) : 0.0; }();
+    k.polish_rho = rho_env > 0.0 ? rho_env : SRB_POLISH_RHO;
     // "up to K nearest": clamp to what exists (batch-uniform), so no row is ever a dummy
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
@@ -379,10 +396,21 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
+    // the solve kernel, then (NLP stage) the active-set polish of its result (srb_polish_kernel,
+    // same instance geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
+    const bool polish = use_nlp && SRB_POLISH_ON;
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
-                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel);
+                       d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
+                       polish ? c->zpol : nullptr, c->zstride);
     HIPCHK(hipGetLastError());
+    HIPCHK(hipEventRecord(c->ev[3], s));
+    if (polish) {
+        hipLaunchKernelGGL(in->polish, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+                           d->obstacles, d->nbr_state, d->x, d->obj, d->status, d->alpha ? d->alpha_buf : nullptr,
+                           d->alpha_buf ? d->alpha : nullptr, (const int *)sel, (const float *)c->zpol, c->zstride);
+        HIPCHK(hipGetLastError());
+    }
     HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
 }
@@ -396,6 +424,14 @@ extern "C" int srb_ctx_set_waves(srb_ctx *c, int nw)
 }
 
 extern "C" int srb_ctx_waves(srb_ctx *c) { return c ? c->last_nw : 0; }
+
+extern "C" int srb_ctx_set_qp_init(srb_ctx *c, int mode)
+{
+    if (!c) return fail(SRB_ERR_ARG, "null ctx");
+    if (mode != 0 && mode != 1) return fail(SRB_ERR_ARG, "QP start: 1 (scaled, default) or 0 (iSWIFT kkt_initialize)");
+    c->qp_init = mode;
+    return SRB_OK;
+}
 
 extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch *dev_io, void *stream)
 {
@@ -527,9 +563,19 @@ extern "C" int srb_last_kernel_ms(srb_ctx *c, float *knn_ms, float *solve_ms)
     HIPCHK(hipEventSynchronize(c->ev[1]));
     float a = 0, b = 0;
     HIPCHK(hipEventElapsedTime(&a, c->ev[0], c->ev[2]));
-    HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[1]));
+    HIPCHK(hipEventElapsedTime(&b, c->ev[2], c->ev[3]));
     if (knn_ms) *knn_ms = a;            // srb_knn_kernel (0 when there is nothing to select)
     if (solve_ms) *solve_ms = b;        // srb_nmpc_kernel_*
+    return SRB_OK;
+}
+
+extern "C" int srb_last_polish_ms(srb_ctx *c, float *polish_ms)
+{
+    if (!c || !c->timed) return fail(SRB_ERR_ARG, "no timed launch");
+    HIPCHK(hipEventSynchronize(c->ev[1]));
+    float t = 0;
+    HIPCHK(hipEventElapsedTime(&t, c->ev[3], c->ev[1]));
+    if (polish_ms) *polish_ms = t;      // srb_polish_kernel_* (0 without the NLP stage)
     return SRB_OK;
 }
 

@@ -27,11 +27,32 @@
 // near-optimal iterates without meeting both, the solve is at its round-off floor: ACCEPTABLE
 #define SRB_NLP_DXTOL 3e-5
 #define SRB_NLP_NEARWAIT 4
+// NLP stage: active-set polish of the final iterate (oracle/nlp_ipm.c `polish`, the same rules):
+// rows with s * KAPPA < z are taken as active and the equality-constrained problem is solved by at
+// most IT Newton steps (fewer once a correction is <= DXTOL) on its KKT system regularised by
+// 1/RHO; at most PASSES active sets (the most negative multiplier leaves, violated rows join).
+// Accepted (-> OPTIMAL) only if every row is within PTOL of its bound, the active rows hold to PTOL,
+// z_A >= -1e-9 max|z_A| and the last Newton correction is <= DXTOL.
+#ifndef SRB_POLISH_ON
+#define SRB_POLISH_ON 1
+#endif
+#define SRB_POLISH_RHO 1e8
+#define SRB_POLISH_KAPPA 1e4
+#define SRB_POLISH_IT 3
+#ifndef SRB_POLISH_PASSES
+#define SRB_POLISH_PASSES 2
+#endif
+#define SRB_POLISH_PTOL 1e-9
+#define SRB_POLISH_DXTOL 1e-7
+// cross-wave reduction scratch: sites of up to 8 doubles per wave (srb_kernels.hip)
+#define SRB_RED_SITES 10
 
 struct SrbKParams {
     int N, C, K_obs, K_nbr;
     int n, nz, mq, use_nlp;
     int qp_maxit, nlp_maxit;
+    int qp_init;                           // QP starting point: 1 scaled (s = max(h - Gx, 0.1), z = 1/s), 0 iSWIFT's kkt_initialize
+    double polish_rho;                     // SRB_POLISH_RHO (SRB_POLISH_RHO env override: tuning runs only)
     double Ad[16], Bd[8];                  // LIP discretisation (MPC_dist.cpp:126-127)
     double Qw, Pw, Rw, Sw, box, fr;        // gains (:172-175), box (:317), mu*h/sqrt(2) (:315)
     double eps_obs, eps_nbr, vsat, tol, Ts;
@@ -66,11 +87,12 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZM + 1;
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
     const int q = 16 * NW;
-    const int TT = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + srb_r4(NK) + q - 1) / q * q;
-    const int red = (NW > 1) ? 8 * 8 * NW : 0;
+    const int rO = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + q - 1) / q * q;   // stored term rows
+    const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
+    const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return TT * LDR + 2 * (TT + 1) + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) + (K + 1) +
-           srb_r4(NK) + (K + 1) + red + part
+    return rO * LDR + 2 * (TT + 1) + 2 * NKP + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
+           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64
 #endif

@@ -76,8 +76,12 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 __device__ double srb_nlp_dbg[8 * 64];
 __device__ int srb_nlp_dbg_agent = -1;
 #define NLPDBG(it, k, v) do { if (nl && agent == srb_nlp_dbg_agent && tid == 0 && (it) < 64) srb_nlp_dbg[8 * (it) + (k)] = (v); } while (0)
+// polish kernel: pass p of the traced agent into row 56 + p: primal, |c_A|, -min z_A, max |z_A|,
+// max inactive violation, last |dx|, accepted, Newton steps
+#define POLDBG(p, k, v) do { if (agent == srb_nlp_dbg_agent && tid == 0 && (p) < 8) srb_nlp_dbg[8 * (56 + (p)) + (k)] = (v); } while (0)
 #else
 #define NLPDBG(it, k, v) do {} while (0)
+#define POLDBG(p, k, v) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- term rows
@@ -89,28 +93,42 @@ struct TermLayout {
     __device__ __forceinline__ int zr(int v) const { return v < 4 * N ? v : v + E4; }
 };
 
-// GRAM: H = sum_t W_t r_t r_t' over the term rows [0, cnt): v_mfma_f64_16x16x4f64 with
-//   A[a][k] = r_{t0+k}[a], B[k][b] = W_{t0+k} r_{t0+k}[b]; lane l supplies term t0 + (l >> 4),
-//   column l & 15; D layout row (l >> 4) + 4 q, column l & 15; NZM = 32: tiles (0,0), (0,1),
-//   (1,1).  The next group's operands are loaded before the current MFMA issues, so the LDS
-//   latency hides under the 64-cycle f64 MFMA.
-// RHS: g[a] = sum_t CF_t r_t[a]: the very element lane l loads for the MFMA is the one its
-//   (column, term) pair needs, so the right-hand side costs one FMA per load; the four term
+// GRAM: H = sum_t W_t r_t r_t' over the stored term rows [0, cnt) and the generated obstacle
+//   term rows [rO, rO + nko): v_mfma_f64_16x16x4f64 with A[a][k] = r_{t0+k}[a],
+//   B[k][b] = W_{t0+k} r_{t0+k}[b]; lane l supplies term t0 + (l >> 4), column l & 15; D layout
+//   row (l >> 4) + 4 q, column l & 15; NZM = 32: tiles (0,0), (0,1), (1,1).  Four term groups per
+//   batch: every operand load of the batch issues before the first MFMA waits on one.
+// Obstacle rows are not stored: M_o = J_o Z = jx Z_x + jy Z_y - e_s (Z_x, Z_y: the stored Z rows of
+//   the grid's CoM position; OJ[2 o] = jx, OJ[2 o + 1] = jy; grid k = o / K), built in
+//   registers from two row loads -- the re-linearisation each iteration is two numbers per row
+//   instead of a stored row, and at N = 20 the rows no longer fill the LDS (2 agents per CU).
+// RHS: g[a] = sum_t CF_t r_t[a]: the very element lane l forms for the MFMA is the one its
+//   (column, term) pair needs, so the right-hand side costs one FMA per element; the four term
 //   chunks combine by permlane swaps.
-// cnt is a multiple of 16; rows / W / CF are zero beyond every real row.
-// NW > 1: wave w takes the term rows [w cnt/NW, (w+1) cnt/NW) and the per-wave partial
-// tiles / right-hand sides are summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
-// SRB_GRAM_CHAINS = 2 (NZM = 16): alternate term groups accumulate into two MFMA chains,
-// summed at the end (a different summation order; half the dependent-MFMA chain)
-#ifndef SRB_GRAM_CHAINS
-#define SRB_GRAM_CHAINS 1
-#endif
-template <int NZL, bool RHS, int NW>
-__device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt,
-                                         double *H, double *g, int nz, int tid, double *part)
+// cnt and nko are multiples of 16 NW; W / CF / OJ are zero beyond every real row.
+// NW > 1: wave w takes the w-th NW-th of both ranges; the per-wave partial tiles / right-hand
+// sides are summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
+// (obstacle term o belongs to grid k = o / K, whose CoM-position Z rows are 4k and 4k + 2: the row
+// index is formed in registers -- from a loaded index the row loads would wait on that load)
+template <int NZL>
+__device__ __forceinline__ double term_elem(const double *R, const double *OJ, int r, int rO, int col, int nz, bool gen,
+                                            float invK)
 {
+    constexpr int LDR = NZL + 1;
+    if (!gen) return (col < NZL) ? R[r * LDR + col] : 0.0;
+    const int o = r - rO;
+    const double jx = OJ[2 * o], jy = OJ[2 * o + 1];
+    const int xr = min(4 * (int)(((float)o + 0.5f) * invK), rO - 4);   // padding terms (jx = jy = 0) stay in R
+    return (col < NZL) ? fma(jx, R[xr * LDR + col], fma(jy, R[(xr + 2) * LDR + col], (col == nz - 1) ? -1.0 : 0.0)) : 0.0;
+}
+
+template <int NZL, bool RHS, int NW>
+__device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt, const double *OJ,
+                                         int rO, int nko, int K, double *H, double *g, int nz, int tid, double *part)
+{
+    const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
-    constexpr int LDR = NZL + 1, LDH = NZM + 1;
+    constexpr int LDH = NZM + 1;
     constexpr int NT = (NZM == 16) ? 1 : 3, NTC = NZM / 16;
     const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
@@ -118,19 +136,15 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     double ps[NTC];
 #pragma unroll
     for (int t = 0; t < NT; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
-    d4 acc2 = d4{0.0, 0.0, 0.0, 0.0};       // second accumulator chain (SRB_GRAM_CHAINS == 2)
 #pragma unroll
     for (int t = 0; t < NTC; t++) ps[t] = 0.0;
-    const int chunk = cnt / NW, tb = wv * chunk;
-    // four term groups per batch: every operand load of the batch issues before the first
-    // MFMA waits on one, and the next batch's loads issue while the MFMAs drain
-    for (int t0 = tb; t0 < tb + chunk; t0 += 16) {
+    auto batch = [&](int t0, bool gen) {
         double a[4][NTC], w[4], c[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int r = t0 + 4 * u + kq;
 #pragma unroll
-            for (int tc = 0; tc < NTC; tc++) a[u][tc] = (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0;
+            for (int tc = 0; tc < NTC; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
             w[u] = W[r];
             c[u] = RHS ? CF[r] : 0.0;
         }
@@ -141,18 +155,20 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 #pragma unroll
                 for (int tc = 0; tc < NTC; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
             if constexpr (NZM == 16) {
-                if (SRB_GRAM_CHAINS == 2 && (u & 1))
-                    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc2, 0, 0, 0);
-                else
-                    acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
             } else {
                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
                 acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][NTC - 1], acc[1], 0, 0, 0);
                 acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][NTC - 1], w[u] * a[u][NTC - 1], acc[2], 0, 0, 0);
             }
         }
+    };
+    {
+        const int chunk = cnt / NW, tb = wv * chunk;
+        for (int t0 = tb; t0 < tb + chunk; t0 += 16) batch(t0, false);
+        const int och = nko / NW, ob = rO + wv * och;
+        for (int t0 = ob; t0 < ob + och; t0 += 16) batch(t0, true);
     }
-    if constexpr (NZM == 16 && SRB_GRAM_CHAINS == 2) acc[0] += acc2;
     double gs[NTC];
     if (RHS)
 #pragma unroll
@@ -202,41 +218,49 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     }
 }
 
-// g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping as gram_rhs, eight term
-// groups per batch so that 16 LDS loads are in flight before the FMAs need them.
+// g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping and term ranges as gram_rhs,
+// eight term groups per batch so that 16 loads are in flight before the FMAs need them.
 template <int NZL, int NW>
-__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, double *g, int nz, int tid,
-                                         double *part)
+__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, const double *OJ, int rO, int nko,
+                                         int K, double *g, int nz, int tid, double *part)
 {
+    const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
-    constexpr int LDR = NZL + 1, NTC = NZM / 16;
+    constexpr int NTC = NZM / 16;
     const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
     double ps[2][NTC];
 #pragma unroll
     for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
-    const int chunk = cnt / NW, tb = wv * chunk, te = tb + chunk;
-    int t0 = tb;
-    for (; t0 + 32 <= te; t0 += 32) {
-        double a[8][NTC], c[8];
+    auto range = [&](int tb, int te, bool gen) {
+        int t0 = tb;
+        for (; t0 + 32 <= te; t0 += 32) {
+            double a[8][NTC], c[8];
 #pragma unroll
-        for (int u = 0; u < 8; u++) {
-            const int r = t0 + 4 * u + kq;
-            c[u] = CF[r];
+            for (int u = 0; u < 8; u++) {
+                const int r = t0 + 4 * u + kq;
+                c[u] = CF[r];
 #pragma unroll
-            for (int tc = 0; tc < NTC; tc++) a[u][tc] = (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0;
+                for (int tc = 0; tc < NTC; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
+            }
+            __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+            for (int u = 0; u < 8; u++)
+#pragma unroll
+                for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
         }
-        __builtin_amdgcn_sched_barrier(0);
+        for (; t0 < te; t0 += 4) {
+            const int r = t0 + kq;
+            const double cc = CF[r];
 #pragma unroll
-        for (int u = 0; u < 8; u++)
-#pragma unroll
-            for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
-    }
-    for (; t0 < te; t0 += 4) {
-        const int r = t0 + kq;
-        const double cc = CF[r];
-#pragma unroll
-        for (int tc = 0; tc < NTC; tc++) ps[0][tc] = fma(cc, (16 * tc + li < NZL) ? R[r * LDR + 16 * tc + li] : 0.0, ps[0][tc]);
+            for (int tc = 0; tc < NTC; tc++) ps[0][tc] = fma(cc, term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK), ps[0][tc]);
+        }
+    };
+    {
+        const int chunk = cnt / NW, tb = wv * chunk;
+        range(tb, tb + chunk, false);
+        const int och = nko / NW, ob = rO + wv * och;
+        range(ob, ob + och, true);
     }
 #pragma unroll
     for (int tc = 0; tc < NTC; tc++) {
@@ -459,6 +483,217 @@ __device__ __forceinline__ double zo_sum(const double *zo, int k, int K)
     return s;
 }
 
+// Slot sl's constants (kind, function indices, term row, bounds, cost terms); see Slot.
+__device__ __forceinline__ void slot_init(Slot &q, int sl, const SrbKParams &prm, const TermLayout &TL, const double *ref,
+                                          int sE, int sV, int sO, int S, int rC, int rO, int K, int TT)
+{
+    const int N = prm.N, n = prm.n;
+    q.kind = K_NONE; q.i0 = q.i1 = 0; q.r = 0; q.h[0] = q.h[1] = 0.0; q.a0 = q.a1 = 0.0; q.rx = 0.0; q.jd = 0.0;
+    q.m[0] = q.m[1] = 0.0; q.wr = TT;
+    if (sl < sE) {                                   // VAR
+        const int v = sl;
+        const bool isX = v < 4 * N, isU = !isX && v < 6 * N, isL = !isX && !isU && v < n - 1;
+        q.kind = K_VAR; q.i0 = q.i1 = v; q.r = TL.zr(v);
+        q.a0 = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : isL ? 0.0 : prm.Sw;
+        q.a1 = isX ? -q.a0 * ref[v] : 0.0;
+        q.h[0] = isL ? 1.0 : prm.box; q.h[1] = isL ? 0.0 : prm.box;
+    } else if (sl < sV) {                            // COP
+        const int e = sl - sE, i = e >> 1, d = e & 1;
+        q.kind = K_COP; q.i0 = 4 * i + 2 * d; q.i1 = 4 * N + 2 * (i + 1) + d; q.r = rC + e;
+        q.h[0] = q.h[1] = prm.fr;
+    } else if (sl < sO) {                            // VEL
+        const int tt = sl - sV, comp = (tt < N) ? 1 : 3, k = tt % N;
+        q.kind = K_VEL; q.i0 = q.i1 = 4 * k + comp; q.r = 4 * k + comp;
+        q.h[0] = q.h[1] = prm.vsat;
+    } else if (sl < S) {                             // OBS (positions filled at the NLP stage)
+        const int o = sl - sO, k = o / K;
+        q.kind = K_OBS; q.i0 = 4 * k; q.i1 = 4 * k + 2; q.r = rO + o;
+    }
+#pragma unroll
+    for (int r = 0; r < 2; r++) { q.s[r] = q.z[r] = 1.0; q.iz[r] = q.is[r] = 1.0; q.dz[r] = q.ds[r] = q.dsT[r] = q.r3[r] = 0.0; }
+}
+
+// the rows of slot q active in the stage (QP: linear rows; NLP: all), and the weight / rhs entry
+// it stores to (VEL adds into its variable's term row instead: the scratch entry TT)
+__device__ __forceinline__ void slot_stage(Slot &q, int n, bool nl, int TT)
+{
+    const bool lin = (q.kind == K_VAR && q.i0 < n - 1) || q.kind == K_COP;
+    q.m[0] = (lin || (nl && (q.kind == K_VEL || q.kind == K_OBS))) ? 1.0 : 0.0;
+    q.m[1] = (lin || (nl && q.kind == K_VEL)) ? 1.0 : 0.0;
+    q.wr = (q.kind == K_VAR || q.kind == K_COP || q.kind == K_OBS) ? q.r : TT;
+}
+
+// cost weight of variable v (Q_qp diagonal, MPC_dist.cpp:168-178)
+__device__ __forceinline__ double var_weight(const SrbKParams &prm, int v)
+{
+    const int N = prm.N;
+    return v < 4 * N ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : v < 6 * N ? prm.Rw : v < prm.n - 1 ? 0.0 : prm.Sw;
+}
+
+// Polish helper: every slot's row function g(x) into q.jd, each obstacle slot's term row M_o
+// re-linearised at x (entry by entry: the polish runs a few times per solve, so the register
+// staging of the interior-point loop is not worth its pressure here) and its multiplier into zo.
+template <int NZL, int TS, int NW>
+__device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double *xs, double *OJ, double *zo, int n,
+                                            int rO)
+{
+    const double s_var = xs[n - 1];
+#pragma unroll
+    for (int t = 0; t < TS; t++)
+        if (t < nts) {
+            Slot &q = Q[t];
+            q.jd = slot_f(q, xs, s_var);
+            if (kind_of(q) == K_OBS) {
+                const int o = q.r - rO;
+                OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
+                zo[o] = q.ds[0] * q.dz[0];
+            }
+        }
+}
+
+// --------------------------------------------------------------------------- shared agent code
+// The solve kernel and the polish kernel run on the same per-agent LDS layout and rebuild the
+// same null-space basis, so the code they share is written once, as statement macros expanded in
+// both template bodies (they bind the locals of the expanding function):
+//   SRB_AGENT_LAYOUT     sizes, term-row layout, slot ranges, the LDS carve (srb_lds_doubles)
+//   SRB_AGENT_SETUP      inputs (a1/a2/a3: x0, reference window, footholds), Z, xbar, CoM-CoP rows
+//   SRB_AGENT_OBSTACLES  the K selected rows per grid (srb_knn_kernel's sel; MPC_dist.cpp:371-396
+//                        generalised, neighbours predicted at constant velocity o_k = p + v Ts (k+1))
+//   SRB_AGENT_OUTPUTS    x, objective, alpha_COM
+#define SRB_AGENT_LAYOUT \
+    constexpr int NZM = ((NZL + 15) / 16) * 16; \
+    constexpr int LDR = NZL + 1, LDH = NZM + 1; \
+    constexpr int NTH = 64 * NW; \
+    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6; \
+    const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz; \
+    const int NK = N * K, NE = 2 * (N - 1); \
+    const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N); \
+    /* stored term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | zero rows up to rO, a */ \
+    /* multiple of 16 NW; then the NKP (NK padded likewise) generated obstacle terms: TT terms */ \
+    const int rC = 4 * N, rU = rC + E4, rO = (rU + UL4 + 16 * NW - 1) / (16 * NW) * (16 * NW); \
+    const int NKP = (NK + 16 * NW - 1) / (16 * NW) * (16 * NW), TT = rO + NKP; \
+    const TermLayout TL{N, C, n, nz, E4}; \
+    const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK; \
+    const double tol = prm.tol, th = tol / sqrt(3.0); \
+    STAMP_DECL; \
+    /* LDS carve (must match srb_lds_doubles) */ \
+    double *p = lds; \
+    double *R = p; p += rO * LDR;                 /* stored term rows (Z rows first) */ \
+    double *W = p; p += TT + 1;                   /* gram weights (+ one scratch entry) */ \
+    double *CF = p; p += TT + 1;                  /* rhs coefficients (+ one scratch entry) */ \
+    double *OJ = p; p += 2 * NKP;                 /* obstacle terms: jx, jy (gram_rhs) */ \
+    double *H0 = p; p += NZM * LDH;               /* assembled Z'HZ (delta = 0) */ \
+    double *HS = p; p += NZM * LDH;               /* Z'HZ + delta Z'Z (when delta != 0) */ \
+    double *ZZ = p; p += NZM * LDH;               /* Z'Z (NLP) */ \
+    double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM; \
+    double *xs = p; p += n4; \
+    double *xb = p; p += n4; \
+    double *xsv = p; p += n4;                     /* NLP: saved iterate (round-off floor / polish) */ \
+    double *ref = p; p += 4 * N; \
+    double *foot = p; p += 2 * C * N; \
+    double *obs = p; p += 2 * NK + 2; \
+    double *eps = p; p += K + 1; \
+    double *zo = p; p += NK4;                     /* obstacle duals (per-grid sums) */ \
+    double *dpos = p; p += 2 * N + 1;             /* Z_x dxi, Z_y dxi per grid, dxi_s (obstacle J dx) */ \
+    int *sel = (int *)p; p += (K + 1); \
+    double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
+    double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs */ \
+    do {} while (0)
+
+#define SRB_AGENT_SETUP \
+    const double *x0 = x0g + 4 * (size_t)agent; \
+    for (int i = tid; i < 4 * N; i += NTH) ref[i] = refg[(size_t)agent * 4 * N + i]; \
+    for (int i = tid; i < 2 * C * N; i += NTH) foot[i] = footg[(size_t)agent * 2 * C * N + i]; \
+    for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0; \
+    for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0; \
+    SYNC(); \
+    /* null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261) */ \
+    if (tid == 0) { \
+        double X[4] = {x0[0], x0[1], x0[2], x0[3]}; \
+        for (int k = 0; k < N; k++) { \
+            const double u0 = foot[(k * 2 + 0) * C + C - 1], u1 = foot[(k * 2 + 1) * C + C - 1]; \
+            double Xn[4]; \
+            for (int d = 0; d < 4; d++) \
+                Xn[d] = prm.Ad[d * 4] * X[0] + prm.Ad[d * 4 + 1] * X[1] + prm.Ad[d * 4 + 2] * X[2] + prm.Ad[d * 4 + 3] * X[3] + \
+                        prm.Bd[d * 2] * u0 + prm.Bd[d * 2 + 1] * u1; \
+            for (int d = 0; d < 4; d++) { X[d] = Xn[d]; xb[4 * k + d] = Xn[d]; } \
+            xb[4 * N + 2 * k] = u0; xb[4 * N + 2 * k + 1] = u1; \
+            for (int j = 0; j < C; j++) xb[6 * N + C * k + j] = (j == C - 1) ? 1.0 : 0.0; \
+        } \
+        xb[n - 1] = 0.0; \
+    } \
+    for (int col = tid; col < nz - 1; col += NTH) { \
+        const int j = col / (C - 1), t = col % (C - 1); \
+        double lam[4]; \
+        const int is_null = lambda_basis(foot + j * 2 * C, C, t, lam); \
+        double g0 = 0.0, g1 = 0.0; \
+        if (!is_null) \
+            for (int i = 0; i < C; i++) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; } \
+        for (int i = 0; i < C; i++) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i]; \
+        R[TL.zr(4 * N + 2 * j) * LDR + col] = g0; \
+        R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = g1; \
+        double v[4]; \
+        for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1; \
+        for (int k = j; k < N; k++) { \
+            for (int d = 0; d < 4; d++) R[(4 * k + d) * LDR + col] = v[d]; \
+            double tt[4]; \
+            for (int d = 0; d < 4; d++) tt[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3]; \
+            for (int d = 0; d < 4; d++) v[d] = tt[d]; \
+        } \
+    } \
+    if (tid == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0; \
+    SYNC(); \
+    /* CoM-CoP term rows M_e = Z_p - Z_u (p: CoM of grid i, u: CoP of grid i+1); xs = xbar */ \
+    if (tid < NE) { \
+        const int i = tid >> 1, d = tid & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d; \
+        for (int a = 0; a < NZL; a++) Rt[tid * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a]; \
+    } \
+    for (int v = tid; v < n; v += NTH) xs[v] = xb[v]; \
+    do {} while (0)
+
+#define SRB_AGENT_OBSTACLES \
+            if (tid < K) sel[tid] = sel_g[(size_t)agent * K + tid]; \
+            SYNC(); \
+            for (int j = 0; j < K; j++) { \
+                const bool st = j < prm.K_obs; \
+                const int bi = sel[j]; \
+                if (tid < N) {         /* no selection (-1): a row 1000 m along +x, as the oracle */ \
+                    const int k = tid; \
+                    const double tt = st ? 0.0 : prm.Ts * (k + 1); \
+                    const size_t bj = (bi >= 0) ? bi : 0; \
+                    const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj; \
+                    obs[2 * (k * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0; \
+                    obs[2 * (k * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2]; \
+                } \
+                if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr; \
+            } \
+    do {} while (0)
+
+#define SRB_AGENT_OUTPUTS \
+    /* x and the objective 0.5 x'Q_qp x + f'x (ExCost::GetCost, dec_vars_constr_cost.h:423-438) */ \
+    double f = 0.0; \
+    for (int v = tid; v < n; v += NTH) { \
+        const double xv = xs[v]; \
+        x_out[(size_t)agent * n + v] = xv; \
+        const double a0 = var_weight(prm, v), a1 = (v < 4 * N) ? -a0 * ref[v] : 0.0; \
+        f += fma(0.5 * a0 * xv, xv, a1 * xv); \
+    } \
+    { \
+        double rv[1] = {f}; \
+        wred_x<1, 0u, NW>(rv, red + 6 * 8 * NW, tid); \
+        f = rv[0]; \
+    } \
+    /* fitComTrajectory_eventbase (MPC_dist.cpp:784-855) as an epilogue: alpha_COM (4 x 5) interpolates */ \
+    /* [buffer, X_0..X_3] at s = 0, 1/4, .., 1 (the reference's 24 x 24 KKT keeps only the s = 0 end */ \
+    /* point row, so its solution is this interpolation): alpha[d][j] = sum_i Binv[j][i] p_i[d] */ \
+    if (alpha_out && tid < 20) { \
+        const int d = tid / 5, j = tid - 5 * (tid / 5); \
+        double acc = prm.Binv[5 * j] * alpha_buf[(size_t)agent * 4 + d]; \
+        for (int i = 1; i < 5; i++) acc = fma(prm.Binv[5 * j + i], xs[4 * (i - 1) + d], acc); \
+        alpha_out[(size_t)agent * 20 + 5 * d + j] = acc; \
+    } \
+    do {} while (0)
+
 // --------------------------------------------------------------------------- main kernel
 // NZL: register bound on nz (one reduced-matrix row per lane); TS: slot trips per thread;
 // NW: wavefronts per agent (1, or 4 = one per SIMD of a CU for small batches).  With NW > 1
@@ -473,42 +708,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
                 const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
-                const int *__restrict__ sel_g, double *lds)
+                const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride, double *lds)
 {
-    constexpr int NZM = ((NZL + 15) / 16) * 16;
-    constexpr int LDR = NZL + 1, LDH = NZM + 1;
-    constexpr int NTH = 64 * NW;                        // threads per agent
-    const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6;
-    const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz;
-    const int NK = N * K, NE = 2 * (N - 1);
-    const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N);
-    // term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | obstacles (NK4) | 4 zero rows
-    const int rC = 4 * N, rU = rC + E4, rO = rU + UL4, TT = (rO + NK4 + 16 * NW - 1) / (16 * NW) * (16 * NW);
-    const TermLayout TL{N, C, n, nz, E4};
-    const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK;
-    const double tol = prm.tol, th = tol / sqrt(3.0);
-    STAMP_DECL;
-
-    // ---- LDS carve (must match srb_lds_doubles)
-    double *p = lds;
-    double *R = p; p += TT * LDR;                       // term rows (Z rows first)
-    double *W = p; p += TT + 1;                         // gram weights (+ one scratch entry)
-    double *CF = p; p += TT + 1;                        // rhs coefficients (+ one scratch entry)
-    double *H0 = p; p += NZM * LDH;                     // assembled Z'HZ (delta = 0)
-    double *HS = p; p += NZM * LDH;                     // Z'HZ + delta Z'Z (when delta != 0)
-    double *ZZ = p; p += NZM * LDH;                     // Z'Z (NLP)
-    double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM;
-    double *xs = p; p += n4;                            // current x
-    double *xb = p; p += n4;                            // xbar
-    double *xsv = p; p += n4;                           // NLP: last near-optimal iterate (restored at the round-off floor)
-    double *ref = p; p += 4 * N;
-    double *foot = p; p += 2 * C * N;
-    double *obs = p; p += 2 * NK + 2;
-    double *eps = p; p += K + 1;
-    double *zo = p; p += NK4;                           // obstacle duals (per-grid sums)
-    int *sel = (int *)p; p += (K + 1);
-    double *red = p; p += (NW > 1) ? 8 * 8 * NW : 0;      // cross-wave reduction scratch, 8 sites of <= 8 values
-    double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   // partial Gram / rhs
+    SRB_AGENT_LAYOUT;
 #ifdef SRB_STAMPS
     unsigned long long *stamp_lds = (unsigned long long *)p; p += SRB_NSTAMP;
     if (tid < 64) stamp_lds[tid] = 0;
@@ -516,87 +718,13 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double *Rt = R + rC * LDR;                          // CoM-CoP rows
 
     STAMP_BEGIN();
-    // ---- load inputs (a1/a2/a3: x0, reference window, footholds); zero the padded tables
-    const double *x0 = x0g + 4 * (size_t)agent;
-    for (int i = tid; i < 4 * N; i += NTH) ref[i] = refg[(size_t)agent * 4 * N + i];
-    for (int i = tid; i < 2 * C * N; i += NTH) foot[i] = footg[(size_t)agent * 2 * C * N + i];
-    for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0;     // tables, matrices, vectors, xs, xb
-    for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0;
-    SYNC();
-
-    // ---- null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261)
-    if (tid == 0) {
-        double X[4] = {x0[0], x0[1], x0[2], x0[3]};
-        for (int k = 0; k < N; k++) {
-            const double u0 = foot[(k * 2 + 0) * C + C - 1], u1 = foot[(k * 2 + 1) * C + C - 1];
-            double Xn[4];
-            for (int d = 0; d < 4; d++)
-                Xn[d] = prm.Ad[d * 4] * X[0] + prm.Ad[d * 4 + 1] * X[1] + prm.Ad[d * 4 + 2] * X[2] + prm.Ad[d * 4 + 3] * X[3] +
-                        prm.Bd[d * 2] * u0 + prm.Bd[d * 2 + 1] * u1;
-            for (int d = 0; d < 4; d++) { X[d] = Xn[d]; xb[4 * k + d] = Xn[d]; }
-            xb[4 * N + 2 * k] = u0; xb[4 * N + 2 * k + 1] = u1;
-            for (int j = 0; j < C; j++) xb[6 * N + C * k + j] = (j == C - 1) ? 1.0 : 0.0;
-        }
-        xb[n - 1] = 0.0;
-    }
-    for (int col = tid; col < nz - 1; col += NTH) {
-        const int j = col / (C - 1), t = col % (C - 1);
-        double lam[4];
-        const int is_null = lambda_basis(foot + j * 2 * C, C, t, lam);
-        double g0 = 0.0, g1 = 0.0;
-        if (!is_null)
-            for (int i = 0; i < C; i++) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; }
-        for (int i = 0; i < C; i++) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i];
-        R[TL.zr(4 * N + 2 * j) * LDR + col] = g0;
-        R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = g1;
-        double v[4];
-        for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1;
-        for (int k = j; k < N; k++) {
-            for (int d = 0; d < 4; d++) R[(4 * k + d) * LDR + col] = v[d];
-            double tt[4];
-            for (int d = 0; d < 4; d++) tt[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3];
-            for (int d = 0; d < 4; d++) v[d] = tt[d];
-        }
-    }
-    if (tid == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0;
-    SYNC();
-    // CoM-CoP term rows M_e = Z_p - Z_u (p = CoM position of grid i, u = CoP of grid i+1); xs = xbar
-    if (tid < NE) {
-        const int i = tid >> 1, d = tid & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d;
-        for (int a = 0; a < NZL; a++) Rt[tid * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a];
-    }
-    for (int v = tid; v < n; v += NTH) xs[v] = xb[v];
+    // ---- inputs (a1/a2/a3: x0, reference window, footholds), null-space basis Z, xbar, term rows
+    SRB_AGENT_SETUP;
 
     // ---- slot constants
     Slot Q[TS];
 #pragma unroll
-    for (int t = 0; t < TS; t++) {
-        Slot &q = Q[t];
-        const int sl = tid + NTH * t;
-        q.kind = K_NONE; q.i0 = q.i1 = 0; q.r = 0; q.h[0] = q.h[1] = 0.0; q.a0 = q.a1 = 0.0; q.rx = 0.0; q.jd = 0.0;
-        q.m[0] = q.m[1] = 0.0; q.wr = TT;
-        if (sl < sE) {                                   // VAR
-            const int v = sl;
-            const bool isX = v < 4 * N, isU = !isX && v < 6 * N, isL = !isX && !isU && v < n - 1;
-            q.kind = K_VAR; q.i0 = q.i1 = v; q.r = TL.zr(v);
-            q.a0 = isX ? ((v >= 4 * (N - 1)) ? prm.Pw : prm.Qw) : isU ? prm.Rw : isL ? 0.0 : prm.Sw;
-            q.a1 = isX ? -q.a0 * ref[v] : 0.0;
-            q.h[0] = isL ? 1.0 : prm.box; q.h[1] = isL ? 0.0 : prm.box;
-        } else if (sl < sV) {                            // COP
-            const int e = sl - sE, i = e >> 1, d = e & 1;
-            q.kind = K_COP; q.i0 = 4 * i + 2 * d; q.i1 = 4 * N + 2 * (i + 1) + d; q.r = rC + e;
-            q.h[0] = q.h[1] = prm.fr;
-        } else if (sl < sO) {                            // VEL
-            const int tt = sl - sV, comp = (tt < N) ? 1 : 3, k = tt % N;
-            q.kind = K_VEL; q.i0 = q.i1 = 4 * k + comp; q.r = 4 * k + comp;
-            q.h[0] = q.h[1] = prm.vsat;
-        } else if (sl < S) {                             // OBS (positions filled at the NLP stage)
-            const int o = sl - sO, k = o / K;
-            q.kind = K_OBS; q.i0 = 4 * k; q.i1 = 4 * k + 2; q.r = rO + o;
-        }
-#pragma unroll
-        for (int r = 0; r < 2; r++) { q.s[r] = q.z[r] = 1.0; q.iz[r] = q.is[r] = 1.0; q.dz[r] = q.ds[r] = q.dsT[r] = q.r3[r] = 0.0; }
-    }
+    for (int t = 0; t < TS; t++) slot_init(Q[t], tid + NTH * t, prm, TL, ref, sE, sV, sO, S, rC, rO, K, TT);
     double Mi[NZL];                                          // inverse of the reduced Newton matrix (row = lane)
     double dxi[NZL];                                         // Newton direction in xi (uniform)
 #pragma unroll
@@ -614,9 +742,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         STAMP_STAGE(stage);
         const int nts = ((nl ? S : sV) + NTH - 1) / NTH;      // active slot trips
         const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
-        const int cnt = ((nl ? rO + NK4 : rO) + 16 * NW - 1) / (16 * NW) * (16 * NW);   // term rows (zero-padded)
+        const int cnt = rO, nko = nl ? NKP : 0;            // stored term rows, generated obstacle terms
         STAMP_BEGIN();
         // stage activity of each row
+        // (written out here rather than through slot_stage: the call form measurably changes the
+        // register allocation of the whole loop, 8 -> 72 VGPR spills for 12_4_1)
 #pragma unroll
         for (int t = 0; t < TS; t++) {
             Slot &q = Q[t];
@@ -640,7 +770,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
             if (gj_reduced<NZL>(Mi, nz, lane, 1) != 0) {
@@ -665,16 +795,47 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             mn = -rv[0]; mx = rv[1];
             const double ssh = (-mn < 0) ? 0.0 : 1.0 - mn, zsh = (mx < 0) ? 0.0 : 1.0 + mx;
             SYNC();                                           // every lane has read xs = xbar
+            // qp_init 1 (default): the scaled start of oracle/qp_ipm.c, s = max(h - Gx, 0.1), z = 1/s
+            // (iSWIFT's z shift by 1 + max(h - Gx) is ~1e3 with the +-1e3 boxes: blocked dual steps,
+            // up to 19 iterations on the bench batch against 9); qp_init 0: iSWIFT's start
+            const bool scaled = prm.qp_init == 1;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
                     const double f = q.jd, z0 = q.h[0] - f, z1 = q.h[1] + f;
-                    q.s[0] = (q.m[0] != 0.0) ? z0 + ssh : 1.0; q.z[0] = (q.m[0] != 0.0) ? -z0 + zsh : 1.0;
-                    q.s[1] = (q.m[1] != 0.0) ? z1 + ssh : 1.0; q.z[1] = (q.m[1] != 0.0) ? -z1 + zsh : 1.0;
+                    q.s[0] = (q.m[0] != 0.0) ? (scaled ? fmax(z0, 0.1) : z0 + ssh) : 1.0;
+                    q.s[1] = (q.m[1] != 0.0) ? (scaled ? fmax(z1, 0.1) : z1 + ssh) : 1.0;
+                    q.z[0] = (q.m[0] != 0.0) ? (scaled ? rcp_d(q.s[0]) : -z0 + zsh) : 1.0;
+                    q.z[1] = (q.m[1] != 0.0) ? (scaled ? rcp_d(q.s[1]) : -z1 + zsh) : 1.0;
                     if (q.kind == K_VAR) xs[q.i0] = f;
-                    q.rx = 0.0;      // = G'(dz_init - z) = -(1+za) G'1 = 0: every G row comes in a +- pair
+                    // rx = -(P x + c + A'y + G'z) = -G'(z - (G x - h)) at the least-squares start: 0 for
+                    // iSWIFT's z (the shift is the same on the two rows of every +- pair), below for the
+                    // scaled one (each row's z + (h - Gx) scattered onto its variables)
+                    q.rx = 0.0;
                 }
+            if (scaled) {
+                SYNC();
+#pragma unroll
+                for (int t = 0; t < TS; t++)              // the VAR rows' own bounds first (plain stores)
+                    if (t < nts && Q[t].kind == K_VAR) {
+                        const Slot &q = Q[t];
+                        CF[q.r] = q.m[0] * (q.z[0] + q.h[0] - q.jd) - q.m[1] * (q.z[1] + q.h[1] + q.jd);
+                    }
+                SYNC();
+#pragma unroll
+                for (int t = 0; t < TS; t++)              // CoM-CoP rows +-(p_i - u_i+1): onto p_i and u_i+1
+                    if (t < nts && Q[t].kind == K_COP) {
+                        const Slot &q = Q[t];
+                        const double g = q.m[0] * (q.z[0] + q.h[0] - q.jd) - q.m[1] * (q.z[1] + q.h[1] + q.jd);
+                        __hip_atomic_fetch_add(&CF[TL.zr(q.i0)], g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&CF[TL.zr(q.i1)], -g, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                SYNC();
+#pragma unroll
+                for (int t = 0; t < TS; t++)
+                    if (t < nts && Q[t].kind == K_VAR) Q[t].rx = -CF[Q[t].r];
+            }
             SYNC();
             STAMP_END(1);
         } else {
@@ -685,22 +846,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
             // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
             // (selected by srb_knn_kernel, launched just before this kernel on the same stream)
-            if (tid < K) sel[tid] = sel_g[(size_t)agent * K + tid];
-            SYNC();
-            STAMP_END(6);                                     // NLP slot 6: neighbour selection
-            for (int j = 0; j < K; j++) {
-                const bool st = j < prm.K_obs;
-                const int bi = sel[j];
-                if (tid < N) {                                // no selection (-1): a row 1000 m along +x, as the oracle
-                    const int k = tid;
-                    const double tt = st ? 0.0 : prm.Ts * (k + 1);
-                    const size_t bj = (bi >= 0) ? bi : 0;     // row 0 exists whenever K_obs / K_nbr > 0
-                    const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj;
-                    obs[2 * (k * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0;
-                    obs[2 * (k * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2];
-                }
-                if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr;
-            }
+            SRB_AGENT_OBSTACLES;
+            STAMP_END(6);                                     // NLP slot 6: neighbour selection (+ positions)
             SYNC();
             // slacks: shifted h - g(x) over every NLP row; duals 1
             const double s_var = xs[n - 1];
@@ -731,27 +878,28 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     const double f = q.jd;
                     q.s[0] = (q.m[0] != 0.0) ? q.h[0] - f + ssh : 1.0;
                     q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
-                    q.z[0] = q.z[1] = SRB_NLP_Z0;
-                    if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x
-                        // both Z rows are read before the first store: the store could alias
-                        // them as far as the compiler knows, and would otherwise put one LDS
-                        // round trip per entry on the path
-                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
-                        double z0[NZL], z1[NZL];
-#pragma unroll
-                        for (int a = 0; a < NZL; a++) { z0[a] = R[q.i0 * LDR + a]; z1[a] = R[q.i1 * LDR + a]; }
-#pragma unroll
-                        for (int a = 0; a < NZL; a++)
-                            R[q.r * LDR + a] = fma(jx, z0[a], jy * z1[a]) - (a == nz - 1 ? 1.0 : 0.0);
+                    // z = Z0 / s: every row starts at complementarity Z0 (oracle/nlp_ipm.c, same rule)
+                    q.z[0] = SRB_NLP_Z0 * rcp_d(q.s[0]);
+                    q.z[1] = SRB_NLP_Z0 * rcp_d(q.s[1]);
+                    if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x (gram_rhs)
+                        const int o = q.r - rO;
+                        OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
                     }
-                    // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z), z = z0: J'1 vanishes on every
-                    // +- pair, leaving the obstacle rows
-                    if (q.kind == K_VAR) { W[q.r] = 1.0; CF[q.r] = fma(q.a0, f, q.a1); }
-                    else if (q.kind == K_COP) { W[q.r] = 0.0; CF[q.r] = 0.0; }
-                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = SRB_NLP_Z0; }
+                    // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z): each row's J'z on its
+                    // term row (the velocity rows' below, onto their variables' rows)
+                    const double jz = q.m[0] * q.z[0] - q.m[1] * q.z[1];
+                    if (q.kind == K_VAR) { W[q.r] = 1.0; CF[q.r] = fma(q.a0, f, q.a1) + jz; }
+                    else if (q.kind == K_COP) { W[q.r] = 0.0; CF[q.r] = jz; }
+                    else if (q.kind == K_OBS) { W[q.r] = 0.0; CF[q.r] = q.z[0]; }
                 }
+            if (NW > 1) SYNC();                               // the VAR rows' plain stores land before the VEL adds
+#pragma unroll
+            for (int t = 0; t < TS; t++)
+                if (t < nts && Q[t].kind == K_VEL)
+                    __hip_atomic_fetch_add(&CF[Q[t].r], Q[t].m[0] * Q[t].z[0] - Q[t].m[1] * Q[t].z[1], __ATOMIC_RELAXED,
+                                           __HIP_MEMORY_SCOPE_WORKGROUP);
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, ZZ, vg, nz, tid, part);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, ZZ, vg, nz, tid, part);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_reduced<NZL>(Mi, nz, lane, 0);
@@ -797,18 +945,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     sz = fma(q.m[0] * q.s[0], q.z[0], fma(q.m[1] * q.s[1], q.z[1], sz));
 #pragma unroll
                     for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
-                    if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z
-                        // both Z rows are read before the first store: the store could alias
-                        // them as far as the compiler knows, and would otherwise put one LDS
-                        // round trip per entry on the path
-                        const double jx = -2.0 * (xs[q.i0] - q.a0), jy = -2.0 * (xs[q.i1] - q.a1);
-                        double z0[NZL], z1[NZL];
-#pragma unroll
-                        for (int a = 0; a < NZL; a++) { z0[a] = R[q.i0 * LDR + a]; z1[a] = R[q.i1 * LDR + a]; }
-#pragma unroll
-                        for (int a = 0; a < NZL; a++)
-                            R[q.r * LDR + a] = fma(jx, z0[a], jy * z1[a]) - (a == nz - 1 ? 1.0 : 0.0);
-                        zo[q.r - rO] = q.z[0];
+                    if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z (gram_rhs)
+                        const int o = q.r - rO;
+                        OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
+                        zo[o] = q.z[0];
                     }
                 }
             }
@@ -906,7 +1046,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 set_rhs(0);
                 SYNC();
                 STAMP_END(17);
-                gram_rhs<NZL, true, NW>(R, W, CF, cnt, H0, vg, nz, tid, part);
+                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
                 SYNC();
                 STAMP_END(4);
                 double dstart = 0.0;
@@ -941,7 +1081,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     set_rhs(pass);
                     SYNC();
                     STAMP_END(6 + 4 * pass);
-                    rhs_only<NZL, NW>(R, CF, cnt, vg, nz, tid, part);
+                    rhs_only<NZL, NW>(R, CF, cnt, OJ, rO, nko, K, vg, nz, tid, part);
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
@@ -949,11 +1089,23 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
+                // obstacle rows: J_o Z dxi = jx (Z_x dxi) + jy (Z_y dxi) - dxi_s, the CoM-position steps
+                // of every grid formed once (dpos) instead of one generated row per obstacle
+                if (nl) {
+                    if (tid <= 2 * N)
+                        dpos[tid] = row_dot<NZL>(R + (tid < 2 * N ? 4 * (tid >> 1) + 2 * (tid & 1) : TL.zr(n - 1)) * LDR, dxi);
+                    SYNC();
+                }
 #pragma unroll
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
+                        if (nl && kind_of(q) == K_OBS) {
+                            const int o = q.r - rO;
+                            q.jd = fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N]));
+                        } else {
+                            q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
+                        }
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
                             q.dz[r] = q.m[r] * q.z[r] * q.is[r] * fma(r ? -1.0 : 1.0, q.jd, -q.r3[r]);
@@ -1049,38 +1201,27 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];     // owner threads, as saved
             flag = 4;
         }
+
+        // the polish kernel (srb_polish_kernel, launched next) starts from this result: its active
+        // set and multipliers -- rows with s * KAPPA < z keep z (as float: only the Newton
+        // iteration's starting guess), the others 0 -- go to HBM, zpol_g[agent][2 slot + row]
+        if (zpol_g && nl) {
+            float *zp = zpol_g + (size_t)agent * zstride;
+#pragma unroll
+            for (int t = 0; t < TS; t++)
+                if (t < nts && tid + NTH * t < S)
+#pragma unroll
+                    for (int r = 0; r < 2; r++)
+                        zp[2 * (tid + NTH * t) + r] = (Q[t].m[r] != 0.0 && Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r]) ? (float)Q[t].z[r] : 0.0f;
+        }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
     }
     SYNC();
     if (x_qp_out && nstage == 1)
         for (int v = tid; v < n; v += NTH) x_qp_out[(size_t)agent * n + v] = xs[v];
 
-    // ---- outputs
-    double f = 0.0;
-#pragma unroll
-    for (int t = 0; t < TS; t++) {
-        const Slot &q = Q[t];
-        if (q.kind == K_VAR) {
-            const double xv = xs[q.i0];
-            x_out[(size_t)agent * n + q.i0] = xv;
-            f += fma(0.5 * q.a0 * xv, xv, q.a1 * xv);
-        }
-    }
-    {
-        double rv[1] = {f};
-        wred_x<1, 0u, NW>(rv, red + 6 * 8 * NW, tid);
-        f = rv[0];
-    }
-    // ---- fitComTrajectory_eventbase (MPC_dist.cpp:784-855) as an epilogue: alpha_COM (4 x 5)
-    // interpolates [buffer, X_0..X_3] at s = 0, 1/4, 1/2, 3/4, 1 (the reference's 24 x 24 KKT
-    // keeps only the s = 0 end-point row, so its solution is this interpolation), i.e.
-    // alpha[d][j] = sum_i Binv[j][i] p_i[d] with the host-inverted 5 x 5 Bernstein matrix.
-    if (alpha_out && tid < 20) {
-        const int d = tid / 5, j = tid - 5 * (tid / 5);
-        double acc = prm.Binv[5 * j] * alpha_buf[(size_t)agent * 4 + d];
-        for (int i = 1; i < 5; i++) acc = fma(prm.Binv[5 * j + i], xs[4 * (i - 1) + d], acc);
-        alpha_out[(size_t)agent * 20 + 5 * d + j] = acc;
-    }
+    // ---- outputs: x, objective (ExCost::GetCost, dec_vars_constr_cost.h:423-438), alpha_COM
+    SRB_AGENT_OUTPUTS;
     STAMP_END(15);
     STAMP_FLUSH(agent);
     if (tid == 0) {
@@ -1090,6 +1231,194 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     }
 }
 
+// --------------------------------------------------------------------------- polish kernel
+// Launched right after the solve kernel on the same stream, same instance geometry.  It rebuilds
+// the agent's basis and term rows (SRB_AGENT_SETUP), takes the NLP result from x_out and the
+// interior-point active set / multipliers from zpol_g, and replaces x, obj, alpha and the NLP
+// status (-> OPTIMAL) only when the polish is accepted.  A kernel of its own: inside the solve
+// kernel the polish's registers competed with the interior-point loop's and pushed its spills
+// from 8 to 100-200 (configs[2] 0.40 -> 0.47-0.66 ms); here the loop is untouched.
+template <int NZL, int TS, int NW>
+__device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
+                const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
+                const double *__restrict__ obstacles, const double *__restrict__ nbr_state,
+                double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,
+                const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
+                const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride, double *lds)
+{
+    SRB_AGENT_LAYOUT;
+    double *Rt = R + rC * LDR;
+    (void)HS; (void)xb; (void)th; (void)tol; (void)wv;
+    const int st1 = status_out[2 * agent + 1];
+    if (!prm.use_nlp || st1 == 1 || st1 == 3) return;          // the whole workgroup: no usable iterate to polish
+    SRB_AGENT_SETUP;
+    SYNC();
+    for (int v = tid; v < n; v += NTH) { const double xv = x_out[(size_t)agent * n + v]; xs[v] = xv; xsv[v] = xv; }
+    SRB_AGENT_OBSTACLES;
+    SYNC();
+    const float *zp = zpol_g + (size_t)agent * zstride;
+    double Mi[NZL], dxi[NZL];
+    // ---------------- active-set polish of the NLP result (oracle/nlp_ipm.c `polish`, the same rules) ----------------
+    // Near its round-off floor the barrier system's active rows carry z/s ~ 1e14, so the
+    // interior-point iterate stops up to ~1e-4 from the optimum along soft directions.  Rows
+    // with s * KAPPA < z are taken as the active set A and min f s.t. Aeq x = beq, g_A(x) = h_A
+    // is solved by Newton steps on its KKT system regularised by 1 / RHO:
+    //   Z'(H_L + RHO J_A'J_A)Z dxi = -Z'(grad f + J_A'(z_A + RHO c_A)),  z_A += RHO (c_A + J_A Z dxi)
+    // -- the interior-point machinery with weight RHO on the active rows, 0 on the others --
+    // whose fixed point is the exact KKT point of that active set; at most SRB_POLISH_IT steps,
+    // fewer once a correction is below SRB_POLISH_DXTOL.  Accepted (OPTIMAL) only when primal
+    // feasible, dual feasible and converged; otherwise the most negative multiplier leaves A,
+    // violated rows join, and the next pass starts again from the interior-point result (at
+    // most SRB_POLISH_PASSES); a rejected polish leaves that result.  The slots are rebuilt
+    // here (the interior-point slot state is dead); their fields ds = active mask, dz = z_A,
+    // r3 = row value g - h, jd = g(x).
+    {
+        const int nts = (S + NTH - 1) / NTH;
+        const int cnt = rO, nko = NKP;
+        Slot P[TS];
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            Slot &q = P[t];
+            const int sl = tid + NTH * t;
+            slot_init(q, sl, prm, TL, ref, sE, sV, sO, S, rC, rO, K, TT);
+            slot_stage(q, n, true, TT);
+            if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                q.dz[r] = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
+                q.ds[r] = (q.dz[r] > 0.0) ? 1.0 : 0.0;
+            }
+        }
+        bool accepted = false;
+#pragma clang loop unroll(disable)
+        for (int pass = 0; pass < SRB_POLISH_PASSES; pass++) {
+            bool bad = false;
+            double lastdx = 1e300;
+#pragma clang loop unroll(disable)
+            for (int pit = 0; pit < SRB_POLISH_IT; pit++) {
+                SYNC();                                      // xs of the previous step / pass
+                polish_rows<NZL, TS, NW>(P, nts, xs, OJ, zo, n, rO);      // q.jd = g(x), M_o (OJ), zo = z_A
+                SYNC();                                      // R rows, zo
+#pragma unroll
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = P[t];
+                        q.r3[0] = q.jd - q.h[0]; q.r3[1] = -q.jd - q.h[1];
+                        const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
+                        const double wa = prm.polish_rho * (q.ds[0] + q.ds[1]);
+                        if (kind_of(q) == K_VAR) {
+                            double hs = 0.0;
+                            if (q.i0 < 4 * N && !(q.i0 & 1)) hs = -2.0 * zo_sum(zo, q.i0 >> 2, K);
+                            W[q.wr] = q.a0 + hs + wa;
+                            CF[q.wr] = -(fma(q.a0, q.jd, q.a1) + cfa);
+                        } else {
+                            W[q.wr] = wa;                    // COP / OBS rows (VEL: the scratch entry)
+                            CF[q.wr] = -cfa;
+                        }
+                    }
+                if (NW > 1) SYNC();                          // the VAR rows' plain stores land before the VEL adds
+#pragma unroll
+                for (int t = 0; t < TS; t++)
+                    if (t < nts && kind_of(P[t]) == K_VEL) {
+                        const Slot &q = P[t];
+                        const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
+                        __hip_atomic_fetch_add(&W[q.r], prm.polish_rho * (q.ds[0] + q.ds[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                SYNC();
+                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
+                SYNC();
+                gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
+                if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; }      // not PD: reject
+                la_solve<NZL>(Mi, H0, vg, vy, vr, vd, dxi, nz, lane);
+                double mdx = 0.0;
+#pragma unroll
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = P[t];
+                        const double jd = (kind_of(q) == K_OBS)      // J_o Z dxi, M_o generated (gram_rhs)
+                            ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),
+                                  fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))
+                            : row_dot<NZL>(R + q.r * LDR, dxi);
+                        q.dz[0] = fma(q.ds[0] * prm.polish_rho, q.r3[0] + jd, q.dz[0]);
+                        q.dz[1] = fma(q.ds[1] * prm.polish_rho, q.r3[1] - jd, q.dz[1]);
+                        if (kind_of(q) == K_VAR) {
+                            xs[q.i0] = q.jd + jd;            // every read of xs this step is behind a barrier
+                            mdx = fmax(mdx, fabs(jd));
+                        }
+                    }
+                {
+                    double rv[1] = {mdx};
+                    wred_x<1, 1u, NW>(rv, red + 8 * 8 * NW, tid);
+                    lastdx = rv[0];
+                }
+                if (lastdx <= SRB_POLISH_DXTOL) break;       // converged: no further step
+            }
+            if (bad) break;
+            SYNC();
+            // ---- acceptance at the polished point
+            double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0, vi = -1e300;
+            {
+                const double s_var = xs[n - 1];
+#pragma unroll
+                for (int t = 0; t < TS; t++)
+                    if (t < nts) {
+                        Slot &q = P[t];
+                        const double fq = slot_f(q, xs, s_var);
+#pragma unroll
+                        for (int r = 0; r < 2; r++) {
+                            const double v = r ? -fq - q.h[1] : fq - q.h[0];
+                            q.r3[r] = v;
+                            if (q.m[r] != 0.0) pv = fmax(pv, v);
+                            if (q.ds[r] != 0.0) { cv = fmax(cv, fabs(v)); nzmin = fmax(nzmin, -q.dz[r]); zm = fmax(zm, fabs(q.dz[r])); }
+                            else if (q.m[r] != 0.0) vi = fmax(vi, v);
+                        }
+                    }
+                double rv[5] = {pv, cv, nzmin, zm, vi};
+                wred_x<5, 0x1Fu, NW>(rv, red + 7 * 8 * NW, tid);
+                pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4];
+            }
+            POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);
+            POLDBG(pass, 5, lastdx);
+            if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL) {
+                POLDBG(pass, 6, 1.0);
+                accepted = true;
+                break;
+            }
+            // next pass: the most negative multiplier leaves A, violated rows join; the rows
+            // that stay keep their multipliers (>= 0), the new ones start at 0
+            double wd = 1e300;
+            int wk = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < TS; t++)
+                if (t < nts)
+#pragma unroll
+                    for (int r = 0; r < 2; r++)
+                        if (P[t].ds[r] != 0.0 && P[t].dz[r] < -1e-9 * zm) lexmin(wd, wk, P[t].dz[r], 2 * (tid + NTH * t) + r);
+            wargmin_x<NW>(wd, wk, red + 9 * 8 * NW, tid);
+            if (wk == 0x7fffffff && !(vi > SRB_POLISH_PTOL)) break;      // nothing to change: rejected
+#pragma unroll
+            for (int t = 0; t < TS; t++) {
+                Slot &q = P[t];
+#pragma unroll
+                for (int r = 0; r < 2; r++) {
+                    if (2 * (tid + NTH * t) + r == wk) q.ds[r] = 0.0;
+                    else if (t < nts && q.ds[r] == 0.0 && q.m[r] != 0.0 && q.r3[r] > SRB_POLISH_PTOL) q.ds[r] = 1.0;
+                    q.dz[r] = q.ds[r] * fmax(q.dz[r], 0.0);
+                }
+            }
+            SYNC();
+            for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];   // the next pass starts from the interior-point result
+        }
+        SYNC();
+        if (accepted) {
+            SRB_AGENT_OUTPUTS;
+            if (tid == 0) { obj_out[agent] = f; status_out[2 * agent + 1] = 0; }
+        }
+    }
+
+}
+
 #define SRB_NMPC_KERNEL(NZL, TS, NW)                                                                           \
     extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE srb_nmpc_kernel_##NZL##_##TS##_##NW(        \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
@@ -1097,14 +1426,27 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
         int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,       \
-        const int *__restrict__ sel_g)                                                                         \
+        const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride)                               \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
         nmpc_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
                                 x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, sel_g, \
-                                lds);                                                                          \
+                                zpol_g, zstride, lds);                                                         \
+    }                                                                                                          \
+    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE srb_polish_kernel_##NZL##_##TS##_##NW(      \
+        SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
+        const double *__restrict__ footg, const double *__restrict__ obstacles,                                 \
+        const double *__restrict__ nbr_state, double *__restrict__ x_out, double *__restrict__ obj_out,          \
+        int *__restrict__ status_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,     \
+        const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride)                         \
+    {                                                                                                          \
+        extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
+        const int agent = blockIdx.x;                                                                          \
+        if (agent >= n_agents) return;                                                                         \
+        polish_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, nbr_state, x_out, obj_out,          \
+                                  status_out, alpha_buf, alpha_out, sel_g, zpol_g, zstride, lds);             \
     }
 
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)

@@ -354,6 +354,21 @@ __device__ __forceinline__ void wargmin(double &d, int &idx)
     d = a; idx = (int)i32[0]; lexmin(d, idx, b, (int)i32[1]);
 }
 
+// wargmin over the NW waves of the workgroup: per-wave DPP argmin, lane 0 of every wave
+// publishes (d, idx) to scr[2 NW], every thread combines the partials in wave order
+template <int NW>
+__device__ __forceinline__ void wargmin_x(double &d, int &idx, double *scr, int tid)
+{
+    wargmin(d, idx);
+    if constexpr (NW > 1) {
+        if ((tid & 63) == 0) { scr[2 * (tid >> 6)] = d; scr[2 * (tid >> 6) + 1] = (double)idx; }
+        __syncthreads();
+        d = scr[0]; idx = (int)scr[1];
+#pragma unroll
+        for (int w = 1; w < NW; w++) lexmin(d, idx, scr[2 * w], (int)scr[2 * w + 1]);
+    }
+}
+
 // Uniform grid over the rows of a table (SURVEY 8(a) row a10 at swarm scale): built on the
 // device each launch by srb_grid_build_kernel for tables of SRB_GRID_MIN_ROWS rows or more.
 // Cells row-major (cy * nx + cx), rows of finite coordinates sorted by cell (the order inside

@@ -89,6 +89,8 @@ def lib():
         L.srb_sync.argtypes = [ctypes.c_void_p]
         L.srb_ctx_set_waves.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.srb_ctx_waves.argtypes = [ctypes.c_void_p]
+        L.srb_ctx_set_qp_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.srb_last_polish_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
         L.srb_hl_plan.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.srb_prepare_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Prep), ctypes.c_void_p]
         L.srb_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
@@ -257,6 +259,10 @@ class BatchSolver:
         """Waves per agent (0 automatic, 1, 2, 4; srb_ctx_set_waves)."""
         _check(lib().srb_ctx_set_waves(self._h, int(nw)))
 
+    def set_qp_init(self, mode: int = 1):
+        """QP-stage starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT's kkt_initialize."""
+        _check(lib().srb_ctx_set_qp_init(self._h, int(mode)))
+
     def waves(self) -> int:
         """Waves per agent of the last launch."""
         return lib().srb_ctx_waves(self._h)
@@ -265,6 +271,12 @@ class BatchSolver:
         a = ctypes.c_float(); b = ctypes.c_float()
         _check(lib().srb_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def last_polish_ms(self) -> float:
+        """HIP-event time of the last launch's polish kernel (srb_polish_kernel), ms."""
+        t = ctypes.c_float()
+        _check(lib().srb_last_polish_ms(self._h, ctypes.byref(t)))
+        return t.value
 
 
 def torch_int32():

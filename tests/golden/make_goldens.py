@@ -11,6 +11,10 @@ Fixtures written (data only -- inputs and expected outputs):
                       QP-stage output (SNOPT start point, print_file.out:30-54) and SNOPT's final
                       point, plus the genuine-iSWIFT QP solution and the KKT-certified NLP optimum
   qp_random.json      seeded instances (N, C in {4,10,20} x {2,4}) with genuine-iSWIFT solutions
+  qp_iswift_md.npz    64 instances per (N, C) in {(4,4),(4,2),(10,2),(10,4),(20,2)}: genuine iSWIFT
+                      under a minimum-degree ordering (the reference's AMD stand-in) and the
+                      quasi-definite one, the oracle's point, flags / iterations / KKT quality
+                      (python tests/golden/make_goldens.py qpmd)
   nlp_random.json     seeded N=10 trot instances, K_obs = 3: KKT-certified NLP optimum (oracle),
                       with SciPy SLSQP's objective from the same warm start for comparison
   ll_ctrl.npz         low-level CLF-QP (LowLevelCtrl::calcTorque) inputs for 8 agents with
@@ -159,6 +163,49 @@ def qp_random():
     dump("qp_random.json", dict(cases=cases))
 
 
+# ----------------------------------------------------------------------------- QP stage vs the reference's ordering
+QPMD_CASES = [(4, 4), (4, 2), (10, 2), (10, 4), (20, 2)]
+
+
+def qp_point_quality(Pd, c, A, b, G, h, x):
+    """KKT quality of a QP-stage point: objective, |Ax - b|_inf, max(Gx - h, 0), and the
+    relative stationarity of the best multipliers on its near-active rows (tests/kkt.certify)."""
+    cert = certify(Pd, c, A, b, lambda v: (G @ v, G), h, x)
+    return [0.5 * Pd @ (x * x) + c @ x, cert["eq"], cert["prim"], cert["stat_rel"]]
+
+
+def qp_md():
+    """qp_iswift_md.npz: 64 bench-distribution instances per (N, C) solved by the genuine iSWIFT
+    with a minimum-degree KKT ordering (the reference's iswift_qp.cpp:184-210 orders with Eigen's
+    AMD, which is absent: a plain minimum-degree order stands in, oracle/iswift_ref_driver.c) and
+    with the quasi-definite order the qp_random.json goldens use, next to the oracle's point (the
+    GPU's algorithm, oracle/qp_ipm.c); flags, iterations and a KKT quality row per point."""
+    out = {}
+    for N, C in QPMD_CASES:
+        b = workload.make_batch(64, N, C, seed=5000 + 10 * N + C)
+        p = oracle.params(N, C)
+        rec = {k: [] for k in ("x_md", "flag_md", "iters_md", "q_md", "x_qd", "flag_qd", "iters_qd", "q_qd",
+                               "x_orc", "flag_orc", "iters_orc", "q_orc")}
+        for a in range(64):
+            Pd, c, A, bb, G, h = oracle.build_qp(p, b["x0"][a], b["ref"][a], b["foot"][a])
+            for tag, (x, f, it) in (("md", oracle.iswift_ref(Pd, c, A, bb, G, h, "md")),
+                                    ("qd", oracle.iswift_ref(Pd, c, A, bb, G, h, "qd")),
+                                    ("orc", oracle.qp_solve(Pd, c, A, bb, G, h)[:3])):
+                rec["x_" + tag].append(x); rec["flag_" + tag].append(f); rec["iters_" + tag].append(it)
+                rec["q_" + tag].append(qp_point_quality(Pd, c, A, bb, G, h, x))
+        key = f"N{N}_C{C}_"
+        out[key + "x0"] = b["x0"]; out[key + "ref"] = b["ref"]; out[key + "foot"] = b["foot"]
+        for k, v in rec.items():
+            out[key + k] = np.asarray(v)
+        d = np.abs(np.asarray(rec["x_orc"]) - np.asarray(rec["x_md"]))
+        d = np.concatenate([d[:, :6 * N], d[:, -1:]], 1).max(1)
+        print(f"N={N} C={C}: iters md {np.mean(rec['iters_md']):.2f} qd {np.mean(rec['iters_qd']):.2f} "
+              f"oracle {np.mean(rec['iters_orc']):.2f}; |x_orc - x_md| (X,U,s) max {d.max():.2e}; "
+              f"flags md {np.bincount(rec['flag_md'])}")
+    np.savez_compressed(os.path.join(HERE, "qp_iswift_md.npz"), **out)
+    print("wrote qp_iswift_md.npz")
+
+
 # ----------------------------------------------------------------------------- random NLP
 def nlp_random():
     cases = []
@@ -205,6 +252,9 @@ if __name__ == "__main__":
     oracle.build()
     if sys.argv[1:] == ["ll"]:
         ll_ctrl()
+        sys.exit(0)
+    if sys.argv[1:] == ["qpmd"]:
+        qp_md()
         sys.exit(0)
     if sys.argv[1:] == ["nlp"]:               # the NLP fixtures only (oracle NLP changes)
         kat2()

@@ -66,3 +66,45 @@ def certify(Pd, c, A, b, g_and_J, hh, x, act_tol=1e-3, comp_tol=1e-3):
     comp = float((z * np.maximum(slack[act], 0)).max()) if act.size else 0.0
     return dict(stat=stat, stat_rel=stat / scale, comp=comp, prim=viol, eq=eq,
                 zmin=float(z.min()) if act.size else 0.0, nact=int(act.size))
+
+
+def qp_exact_optimum(Pd, c, A, b, G, h, x_start, act_tol=1e-5, max_changes=20):
+    """Exact optimum of the convex QP  min 0.5 x'diag(Pd)x + c'x  s.t. Ax = b, Gx <= h  by a
+    primal-dual active-set iteration started from the rows within act_tol of their bound at
+    x_start: the equality-constrained optimum of [A; G_act] on its null space (least squares
+    where lambda is not unique, C = 4), multipliers by bounded least squares (y free, z >= 0),
+    then drop / add rows until z >= 0 fits exactly and every row holds.  Returns (x*, y, z)."""
+    from scipy.optimize import lsq_linear
+    act = np.where(G @ x_start - h > -act_tol)[0]
+    P = np.diag(Pd)
+    for _ in range(max_changes):
+        M = np.vstack([A, G[act]])
+        r = np.r_[b, h[act]]
+        _, S, Vt = np.linalg.svd(M)
+        rank = int((S > 1e-10 * S[0]).sum())
+        Zn = Vt[rank:].T
+        xp = np.linalg.lstsq(M, r, rcond=None)[0]
+        xs = xp - Zn @ np.linalg.lstsq(Zn.T @ P @ Zn, Zn.T @ (P @ xp + c), rcond=1e-13)[0]
+        grad = P @ xs + c
+        lb = np.r_[-np.inf * np.ones(A.shape[0]), np.zeros(act.size)]
+        sol = lsq_linear(M.T, -grad, bounds=(lb, np.inf * np.ones(M.shape[0])), method="bvls", tol=1e-14)
+        res = np.abs(M.T @ sol.x + grad).max()
+        viol = G @ xs - h
+        if res > 1e-7 * max(1.0, np.abs(grad).max()):
+            m2 = np.linalg.lstsq(M.T, -grad, rcond=None)[0][A.shape[0]:]
+            act = np.delete(act, np.argmin(m2))
+            continue
+        if viol.max() > 1e-9:
+            act = np.union1d(act, np.where(viol > 1e-9)[0])
+            continue
+        z = np.zeros(G.shape[0])
+        z[act] = sol.x[A.shape[0]:]
+        return xs, sol.x[:A.shape[0]], z
+    raise RuntimeError("qp_exact_optimum: active set did not settle")
+
+
+def l1_merit(Pd, c, A, b, G, h, x, y, z):
+    """Exact l1-penalty merit with the optimal multipliers (|y|, z): minimised by the optimum
+    and >= f(x*) at every point, feasible or not -- a fair 'how optimal' measure for two
+    approximate solutions with different residuals."""
+    return 0.5 * Pd @ (x * x) + c @ x + np.abs(y) @ np.abs(A @ x - b) + z @ np.maximum(G @ x - h, 0)

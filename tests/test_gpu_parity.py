@@ -28,21 +28,20 @@ NLP_TOL = 1e-4
 
 
 def conv(st):
-    """Exit codes with the two converged NLP outcomes merged: OPTIMAL (0) and ACCEPTABLE (4, an
-    iterate at the condensed system's round-off floor after the residual tests passed, see
-    DESIGN.md 3) are the same answer to NLP_TOL; which of the two a solve reports near that
-    floor is decided by round-off (GPU vs oracle linear algebra)."""
-    st = np.array(st, copy=True)
-    st[..., 1][st[..., 1] == 4] = 0
-    return st
+    """Exit codes as compared between GPU and oracle: exactly (round 3: the active-set polish ends
+    both at the exact KKT point as OPTIMAL, so ACCEPTABLE is no longer merged into OPTIMAL)."""
+    return np.array(st, copy=True)
+
+
 _solvers = {}
 
 
-def solver(N, C, K_obs=1, K_nbr=0, use_nlp=1, max_agents=2048):
-    key = (N, C, K_obs, K_nbr, use_nlp, max_agents)
+def solver(N, C, K_obs=1, K_nbr=0, use_nlp=1, max_agents=2048, qp_init=1):
+    key = (N, C, K_obs, K_nbr, use_nlp, max_agents, qp_init)
     if key not in _solvers:
         p = srbnmpc.default_params(N, C, K_obs=K_obs, K_nbr=K_nbr, use_nlp=use_nlp)
         _solvers[key] = srbnmpc.BatchSolver(p, max_agents)
+        _solvers[key].set_qp_init(qp_init)
     return _solvers[key]
 
 
@@ -52,33 +51,50 @@ def xus(N, x):
 
 
 # ----------------------------------------------------------------------------- goldens
-def test_kat2_reference_instance(kat2):
+@pytest.mark.parametrize("qp_init", [0, 1])
+def test_kat2_reference_instance(kat2, qp_init):
     """The reference's logged instance: QP stage == the reference's own logged output and
-    genuine iSWIFT; NLP stage == KKT-certified optimum."""
-    s = solver(4, 4, K_obs=1)
+    genuine iSWIFT; NLP stage == KKT-certified optimum.  qp_init 0 (iSWIFT's start) follows the
+    genuine iSWIFT step for step (same iteration count); the default scaled start ends at the same
+    point to the log's precision in fewer iterations."""
+    s = solver(4, 4, K_obs=1, qp_init=qp_init)
     foot = np.repeat(kat2["F"][None], 4, 0)
     out = s.solve(kat2["x0"][None], kat2["ref"][None], foot[None], np.asarray(kat2["obstacle"])[None])
     assert out["status"][0].tolist() == [0, 0]
-    assert out["iters"][0, 0] == kat2["iters_qp_qd"]
+    if qp_init == 0:
+        assert out["iters"][0, 0] == kat2["iters_qp_qd"]
+    else:
+        assert out["iters"][0, 0] < kat2["iters_qp_qd"]
     xq = out["x_qp"][0]
     np.testing.assert_allclose(xq[:24], kat2["logged_qp_x"], atol=2e-9, rtol=0)
     np.testing.assert_allclose(xus(4, xq), xus(4, kat2["x_qp_iswift_qd"]), atol=1e-8, rtol=0)
-    np.testing.assert_allclose(xus(4, out["x"][0]), xus(4, kat2["x_nlp"]), atol=1e-6, rtol=0)
-    assert abs(out["obj"][0] - kat2["obj_nlp"]) < 1e-6
+    np.testing.assert_allclose(xus(4, out["x"][0]), xus(4, kat2["x_nlp"]), atol=1e-9, rtol=0)
+    assert abs(out["obj"][0] - kat2["obj_nlp"]) < 1e-8
 
 
-def test_qp_random_vs_genuine_iswift():
+@pytest.mark.parametrize("qp_init", [0, 1])
+def test_qp_random_vs_genuine_iswift(qp_init):
+    """QP stage (use_snopt == false) against the genuine iSWIFT.  qp_init 0: iSWIFT's own start,
+    step for step (iteration counts equal but for round-off at the exit threshold, x to 1e-8);
+    qp_init 1 (default): the scaled start, the same optimum to the QP tolerance in fewer or equal
+    iterations."""
     cases = load_golden("qp_random.json")["cases"]
     groups = {}
     for cs in cases:
         groups.setdefault((cs["N"], cs["C"]), []).append(cs)
     for (N, C), cl in groups.items():
-        s = solver(N, C, use_nlp=0)
+        s = solver(N, C, use_nlp=0, qp_init=qp_init)
         x0 = np.array([c["x0"] for c in cl]); ref = np.array([c["ref"] for c in cl]); foot = np.array([c["foot"] for c in cl])
         out = s.solve(x0, ref, foot, qp_only=True)
         xr = np.array([c["x"] for c in cl])
         assert (out["status"][:, 0] == 0).all()
         it_ref = np.array([c["iters"] for c in cl])
+        if qp_init == 1:
+            assert out["iters"][:, 0].mean() <= it_ref.mean()
+            np.testing.assert_allclose(xus(N, out["x"]), xus(N, xr), atol=1e-7, rtol=0)
+            if C == 2:
+                np.testing.assert_allclose(out["x"], xr, atol=QP_TOL, rtol=0)
+            continue
         same = out["iters"][:, 0] == it_ref
         # the exit test sits on iSWIFT's 1e-6 residual threshold: round-off may move one
         # instance across it by a single iteration (seen for 4 contacts, non-unique lambda)
@@ -159,7 +175,7 @@ def test_full_size_properties(A, Kn):
     s = solver(N, C, Ko, Kn)
     out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
     p = s.params
-    assert (out["status"] == 0).mean() >= 0.99
+    assert (out["status"] == 0).all(1).mean() >= 0.999          # OPTIMAL (polished) on both stages
     x = out["x"]
     assert _dynamics_residual(p, b["x0"], x) < 1e-9                          # Aeq x = beq (dynamics)
     Xs, U, L, sl = srbnmpc.split(p, x)
@@ -184,15 +200,15 @@ def test_full_size_properties(A, Kn):
 
 
 def test_config5_full_size_vs_oracle_and_acceptable_exit():
-    """bench config 5 (2048 agents, N = 20, 3 static + 8 neighbour rows) at full size, every
+    """bench config 5 (2048 agents, N = 20, 3 static + 8 neighbour rows) at full size, EVERY
     agent within NLP_TOL (1e-4) of the oracle in X, U, s.
 
-    The NLP exit needs the residual tests AND a last primal step max |ap dx| < 1e-5
-    (SRB_NLP_DXTOL; profiles/r02_nlp_exit.txt: the residual tests alone left 3.6 % of these
-    solves 1e-4..5e-4 from the optimum along flat directions).  Solves that reach the
-    round-off floor of the condensed system first end ACCEPTABLE (4) at a near-optimal
-    iterate; every ACCEPTABLE solution, plus a sample of the rest, must pass
-    the KKT certificate."""
+    The interior-point exit needs the residual tests AND a last primal step max |ap dx| < 3e-5
+    (SRB_NLP_DXTOL); its result is then polished to the exact KKT point of its active set
+    (srb_polish_kernel), which ends the solve OPTIMAL.  A polish that is not
+    accepted (measured: well under 1 % of these solves) leaves the interior-point result with
+    its status (ACCEPTABLE = 4 at the round-off floor); every such solution, plus a sample of the
+    rest, must pass the KKT certificate."""
     A, N, C, Ko, Kn = 2048, 20, 2, 3, 8
     b = workload.make_batch(A, N, C, seed=1234)
     s = solver(N, C, Ko, Kn)
@@ -200,17 +216,15 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
     st, it = out["status"], out["iters"]
     assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
     acc = np.where(st[:, 1] == srbnmpc.ACCEPTABLE)[0]
-    assert acc.size <= 0.1 * A
-    assert it[:, 1].max() <= 25                                    # no MAXIT tail
+    assert acc.size <= 0.005 * A, acc.size                         # polish accepted on >= 99.5 %
+    assert it[:, 1].max() <= 20                                    # no MAXIT tail (measured max 17)
     op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
     r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], nthreads=16)
     assert np.isin(r["status"][:, 1], [0, 4]).all() and (r["status"][:, 0] == 0).all()
     e = np.abs(xus(N, out["x"]) - xus(N, r["x"])).max(1)
-    # every OPTIMAL solve within NLP_TOL; an ACCEPTABLE one may stop one round-off-limited step
-    # earlier than the oracle's full-space LU (measured: 3 of 2048 at 1.2e-4)
-    opt = st[:, 1] == 0
-    assert e[opt].max() < NLP_TOL, (int(np.argmax(np.where(opt, e, 0))), float(e[opt].max()))
-    assert e.max() < 2 * NLP_TOL and np.mean(e < NLP_TOL) >= 0.998, (int(np.argmax(e)), float(e.max()))
+    assert e.max() < NLP_TOL, (int(np.argmax(e)), float(e.max()))
+    both = (st[:, 1] == 0) & (r["status"][:, 1] == 0)        # polished on both sides: the same KKT point
+    assert both.mean() >= 0.995 and e[both].max() < 1e-6, (both.mean(), float(e[both].max()))
     rng = np.random.default_rng(5)
     for a in np.r_[acc[:64], rng.choice(A, 16, replace=False)]:
         obs, eps = oracle.select_obstacles(op, b["x0"][a], b["obstacles"], b["nbr_state"], int(a))

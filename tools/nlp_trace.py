@@ -19,7 +19,7 @@ c = int(sys.argv[1])
 cfg = bench.CONFIGS[c]
 A, N, C = cfg["agents"], cfg["N"], cfg["C"]
 p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
-b = workload.make_batch(A, N, C, seed=1234)
+A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 s = srbnmpc.BatchSolver(p, A)
 L = srbnmpc.lib()
 L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
@@ -30,6 +30,11 @@ for ag in map(int, sys.argv[2:]):
     L.srb_debug_nlp_trace(-1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
     print(f"agent {ag}: status {out['status'][ag].tolist()} iters {out['iters'][ag].tolist()}")
     print("  it     |rx|        thx        |rz|       s'z/m      ap        ad        delta     sigma")
-    for i in range(int(out["iters"][ag, 1]) + 1):
+    for i in range(min(int(out["iters"][ag, 1]) + 1, 56)):
         r = buf[8 * i:8 * i + 8]
         print(f"  {i:2d} " + " ".join(f"{v:10.3e}" for v in r), flush=True)
+    print("  polish pass: primal     |c_A|     -min z_A   max|z_A|   inact.viol  last|dx|   accepted")
+    for p in range(8):
+        r = buf[8 * (56 + p):8 * (56 + p) + 8]
+        if r.any():
+            print(f"  {p:2d}          " + " ".join(f"{v:10.3e}" for v in r[:7]), flush=True)
