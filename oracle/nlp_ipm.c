@@ -151,6 +151,7 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #define ORC_POLISH_PASSES 2       /* active-set passes (the most negative z_A leaves, violated rows join) */
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
+#define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */
 
 static double g_polish_rho = ORC_POLISH_RHO;
 static double g_polish_kappa = 1e4;
@@ -158,12 +159,13 @@ static int g_polish_zinit = 1;    /* exploration: 1 = a later pass starts from t
 int orc_early_stats[2];
 int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */          /* exploration counters: early polish attempts failed / accepted */
 static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
+static double g_polish_omcap = ORC_POLISH_OMCAP;
 
 /* Newton steps of the regularised equality-constrained KKT for the active set `act`; returns 0
  * on success, -1 when the reduced matrix is not positive definite */
-static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int nz, const int *act, double *xt,
-                         double *za, double *g, double *Jv, int *Ji, double *Hl, double *K, double *rhs, double *cA,
-                         double *Hr, double *HZ, int *piv, double *lastdx, int trace)
+static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int nz, const int *act, const double *om,
+                         double *xt, double *za, double *g, double *Jv, int *Ji, double *Hl, double *K, double *rhs,
+                         double *cA, double *Hr, double *HZ, int *piv, double *lastdx, int trace)
 {
     const int n = P->n, p = P->p, m = P->m, dim = n + p;
     const double rho = g_polish_rho;
@@ -178,11 +180,15 @@ static int polish_newton(const nlp_t *P, const double *hh, const double *Z, int 
             Hl[(4 * k) * n + 4 * k] -= 2 * zs; Hl[(4 * k + 2) * n + 4 * k + 2] -= 2 * zs;
         }
         for (int r = 0; r < m; r++) {
-            if (!act[r]) continue;
+            /* active rows: rho; inactive ones keep their interior-point weight z/s, capped at
+             * OMCAP (om), in the Hessian only -- a proximal term that leaves the fixed point alone
+             * and keeps the reduced matrix definite along directions no active row pins (lambda
+             * with 4 contacts); the cap keeps it from slowing the Newton steps elsewhere */
+            const double wr = act[r] ? rho : om[r];
             for (int a = 0; a < 4; a++) {
                 const int ia = Ji[4 * r + a]; if (ia < 0) continue;
-                rhs[ia] -= Jv[4 * r + a] * (za[r] + rho * cA[r]);
-                for (int bb = 0; bb < 4; bb++) { const int ib = Ji[4 * r + bb]; if (ib >= 0) Hl[ia * n + ib] += rho * Jv[4 * r + a] * Jv[4 * r + bb]; }
+                if (act[r]) rhs[ia] -= Jv[4 * r + a] * (za[r] + rho * cA[r]);
+                for (int bb = 0; bb < 4; bb++) { const int ib = Ji[4 * r + bb]; if (ib >= 0) Hl[ia * n + ib] += wr * Jv[4 * r + a] * Jv[4 * r + bb]; }
             }
         }
         /* the reduced matrix Z'(H_L + rho J_A'J_A)Z must be positive definite */
@@ -233,13 +239,17 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
     double *rhs = malloc(sizeof(double) * dim), *cA = malloc(sizeof(double) * m), *v = malloc(sizeof(double) * n);
     double *Hr = malloc(sizeof(double) * nz * nz), *HZ = malloc(sizeof(double) * (size_t)n * nz), *gr = malloc(sizeof(double) * nz);
     int *Ji = malloc(sizeof(int) * 4 * m), *piv = malloc(sizeof(int) * dim), *act = malloc(sizeof(int) * m);
+    double *om = malloc(sizeof(double) * m);
     int ok = 0;
-    for (int r = 0; r < m; r++) { act[r] = s[r] * g_polish_kappa < z[r]; za[r] = act[r] ? z[r] : 0.0; }
+    for (int r = 0; r < m; r++) { act[r] = s[r] * g_polish_kappa < z[r]; za[r] = act[r] ? z[r] : 0.0; om[r] = act[r] ? 0.0 : fmin(z[r] / s[r], g_polish_omcap); }
     int npass = 0;
     for (int pass = 0; pass < g_polish_passes && !ok; pass++, npass++) {
         memcpy(xt, x, sizeof(double) * n);
         double lastdx = 1e300;
-        if (polish_newton(P, hh, Z, nz, act, xt, za, g, Jv, Ji, Hl, K, rhs, cA, Hr, HZ, piv, &lastdx, trace)) break;
+        if (polish_newton(P, hh, Z, nz, act, om, xt, za, g, Jv, Ji, Hl, K, rhs, cA, Hr, HZ, piv, &lastdx, trace)) {
+            if (trace) fprintf(stderr, "  polish pass %d: reduced matrix not positive definite -> rejected\n", pass);
+            break;
+        }
         rows_eval(P, xt, g, Jv, Ji);
         double zm = 1.0, pv = -1e300, cv = 0.0, zmin = 1e300;
         int nact = 0, changed = 0;
@@ -290,7 +300,7 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
     }
     __atomic_add_fetch(&orc_polish_stats[ok ? 1 + npass : 0], 1, __ATOMIC_RELAXED);
     free(xt); free(za); free(g); free(Jv); free(Hl); free(K); free(rhs); free(cA); free(v); free(Hr); free(HZ); free(gr);
-    free(Ji); free(piv); free(act);
+    free(Ji); free(piv); free(act); free(om);
     return ok;
 }
 
@@ -368,8 +378,9 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     if (getenv("ORC_NLP_EXIT")) sscanf(getenv("ORC_NLP_EXIT"), "%lf %lf %lf %lf", &fx, &fmu, &facc, &fdx);
     double dxlast = 1e300;                                  /* max |ap dx| of the last update */
     int npassed = 0;                                        /* near-optimal iterates so far */
-    int saved = 0, restore = 0;                             /* last near-optimal iterate since the residual tests passed */
-    double *xsave = malloc(sizeof(double) * n);
+    int saved = 0, restore = 0;                             /* best near-optimal iterate since the residual tests passed */
+    double best_rx = 1e300;
+    double *xsave = malloc(sizeof(double) * n), *ssave = malloc(sizeof(double) * m), *zsave = malloc(sizeof(double) * m);
     int nearwait = ORC_NLP_NEARWAIT;
     if (getenv("ORC_NLP_NEARWAIT")) nearwait = atoi(getenv("ORC_NLP_NEARWAIT"));
     double tr_sigma = 0.0;
@@ -406,7 +417,13 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         /* a solve that passed the residual tests and then left the near-optimal region is past
          * its round-off floor: ACCEPTABLE at the last near-optimal iterate */
         if (saved && !near) { restore = 1; flag = 4; break; }
-        if (near && (saved || pass)) { memcpy(xsave, x, sizeof(double) * n); saved = 1; }
+        /* the saved iterate is the best near-optimal one (smallest scaled dual residual) since the
+         * residual tests passed; the polish starts from its s, z too */
+        if (near && (saved || pass) && nrx / gmax <= best_rx) {
+            best_rx = nrx / gmax;
+            memcpy(xsave, x, sizeof(double) * n); memcpy(ssave, s, sizeof(double) * m); memcpy(zsave, z, sizeof(double) * m);
+            saved = 1;
+        }
         if (near && ++npassed >= nearwait) { flag = 4; break; }
         for (int r = 0; r < m; r++) { lam[r] = sqrt(s[r] * z[r]); wgt[r] = s[r] / z[r]; }
         double mu = dotv(lam, lam, m) / m;
@@ -503,18 +520,22 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         for (int r = 0; r < m; r++) { s[r] += ap * dsv[r]; z[r] += ad * dz[r]; }
         it++;
     }
-    if (restore || (flag == 2 && saved)) { memcpy(x, xsave, sizeof(double) * n); flag = 4; }
+    if (saved && (restore || flag == 2 || flag == 4)) {   /* ACCEPTABLE / MAXIT: the best saved iterate */
+        memcpy(x, xsave, sizeof(double) * n); memcpy(s, ssave, sizeof(double) * m); memcpy(z, zsave, sizeof(double) * m);
+        flag = 4;
+    }
     if (getenv("ORC_POLISH_RHO")) g_polish_rho = atof(getenv("ORC_POLISH_RHO"));
     if (getenv("ORC_POLISH_ZINIT")) g_polish_zinit = atoi(getenv("ORC_POLISH_ZINIT"));
     if (getenv("ORC_POLISH_KAPPA")) g_polish_kappa = atof(getenv("ORC_POLISH_KAPPA"));
     if (getenv("ORC_POLISH_IT")) g_polish_it = atoi(getenv("ORC_POLISH_IT"));
     if (getenv("ORC_POLISH_PASSES")) g_polish_passes = atoi(getenv("ORC_POLISH_PASSES"));
+    if (getenv("ORC_POLISH_OMCAP")) g_polish_omcap = atof(getenv("ORC_POLISH_OMCAP"));
     const int do_polish = ORC_POLISH_ON ? getenv("ORC_NO_POLISH") == NULL : getenv("ORC_POLISH") != NULL;
     if (do_polish && !early_done && (flag == 0 || flag == 4 || flag == 2) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
     free(xe); free(ze);
     memcpy(x_out, x, sizeof(double) * n);
     if (iters_out) *iters_out = it;
-    free(xsave);
+    free(xsave); free(ssave); free(zsave);
     free(P.gnz); free(P.gval); free(hh); free(x); free(q); free(s); free(z); free(g); free(Jv); free(Ji);
     free(rx); free(ry); free(rz); free(lam); free(wgt); free(ds); free(dsv); free(dz); free(r3); free(K); free(Hl);
     free(rhs); free(dx); free(dq); free(hdiag); free(Z); free(Hr); free(HZ); free(piv);

@@ -692,14 +692,14 @@ extern "C" void srb_fit_bezier(const double buf[4], const double *X, double alph
 extern "C" const char *srb_last_error(void) { return g_err.c_str(); }
 
 #ifdef SRB_NLPDBG
-extern __device__ double srb_nlp_dbg[8 * 64];
+extern __device__ double srb_nlp_dbg[SRB_NLP_DBG_LEN];
 extern __device__ int srb_nlp_dbg_agent;
 // diagnostic build only: select the traced agent (-1: none) and read/clear the trace
 extern "C" int srb_debug_nlp_trace(int agent, double *out)
 {
     HIPCHK(hipDeviceSynchronize());
-    if (out) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_nlp_dbg), sizeof(double) * 8 * 64));
-    double z[8 * 64] = {0};
+    if (out) HIPCHK(hipMemcpyFromSymbol(out, HIP_SYMBOL(srb_nlp_dbg), sizeof(double) * SRB_NLP_DBG_LEN));
+    double z[SRB_NLP_DBG_LEN] = {0};
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(srb_nlp_dbg), z, sizeof z));
     HIPCHK(hipMemcpyToSymbol(HIP_SYMBOL(srb_nlp_dbg_agent), &agent, sizeof(int)));
     return SRB_OK;

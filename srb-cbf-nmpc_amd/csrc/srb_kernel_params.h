@@ -36,8 +36,12 @@
 #ifndef SRB_POLISH_ON
 #define SRB_POLISH_ON 1
 #endif
+
+// diagnostic trace buffer of the nlpdbg build (srb_kernels.hip, srb_capi.cpp)
+#define SRB_NLP_DBG_LEN (8 * 64 + 32 * 32 + 32 + 1024 + 256)
 #define SRB_POLISH_RHO 1e8
 #define SRB_POLISH_KAPPA 1e4
+#define SRB_POLISH_OMCAP 1e-2      // inactive rows: proximal Hessian weight min(z/s, OMCAP)
 #define SRB_POLISH_IT 3
 #ifndef SRB_POLISH_PASSES
 #define SRB_POLISH_PASSES 2

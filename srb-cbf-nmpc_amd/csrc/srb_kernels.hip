@@ -73,13 +73,24 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 // srb_nlp_dbg_agent records, per NLP iteration, ||rx||, its threshold, ||rz||, s'z/m, ap, ad,
 // delta and sigma (8 doubles) into srb_nlp_dbg; nothing else reads it.
 #ifdef SRB_NLPDBG
-__device__ double srb_nlp_dbg[8 * 64];
+__device__ double srb_nlp_dbg[SRB_NLP_DBG_LEN];
 __device__ int srb_nlp_dbg_agent = -1;
 #define NLPDBG(it, k, v) do { if (nl && agent == srb_nlp_dbg_agent && tid == 0 && (it) < 64) srb_nlp_dbg[8 * (it) + (k)] = (v); } while (0)
 // polish kernel: pass p of the traced agent into row 56 + p: primal, |c_A|, -min z_A, max |z_A|,
 // max inactive violation, last |dx|, accepted, Newton steps
 #define POLDBG(p, k, v) do { if (agent == srb_nlp_dbg_agent && tid == 0 && (p) < 8) srb_nlp_dbg[8 * (56 + (p)) + (k)] = (v); } while (0)
+// polish kernel, first Newton step of pass 0: the reduced matrix (32 x 32 at 512) and right-hand
+// side (at 512 + 1024) of the traced agent, for an eigenvalue check on the host
+// and, at the polish kernel's start, the exported zpol row values (2 S at 1568) and x (at 2592)
+#define POLDBG_IN(zp, S, xs, n) do { if (agent == srb_nlp_dbg_agent) { \
+    for (int e = tid; e < 2 * (S) && e < 1024; e += NTH) srb_nlp_dbg[1568 + e] = (zp)[e]; \
+    for (int e = tid; e < (n) && e < 256; e += NTH) srb_nlp_dbg[2592 + e] = (xs)[e]; } } while (0)
+#define POLDBG_MAT(H, LDH, v, nz) do { if (agent == srb_nlp_dbg_agent) \
+    for (int e = tid; e < (nz) * (nz); e += NTH) { srb_nlp_dbg[512 + 32 * (e / (nz)) + e % (nz)] = (H)[(e / (nz)) * (LDH) + e % (nz)]; \
+        if (e < (nz)) srb_nlp_dbg[512 + 1024 + e] = (v)[e]; } } while (0)
 #else
+#define POLDBG_MAT(H, LDH, v, nz) do {} while (0)
+#define POLDBG_IN(zp, S, xs, n) do {} while (0)
 #define NLPDBG(it, k, v) do {} while (0)
 #define POLDBG(p, k, v) do {} while (0)
 #endif
@@ -922,7 +933,24 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double inv_m = 1.0 / (double)mrows;
         double dxl = 1e300;              // this lane's max |ap dx| over its variable slots, last update
         int npassed = 0;                 // NLP: near-optimal iterates so far
-        bool saved = false, restore = false;   // NLP: xsv holds the last near-optimal iterate since the residual tests passed
+        bool saved = false, restore = false;   // NLP: xsv holds the best near-optimal iterate since the residual tests passed
+        double best_rx = 1e300;                // its dual residual / max(1, ||Q x + f||_inf)
+        // the polish kernel (srb_polish_kernel, launched next) starts from the NLP result: its active
+        // set and multipliers -- rows with s * KAPPA < z keep z (as float: only the Newton
+        // iteration's starting guess), the others -min(z/s, OMCAP), their barrier weight, as a proximal term
+        // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
+        // (the saved one on a restore)
+        auto export_zpol = [&]() {
+            float *zp = zpol_g + (size_t)agent * zstride;
+#pragma unroll
+            for (int t = 0; t < TS; t++)
+                if (t < nts && tid + NTH * t < S)
+#pragma unroll
+                    for (int r = 0; r < 2; r++)
+                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0f
+                            : Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? (float)Q[t].z[r]
+                            : (float)(-fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP));
+        };
         for (int iter = 0; iter < maxit; iter++) {
             STAMP_BEGIN();
             // ---- residuals (computeresiduals, Auxilary.c:524-553), norms, reciprocals
@@ -975,8 +1003,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // a solve that passed the residual tests and then left the near-optimal region is
             // past its round-off floor: ACCEPTABLE at the last near-optimal iterate (oracle, same rule)
             if (nl && saved && !near) { restore = true; flag = 4; break; }
-            if (near && (saved || pass)) {         // each thread copies the variables it owns
+            if (near && (saved || pass) && nrx / gm <= best_rx) {   // each thread copies the variables it owns
+                best_rx = nrx / gm;
                 for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
+                if (zpol_g) export_zpol();
                 saved = true;
             }
             if (near && ++npassed >= SRB_NLP_NEARWAIT) { flag = 4; break; }
@@ -1197,22 +1227,11 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             if (acc) { flag = 4; break; }
             it++;
         }
-        if (nl && (restore || (flag == 2 && saved))) {
+        if (nl && saved && (restore || flag == 2 || flag == 4)) {      // ACCEPTABLE / MAXIT: the best saved iterate
             for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];     // owner threads, as saved
-            flag = 4;
-        }
-
-        // the polish kernel (srb_polish_kernel, launched next) starts from this result: its active
-        // set and multipliers -- rows with s * KAPPA < z keep z (as float: only the Newton
-        // iteration's starting guess), the others 0 -- go to HBM, zpol_g[agent][2 slot + row]
-        if (zpol_g && nl) {
-            float *zp = zpol_g + (size_t)agent * zstride;
-#pragma unroll
-            for (int t = 0; t < TS; t++)
-                if (t < nts && tid + NTH * t < S)
-#pragma unroll
-                    for (int r = 0; r < 2; r++)
-                        zp[2 * (tid + NTH * t) + r] = (Q[t].m[r] != 0.0 && Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r]) ? (float)Q[t].z[r] : 0.0f;
+            flag = 4;                                               // (zpol_g: exported at the save)
+        } else if (zpol_g && nl) {
+            export_zpol();
         }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
     }
@@ -1257,6 +1276,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     SRB_AGENT_OBSTACLES;
     SYNC();
     const float *zp = zpol_g + (size_t)agent * zstride;
+    POLDBG_IN(zp, S, xs, n);
     double Mi[NZL], dxi[NZL];
     // ---------------- active-set polish of the NLP result (oracle/nlp_ipm.c `polish`, the same rules) ----------------
     // Near its round-off floor the barrier system's active rows carry z/s ~ 1e14, so the
@@ -1271,7 +1291,9 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     // violated rows join, and the next pass starts again from the interior-point result (at
     // most SRB_POLISH_PASSES); a rejected polish leaves that result.  The slots are rebuilt
     // here (the interior-point slot state is dead); their fields ds = active mask, dz = z_A,
-    // r3 = row value g - h, jd = g(x).
+    // r3 = row value g - h, jd = g(x), s = the inactive rows' interior-point weight z/s, kept in
+    // the Hessian only (a proximal term: the fixed point is unchanged, and the reduced matrix
+    // stays definite along directions no active row pins, lambda with four contacts).
     {
         const int nts = (S + NTH - 1) / NTH;
         const int cnt = rO, nko = NKP;
@@ -1285,8 +1307,10 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                q.dz[r] = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
-                q.ds[r] = (q.dz[r] > 0.0) ? 1.0 : 0.0;
+                const double v = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
+                q.ds[r] = (v > 0.0) ? 1.0 : 0.0;
+                q.dz[r] = fmax(v, 0.0);
+                q.s[r] = fmax(-v, 0.0);
             }
         }
         bool accepted = false;
@@ -1305,7 +1329,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                         Slot &q = P[t];
                         q.r3[0] = q.jd - q.h[0]; q.r3[1] = -q.jd - q.h[1];
                         const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
-                        const double wa = prm.polish_rho * (q.ds[0] + q.ds[1]);
+                        const double wa = (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]);
                         if (kind_of(q) == K_VAR) {
                             double hs = 0.0;
                             if (q.i0 < 4 * N && !(q.i0 & 1)) hs = -2.0 * zo_sum(zo, q.i0 >> 2, K);
@@ -1322,12 +1346,14 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                     if (t < nts && kind_of(P[t]) == K_VEL) {
                         const Slot &q = P[t];
                         const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
-                        __hip_atomic_fetch_add(&W[q.r], prm.polish_rho * (q.ds[0] + q.ds[1]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&W[q.r], (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]),
+                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                         __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 SYNC();
                 gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
                 SYNC();
+                if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);
                 gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
                 if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; }      // not PD: reject
                 la_solve<NZL>(Mi, H0, vg, vy, vr, vd, dxi, nz, lane);

@@ -23,7 +23,7 @@ A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 s = srbnmpc.BatchSolver(p, A)
 L = srbnmpc.lib()
 L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-buf = np.zeros(8 * 64)
+buf = np.zeros(8 * 64 + 32 * 32 + 32 + 1024 + 256)
 for ag in map(int, sys.argv[2:]):
     L.srb_debug_nlp_trace(ag, None)
     out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"] if cfg["K_nbr"] else None)
@@ -38,3 +38,11 @@ for ag in map(int, sys.argv[2:]):
         r = buf[8 * (56 + p):8 * (56 + p) + 8]
         if r.any():
             print(f"  {p:2d}          " + " ".join(f"{v:10.3e}" for v in r[:7]), flush=True)
+    nzr = int((np.abs(buf[512 + 32 * np.arange(32) + np.arange(32)]) > 0).sum())
+    if nzr:
+        Hm = buf[512:512 + 1024].reshape(32, 32)[:nzr, :nzr]
+        ev = np.linalg.eigvalsh(0.5 * (Hm + Hm.T))
+        print(f"  polish reduced matrix (pass 0, step 0): nz {nzr}  asym {np.abs(Hm - Hm.T).max():.3e}  "
+              f"eig min {ev[0]:.6e} max {ev[-1]:.6e}  diag min {np.diag(Hm).min():.3e}", flush=True)
+        np.save(os.path.join("gpurun_out", f"polish_H_{ag}.npy"), np.concatenate([Hm.ravel(), buf[512 + 1024:512 + 1024 + nzr]]))
+        np.save(os.path.join("gpurun_out", f"polish_in_{ag}.npy"), buf[1568:])
