@@ -146,9 +146,9 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #ifndef ORC_POLISH_ON
 #define ORC_POLISH_ON 1           /* the kernel's SRB_POLISH_ON */
 #endif
-#define ORC_POLISH_RHO 1e8
-#define ORC_POLISH_IT 3           /* at most this many Newton steps per active-set pass */
-#define ORC_POLISH_PASSES 2       /* active-set passes (the most negative z_A leaves, violated rows join) */
+#define ORC_POLISH_RHO 1e9
+#define ORC_POLISH_IT 5           /* at most this many Newton steps per active-set pass */
+#define ORC_POLISH_PASSES 3       /* active-set passes (the most negative z_A leaves, violated rows join) */
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
 #define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */
@@ -351,11 +351,12 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         for (int r = 1; r < m; r++) if (hh[r] - g[r] < mn) mn = hh[r] - g[r];
         double ap = -mn;
         for (int r = 0; r < m; r++) { s[r] = (ap < 0) ? hh[r] - g[r] : hh[r] - g[r] + (1 + ap); z[r] = ORC_NLP_Z0; }
-        /* duals z_r = ORC_NLP_Z0 / s_r (round 3; the kernel's SRB_NLP_Z0, the same rule): every row
-         * starts at complementarity Z0 instead of z = Z0 on rows whose slack is far from the
-         * bound (the +-1e3 boxes); on the bench batches the NLP needs 8.1 / 8.5 iterations on
-         * average against 8.9 / 9.3 (N = 10 / 20) and at most 12 / 13 against 13 / 17 */
-        for (int r = 0; r < m; r++) z[r] = ORC_NLP_Z0 / s[r];
+        /* duals z_r = ORC_NLP_Z0 / max(s_r, 1) (round 3; the kernel's SRB_NLP_Z0, the same rule):
+         * rows whose slack is far from the bound (the +-1e3 boxes) start at complementarity Z0
+         * instead of z = Z0; on the bench batches the NLP needs 8.1 / 8.5 iterations on average
+         * against 8.9 / 9.3 (N = 10 / 20) and at most 12 / 13 against 13 / 17.  The floor keeps
+         * rows the QP left at their bound (s ~ 1e-12 when no shift is needed) from z ~ 1e14 */
+        for (int r = 0; r < m; r++) z[r] = ORC_NLP_Z0 / fmax(s[r], 1.0);
     }
     {   /* q = A'y, y = argmin |A'y + (Px + c + J'z)|  ->  (A A') y = -A v */
         double *v = malloc(sizeof(double) * n), *AAt = malloc(sizeof(double) * (p ? p * p : 1)), *yy = malloc(sizeof(double) * (p + 1));
@@ -378,7 +379,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     if (getenv("ORC_NLP_EXIT")) sscanf(getenv("ORC_NLP_EXIT"), "%lf %lf %lf %lf", &fx, &fmu, &facc, &fdx);
     double dxlast = 1e300;                                  /* max |ap dx| of the last update */
     int npassed = 0;                                        /* near-optimal iterates so far */
-    int saved = 0, restore = 0;                             /* best near-optimal iterate since the residual tests passed */
+    int saved = 0, restore = 0;                             /* best near-optimal iterate */
     double best_rx = 1e300;
     double *xsave = malloc(sizeof(double) * n), *ssave = malloc(sizeof(double) * m), *zsave = malloc(sizeof(double) * m);
     int nearwait = ORC_NLP_NEARWAIT;
@@ -414,12 +415,12 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
          * threshold.  An inertia shift or a blocked step from here is the condensed system's
          * round-off (W = z/s ~ 1e14 swamps the soft curvature), not progress: ACCEPTABLE (4) */
         const int near = nrz < th && nry < th && sz / m < fmu * tol && nrx < facc * fx * th * gmax;
-        /* a solve that passed the residual tests and then left the near-optimal region is past
-         * its round-off floor: ACCEPTABLE at the last near-optimal iterate */
+        /* a solve that reached the near-optimal region and then left it is past its round-off
+         * floor: ACCEPTABLE at the best near-optimal iterate */
         if (saved && !near) { restore = 1; flag = 4; break; }
-        /* the saved iterate is the best near-optimal one (smallest scaled dual residual) since the
-         * residual tests passed; the polish starts from its s, z too */
-        if (near && (saved || pass) && nrx / gmax <= best_rx) {
+        /* the saved iterate is the best near-optimal one (smallest scaled dual residual); the
+         * polish starts from its s, z too */
+        if (near && nrx / gmax <= best_rx) {
             best_rx = nrx / gmax;
             memcpy(xsave, x, sizeof(double) * n); memcpy(ssave, s, sizeof(double) * m); memcpy(zsave, z, sizeof(double) * m);
             saved = 1;

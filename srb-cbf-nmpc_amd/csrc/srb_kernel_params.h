@@ -38,13 +38,13 @@
 #endif
 
 // diagnostic trace buffer of the nlpdbg build (srb_kernels.hip, srb_capi.cpp)
-#define SRB_NLP_DBG_LEN (8 * 64 + 32 * 32 + 32 + 1024 + 256)
-#define SRB_POLISH_RHO 1e8
+#define SRB_NLP_DBG_LEN (8 * 64 + 32 * 32 + 32 + 1024 + 256 + 3 * 256)
+#define SRB_POLISH_RHO 1e9
 #define SRB_POLISH_KAPPA 1e4
 #define SRB_POLISH_OMCAP 1e-2      // inactive rows: proximal Hessian weight min(z/s, OMCAP)
-#define SRB_POLISH_IT 3
+#define SRB_POLISH_IT 5
 #ifndef SRB_POLISH_PASSES
-#define SRB_POLISH_PASSES 2
+#define SRB_POLISH_PASSES 3
 #endif
 #define SRB_POLISH_PTOL 1e-9
 #define SRB_POLISH_DXTOL 1e-7

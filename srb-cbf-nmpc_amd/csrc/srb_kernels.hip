@@ -85,12 +85,16 @@ __device__ int srb_nlp_dbg_agent = -1;
 #define POLDBG_IN(zp, S, xs, n) do { if (agent == srb_nlp_dbg_agent) { \
     for (int e = tid; e < 2 * (S) && e < 1024; e += NTH) srb_nlp_dbg[1568 + e] = (zp)[e]; \
     for (int e = tid; e < (n) && e < 256; e += NTH) srb_nlp_dbg[2592 + e] = (xs)[e]; } } while (0)
+// x after each Newton step of pass 0 (3 x 256 at 2848)
+#define POLDBG_X(p, it, xs, n) do { SYNC(); if (agent == srb_nlp_dbg_agent && (p) == 0 && (it) < 3) \
+    for (int e = tid; e < (n) && e < 256; e += NTH) srb_nlp_dbg[2848 + 256 * (it) + e] = (xs)[e]; } while (0)
 #define POLDBG_MAT(H, LDH, v, nz) do { if (agent == srb_nlp_dbg_agent) \
     for (int e = tid; e < (nz) * (nz); e += NTH) { srb_nlp_dbg[512 + 32 * (e / (nz)) + e % (nz)] = (H)[(e / (nz)) * (LDH) + e % (nz)]; \
         if (e < (nz)) srb_nlp_dbg[512 + 1024 + e] = (v)[e]; } } while (0)
 #else
 #define POLDBG_MAT(H, LDH, v, nz) do {} while (0)
 #define POLDBG_IN(zp, S, xs, n) do {} while (0)
+#define POLDBG_X(p, it, xs, n) do {} while (0)
 #define NLPDBG(it, k, v) do {} while (0)
 #define POLDBG(p, k, v) do {} while (0)
 #endif
@@ -719,7 +723,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
                 const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
-                const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride, double *lds)
+                const int *__restrict__ sel_g, double *__restrict__ zpol_g, int zstride, double *lds)
 {
     SRB_AGENT_LAYOUT;
 #ifdef SRB_STAMPS
@@ -889,9 +893,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     const double f = q.jd;
                     q.s[0] = (q.m[0] != 0.0) ? q.h[0] - f + ssh : 1.0;
                     q.s[1] = (q.m[1] != 0.0) ? q.h[1] + f + ssh : 1.0;
-                    // z = Z0 / s: every row starts at complementarity Z0 (oracle/nlp_ipm.c, same rule)
-                    q.z[0] = SRB_NLP_Z0 * rcp_d(q.s[0]);
-                    q.z[1] = SRB_NLP_Z0 * rcp_d(q.s[1]);
+                    // z = Z0 / max(s, 1): rows far from their bound start at complementarity Z0, the
+                    // others at Z0 (oracle/nlp_ipm.c, same rule)
+                    q.z[0] = SRB_NLP_Z0 * rcp_d(fmax(q.s[0], 1.0));
+                    q.z[1] = SRB_NLP_Z0 * rcp_d(fmax(q.s[1], 1.0));
                     if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x (gram_rhs)
                         const int o = q.r - rO;
                         OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
@@ -933,23 +938,23 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         const double inv_m = 1.0 / (double)mrows;
         double dxl = 1e300;              // this lane's max |ap dx| over its variable slots, last update
         int npassed = 0;                 // NLP: near-optimal iterates so far
-        bool saved = false, restore = false;   // NLP: xsv holds the best near-optimal iterate since the residual tests passed
+        bool saved = false, restore = false;   // NLP: xsv holds the best near-optimal iterate
         double best_rx = 1e300;                // its dual residual / max(1, ||Q x + f||_inf)
         // the polish kernel (srb_polish_kernel, launched next) starts from the NLP result: its active
-        // set and multipliers -- rows with s * KAPPA < z keep z (as float: only the Newton
-        // iteration's starting guess), the others -min(z/s, OMCAP), their barrier weight, as a proximal term
+        // set and multipliers -- rows with s * KAPPA < z keep z (in double: a multiplier rounded
+        // to float costs the Newton iteration a step), the others -min(z/s, OMCAP), their barrier
+        // weight, as a proximal term
         // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
         // (the saved one on a restore)
         auto export_zpol = [&]() {
-            float *zp = zpol_g + (size_t)agent * zstride;
+            double *zp = zpol_g + (size_t)agent * zstride;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts && tid + NTH * t < S)
 #pragma unroll
                     for (int r = 0; r < 2; r++)
-                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0f
-                            : Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? (float)Q[t].z[r]
-                            : (float)(-fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP));
+                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0
+                            : Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? Q[t].z[r] : -fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP);
         };
         for (int iter = 0; iter < maxit; iter++) {
             STAMP_BEGIN();
@@ -1000,10 +1005,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // system (W = z/s ~ 1e14 swamps the soft curvature in Z'HZ), not progress -> exit
             // ACCEPTABLE (4) at this iterate (oracle/nlp_ipm.c, the same rule)
             const bool near = nl && nrz < th && sz * inv_m < tol && nrx < 100.0 * thx;
-            // a solve that passed the residual tests and then left the near-optimal region is
-            // past its round-off floor: ACCEPTABLE at the last near-optimal iterate (oracle, same rule)
+            // a solve that reached the near-optimal region and then left it is past its round-off
+            // floor: ACCEPTABLE at the best near-optimal iterate (oracle, same rule)
             if (nl && saved && !near) { restore = true; flag = 4; break; }
-            if (near && (saved || pass) && nrx / gm <= best_rx) {   // each thread copies the variables it owns
+            if (near && nrx / gm <= best_rx) {     // each thread copies the variables it owns
                 best_rx = nrx / gm;
                 for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
                 if (zpol_g) export_zpol();
@@ -1263,7 +1268,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ obstacles, const double *__restrict__ nbr_state,
                 double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,
                 const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
-                const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride, double *lds)
+                const int *__restrict__ sel_g, const double *__restrict__ zpol_g, int zstride, double *lds)
 {
     SRB_AGENT_LAYOUT;
     double *Rt = R + rC * LDR;
@@ -1275,7 +1280,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     for (int v = tid; v < n; v += NTH) { const double xv = x_out[(size_t)agent * n + v]; xs[v] = xv; xsv[v] = xv; }
     SRB_AGENT_OBSTACLES;
     SYNC();
-    const float *zp = zpol_g + (size_t)agent * zstride;
+    const double *zp = zpol_g + (size_t)agent * zstride;
     POLDBG_IN(zp, S, xs, n);
     double Mi[NZL], dxi[NZL];
     // ---------------- active-set polish of the NLP result (oracle/nlp_ipm.c `polish`, the same rules) ----------------
@@ -1307,7 +1312,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                const double v = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
+                const double v = (t < nts && sl < S) ? zp[2 * sl + r] : 0.0;
                 q.ds[r] = (v > 0.0) ? 1.0 : 0.0;
                 q.dz[r] = fmax(v, 0.0);
                 q.s[r] = fmax(-v, 0.0);
@@ -1378,6 +1383,8 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                     wred_x<1, 1u, NW>(rv, red + 8 * 8 * NW, tid);
                     lastdx = rv[0];
                 }
+                POLDBG(4 + pass, pit, lastdx);
+                POLDBG_X(pass, pit, xs, n);
                 if (lastdx <= SRB_POLISH_DXTOL) break;       // converged: no further step
             }
             if (bad) break;
@@ -1452,7 +1459,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
         int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,       \
-        const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride)                               \
+        const int *__restrict__ sel_g, double *__restrict__ zpol_g, int zstride)                               \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
@@ -1466,7 +1473,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ footg, const double *__restrict__ obstacles,                                 \
         const double *__restrict__ nbr_state, double *__restrict__ x_out, double *__restrict__ obj_out,          \
         int *__restrict__ status_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,     \
-        const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride)                         \
+        const int *__restrict__ sel_g, const double *__restrict__ zpol_g, int zstride)                         \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \

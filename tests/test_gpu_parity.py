@@ -206,9 +206,9 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
     The interior-point exit needs the residual tests AND a last primal step max |ap dx| < 3e-5
     (SRB_NLP_DXTOL); its result is then polished to the exact KKT point of its active set
     (srb_polish_kernel), which ends the solve OPTIMAL.  A polish that is not
-    accepted (measured: well under 1 % of these solves) leaves the interior-point result with
-    its status (ACCEPTABLE = 4 at the round-off floor); every such solution, plus a sample of the
-    rest, must pass the KKT certificate."""
+    accepted leaves the interior-point result with
+    its status (ACCEPTABLE = 4 at the round-off floor; measured 1 of 2048, the oracle 0); every such
+    solution, plus a sample of the rest, must pass the KKT certificate."""
     A, N, C, Ko, Kn = 2048, 20, 2, 3, 8
     b = workload.make_batch(A, N, C, seed=1234)
     s = solver(N, C, Ko, Kn)
@@ -216,7 +216,7 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
     st, it = out["status"], out["iters"]
     assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
     acc = np.where(st[:, 1] == srbnmpc.ACCEPTABLE)[0]
-    assert acc.size <= 0.005 * A, acc.size                         # polish accepted on >= 99.5 %
+    assert acc.size <= 0.001 * A, acc.size                         # polish accepted on >= 99.9 %
     assert it[:, 1].max() <= 20                                    # no MAXIT tail (measured max 17)
     op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
     r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], nthreads=16)
@@ -224,7 +224,7 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
     e = np.abs(xus(N, out["x"]) - xus(N, r["x"])).max(1)
     assert e.max() < NLP_TOL, (int(np.argmax(e)), float(e.max()))
     both = (st[:, 1] == 0) & (r["status"][:, 1] == 0)        # polished on both sides: the same KKT point
-    assert both.mean() >= 0.995 and e[both].max() < 1e-6, (both.mean(), float(e[both].max()))
+    assert both.mean() >= 0.999 and e[both].max() < 1e-6, (both.mean(), float(e[both].max()))
     rng = np.random.default_rng(5)
     for a in np.r_[acc[:64], rng.choice(A, 16, replace=False)]:
         obs, eps = oracle.select_obstacles(op, b["x0"][a], b["obstacles"], b["nbr_state"], int(a))

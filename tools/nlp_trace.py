@@ -23,7 +23,7 @@ A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 s = srbnmpc.BatchSolver(p, A)
 L = srbnmpc.lib()
 L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-buf = np.zeros(8 * 64 + 32 * 32 + 32 + 1024 + 256)
+buf = np.zeros(8 * 64 + 32 * 32 + 32 + 1024 + 256 + 3 * 256)
 for ag in map(int, sys.argv[2:]):
     L.srb_debug_nlp_trace(ag, None)
     out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"] if cfg["K_nbr"] else None)
@@ -34,10 +34,11 @@ for ag in map(int, sys.argv[2:]):
         r = buf[8 * i:8 * i + 8]
         print(f"  {i:2d} " + " ".join(f"{v:10.3e}" for v in r), flush=True)
     print("  polish pass: primal     |c_A|     -min z_A   max|z_A|   inact.viol  last|dx|   accepted")
-    for p in range(8):
+    for p in range(4):
         r = buf[8 * (56 + p):8 * (56 + p) + 8]
         if r.any():
             print(f"  {p:2d}          " + " ".join(f"{v:10.3e}" for v in r[:7]), flush=True)
+            print("      Newton |dx|: " + " ".join(f"{v:10.3e}" for v in buf[8 * (60 + p):8 * (60 + p) + 8] if v), flush=True)
     nzr = int((np.abs(buf[512 + 32 * np.arange(32) + np.arange(32)]) > 0).sum())
     if nzr:
         Hm = buf[512:512 + 1024].reshape(32, 32)[:nzr, :nzr]
