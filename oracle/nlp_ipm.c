@@ -148,7 +148,7 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #endif
 #define ORC_POLISH_RHO 1e9
 #define ORC_POLISH_IT 5           /* at most this many Newton steps per active-set pass */
-#define ORC_POLISH_PASSES 3       /* active-set passes (the most negative z_A leaves, violated rows join) */
+#define ORC_POLISH_PASSES 4       /* active-set passes (the most negative z_A leaves, violated rows join) */
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
 #define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */

@@ -44,7 +44,7 @@
 #define SRB_POLISH_OMCAP 1e-2      // inactive rows: proximal Hessian weight min(z/s, OMCAP)
 #define SRB_POLISH_IT 5
 #ifndef SRB_POLISH_PASSES
-#define SRB_POLISH_PASSES 3
+#define SRB_POLISH_PASSES 4
 #endif
 #define SRB_POLISH_PTOL 1e-9
 #define SRB_POLISH_DXTOL 1e-7
@@ -86,6 +86,15 @@ static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
 // doubles of dynamic LDS one agent needs for instance bound NZL; must match the carve in
 // nmpc_agent (srb_kernels.hip)
+// Obstacle term rows: materialised in LDS at each re-linearisation for the small instances
+// (NZL <= SRB_OBS_STORED_MAX: the rows fit and a stored row is one LDS load per Gram element),
+// generated inside the Gram from the grid's CoM rows and (jx, jy) for the large ones, where the
+// N K stored rows would fill the LDS (N = 20: 1 agent per CU instead of 2)
+#ifndef SRB_OBS_STORED_MAX
+#define SRB_OBS_STORED_MAX 16
+#endif
+#define SRB_OBS_STORED(NZL) ((NZL) <= SRB_OBS_STORED_MAX)
+
 static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
 {
     const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZM + 1;
@@ -95,7 +104,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return rO * LDR + 2 * (TT + 1) + 2 * NKP + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
+    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
            (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64

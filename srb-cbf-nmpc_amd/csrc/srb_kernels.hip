@@ -137,6 +137,23 @@ __device__ __forceinline__ double term_elem(const double *R, const double *OJ, i
     return (col < NZL) ? fma(jx, R[xr * LDR + col], fma(jy, R[(xr + 2) * LDR + col], (col == nz - 1) ? -1.0 : 0.0)) : 0.0;
 }
 
+// Re-linearisation of obstacle row o at x: J_o = (jx, jy, -1) on (p_x(k), p_y(k), slack).  Stored-row
+// instances (SRB_OBS_STORED(NZL)) materialise its term row in R, M_o = jx Z_x(k) + jy Z_y(k) - e_s
+// (i0 = 4k, i1 = 4k + 2: the grid's CoM rows); the others keep (jx, jy) in OJ for gram_rhs
+template <int NZL>
+__device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, int i0, int i1, double jx, double jy, int nz)
+{
+    if constexpr (SRB_OBS_STORED(NZL)) {
+        constexpr int LDR = NZL + 1;
+        double *dst = R + (rO + o) * LDR;
+        const double *zx = R + i0 * LDR, *zy = R + i1 * LDR;
+#pragma unroll
+        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == nz - 1) ? -1.0 : 0.0));
+    } else {
+        OJ[2 * o] = jx; OJ[2 * o + 1] = jy;
+    }
+}
+
 template <int NZL, bool RHS, int NW>
 __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt, const double *OJ,
                                          int rO, int nko, int K, double *H, double *g, int nz, int tid, double *part)
@@ -182,7 +199,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
         const int chunk = cnt / NW, tb = wv * chunk;
         for (int t0 = tb; t0 < tb + chunk; t0 += 16) batch(t0, false);
         const int och = nko / NW, ob = rO + wv * och;
-        for (int t0 = ob; t0 < ob + och; t0 += 16) batch(t0, true);
+        for (int t0 = ob; t0 < ob + och; t0 += 16) batch(t0, !SRB_OBS_STORED(NZL));
     }
     double gs[NTC];
     if (RHS)
@@ -275,7 +292,7 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
         const int chunk = cnt / NW, tb = wv * chunk;
         range(tb, tb + chunk, false);
         const int och = nko / NW, ob = rO + wv * och;
-        range(ob, ob + och, true);
+        range(ob, ob + och, !SRB_OBS_STORED(NZL));
     }
 #pragma unroll
     for (int tc = 0; tc < NTC; tc++) {
@@ -550,7 +567,7 @@ __device__ __forceinline__ double var_weight(const SrbKParams &prm, int v)
 // staging of the interior-point loop is not worth its pressure here) and its multiplier into zo.
 template <int NZL, int TS, int NW>
 __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double *xs, double *OJ, double *zo, int n,
-                                            int rO)
+                                            int rO, double *R, int nz)
 {
     const double s_var = xs[n - 1];
 #pragma unroll
@@ -560,7 +577,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
             q.jd = slot_f(q, xs, s_var);
             if (kind_of(q) == K_OBS) {
                 const int o = q.r - rO;
-                OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
+                obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
                 zo[o] = q.ds[0] * q.dz[0];
             }
         }
@@ -593,10 +610,10 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     STAMP_DECL; \
     /* LDS carve (must match srb_lds_doubles) */ \
     double *p = lds; \
-    double *R = p; p += rO * LDR;                 /* stored term rows (Z rows first) */ \
+    double *R = p; p += (SRB_OBS_STORED(NZL) ? TT : rO) * LDR;   /* stored term rows (Z rows first) */ \
     double *W = p; p += TT + 1;                   /* gram weights (+ one scratch entry) */ \
     double *CF = p; p += TT + 1;                  /* rhs coefficients (+ one scratch entry) */ \
-    double *OJ = p; p += 2 * NKP;                 /* obstacle terms: jx, jy (gram_rhs) */ \
+    double *OJ = p; p += SRB_OBS_STORED(NZL) ? 0 : 2 * NKP;   /* generated obstacle terms: jx, jy (gram_rhs) */ \
     double *H0 = p; p += NZM * LDH;               /* assembled Z'HZ (delta = 0) */ \
     double *HS = p; p += NZM * LDH;               /* Z'HZ + delta Z'Z (when delta != 0) */ \
     double *ZZ = p; p += NZM * LDH;               /* Z'Z (NLP) */ \
@@ -899,7 +916,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     q.z[1] = SRB_NLP_Z0 * rcp_d(fmax(q.s[1], 1.0));
                     if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x (gram_rhs)
                         const int o = q.r - rO;
-                        OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
+                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
                     }
                     // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z): each row's J'z on its
                     // term row (the velocity rows' below, onto their variables' rows)
@@ -980,7 +997,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
                     if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z (gram_rhs)
                         const int o = q.r - rO;
-                        OJ[2 * o] = -2.0 * (xs[q.i0] - q.a0); OJ[2 * o + 1] = -2.0 * (xs[q.i1] - q.a1);
+                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
                         zo[o] = q.z[0];
                     }
                 }
@@ -1126,7 +1143,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 double mxs = 0.0, mxz = 0.0;
                 // obstacle rows: J_o Z dxi = jx (Z_x dxi) + jy (Z_y dxi) - dxi_s, the CoM-position steps
                 // of every grid formed once (dpos) instead of one generated row per obstacle
-                if (nl) {
+                // (stored-row instances: every slot dots its own row)
+                if (nl && !SRB_OBS_STORED(NZL)) {
                     if (tid <= 2 * N)
                         dpos[tid] = row_dot<NZL>(R + (tid < 2 * N ? 4 * (tid >> 1) + 2 * (tid & 1) : TL.zr(n - 1)) * LDR, dxi);
                     SYNC();
@@ -1135,7 +1153,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        if (nl && kind_of(q) == K_OBS) {
+                        if (!SRB_OBS_STORED(NZL) && nl && kind_of(q) == K_OBS) {
                             const int o = q.r - rO;
                             q.jd = fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N]));
                         } else {
@@ -1326,7 +1344,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
 #pragma clang loop unroll(disable)
             for (int pit = 0; pit < SRB_POLISH_IT; pit++) {
                 SYNC();                                      // xs of the previous step / pass
-                polish_rows<NZL, TS, NW>(P, nts, xs, OJ, zo, n, rO);      // q.jd = g(x), M_o (OJ), zo = z_A
+                polish_rows<NZL, TS, NW>(P, nts, xs, OJ, zo, n, rO, R, nz);      // q.jd = g(x), M_o (OJ), zo = z_A
                 SYNC();                                      // R rows, zo
 #pragma unroll
                 for (int t = 0; t < TS; t++)
@@ -1367,7 +1385,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = P[t];
-                        const double jd = (kind_of(q) == K_OBS)      // J_o Z dxi, M_o generated (gram_rhs)
+                        const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS)      // J_o Z dxi, M_o generated (gram_rhs)
                             ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),
                                   fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))
                             : row_dot<NZL>(R + q.r * LDR, dxi);
