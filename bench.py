@@ -300,7 +300,7 @@ def main():
                     help="diagnostic: solve rank 0's shard of a swarm this many GPUs wide on one GPU (the whole "
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (tools/pmc_traffic.py); default profiles/r02_pmc_traffic_c<config>.json")
+                    help="PMC summary (tools/pmc_traffic.py); default profiles/r03_pmc_traffic_c<config>.json")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU check of the multi-process launch only (gloo, no GPU, no solve; tests/test_bench_launch.py)")
     args = ap.parse_args()
@@ -405,14 +405,15 @@ def main():
     achieved = flops / (solve_ms * 1e-3) / 1e12
     dense_per_solve = dense_equiv_flops(p, iters) / max(1, iters.shape[0])
     cyc_iter = solve_ms * 1e-3 * SCLK_GHZ * 1e9 / max(1, int(iters.sum(1).max()))
-    traffic = None
+    traffic = traffic_polish = None
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", f"r02_pmc_traffic_c{args.config}.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", f"r03_pmc_traffic_c{args.config}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
             if tj.get("config") == args.config and tj.get("agents") == n_loc:
                 traffic = tj.get("hbm_bytes_per_launch")
+                traffic_polish = tj.get("kernels", {}).get("srb_polish_kernel", {}).get("hbm_bytes")
         except Exception:
             traffic = None
     line = {
@@ -433,17 +434,19 @@ def main():
         "dense_kkt_flops_note": "SURVEY.md 8(d) work-equivalence figure: (2/3) d^3 + 4 d^2 per IPM iteration of the "
                                 "unreduced dense KKT (d = nv + neq) x this batch's iterations, per solve; a "
                                 "comparison with a dense-KKT solver, not executed flops and not a rate",
-        "roofline": {"bound": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+        "roofline": {"bound": "mfma", "limiter": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic,
+                     "traffic_source": os.path.relpath(args.traffic_json, ROOT) if traffic is not None else None,
                      "cycles_per_iter": cyc_iter,
                      "cycles_per_iter_note": "solve-kernel HIP-event time x 2.4 GHz / IPM iterations (QP + NLP) of "
                                              "the slowest agent: the critical-path cost of one iteration; per-phase "
-                                             "split in profiles/r02_*_stamps.txt",
+                                             "split in profiles/r03_*_stamps.txt",
                      "kernel": "srb_nmpc_kernel", "waves_per_agent": solver.waves(), "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
                      "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
                                    "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
                                    "agent), neither MFMA- nor HBM-throughput-bound",
                      "polish_ms": float(np.median(pol)), "polish_kernel": "srb_polish_kernel",
+                     "polish_traffic": traffic_polish,
                      "io_bytes_per_launch": io_bytes(p, n_loc, sh["obstacles"].shape[0], A_total if cfg["K_nbr"] else 0)},
         "cpu_baseline": None,
     }

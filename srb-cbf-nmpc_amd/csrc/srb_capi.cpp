@@ -19,20 +19,20 @@
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
-        const double *alpha_buf, double *alpha_out, const int *sel_g, double *zpol_g, int zstride);            \
+        const double *alpha_buf, double *alpha_out, const int *sel_g, float *zpol_g, int zstride);            \
     extern "C" __global__ void srb_polish_kernel_##NZL##_##TS##_##NW(                                         \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, const double *nbr_state, double *x_out, double *obj_out, int *status_out,     \
-        const double *alpha_buf, double *alpha_out, const int *sel_g, const double *zpol_g, int zstride);
+        const double *alpha_buf, double *alpha_out, const int *sel_g, const float *zpol_g, int zstride);
 SRB_KERNEL_INSTANCES(DECL_NMPC)
 #undef DECL_NMPC
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
-                              double *, const int *, double *, int);
+                              double *, const int *, float *, int);
 typedef void (*srb_polish_fn)(SrbKParams, int, const double *, const double *, const double *, const double *,
                               const double *, double *, double *, int *, const double *, double *, const int *,
-                              const double *, int);
+                              const float *, int);
 struct SrbGrid;
 extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const double *obstacles, int n_obs,
                                           const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
@@ -114,7 +114,7 @@ struct srb_ctx {
     int last_nw;
     int nw;                        // waves per agent forced by srb_ctx_set_waves (0: automatic)
     int qp_init;                   // QP starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT
-    double *zpol;                  // [max_agents][zstride] NLP active set / multipliers for the polish kernel
+    float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
     float polish_ms;
     // selection grids (table 0: static obstacles, 1: neighbour snapshot), rebuilt per launch
@@ -309,7 +309,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     HIPCHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
     HIPCHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
     HIPCHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
-    HIPCHK(hipMalloc(&c->zpol, A * (size_t)c->zstride * sizeof(double)));
+    HIPCHK(hipMalloc(&c->zpol, A * (size_t)c->zstride * sizeof(float)));
     *out = c;
     return SRB_OK;
 }
@@ -408,7 +408,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (polish) {
         hipLaunchKernelGGL(in->polish, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot,
                            d->obstacles, d->nbr_state, d->x, d->obj, d->status, d->alpha ? d->alpha_buf : nullptr,
-                           d->alpha_buf ? d->alpha : nullptr, (const int *)sel, (const double *)c->zpol, c->zstride);
+                           d->alpha_buf ? d->alpha : nullptr, (const int *)sel, (const float *)c->zpol, c->zstride);
         HIPCHK(hipGetLastError());
     }
     HIPCHK(hipEventRecord(c->ev[1], s));

@@ -740,7 +740,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 double *__restrict__ x_qp_out, double *__restrict__ x_out,
                 double *__restrict__ obj_out, int *__restrict__ status_out, int *__restrict__ iters_out,
                 const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
-                const int *__restrict__ sel_g, double *__restrict__ zpol_g, int zstride, double *lds)
+                const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride, double *lds)
 {
     SRB_AGENT_LAYOUT;
 #ifdef SRB_STAMPS
@@ -958,20 +958,20 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         bool saved = false, restore = false;   // NLP: xsv holds the best near-optimal iterate
         double best_rx = 1e300;                // its dual residual / max(1, ||Q x + f||_inf)
         // the polish kernel (srb_polish_kernel, launched next) starts from the NLP result: its active
-        // set and multipliers -- rows with s * KAPPA < z keep z (in double: a multiplier rounded
-        // to float costs the Newton iteration a step), the others -min(z/s, OMCAP), their barrier
-        // weight, as a proximal term
+        // set and multipliers -- rows with s * KAPPA < z keep z (as float: the Newton iteration's
+        // starting guess, corrected by its first step; measured no different from double), the
+        // others -min(z/s, OMCAP), their barrier weight, as a proximal term
         // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
         // (the saved one on a restore)
         auto export_zpol = [&]() {
-            double *zp = zpol_g + (size_t)agent * zstride;
+            float *zp = zpol_g + (size_t)agent * zstride;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts && tid + NTH * t < S)
 #pragma unroll
                     for (int r = 0; r < 2; r++)
-                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0
-                            : Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? Q[t].z[r] : -fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP);
+                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0f
+                            : (float)(Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? Q[t].z[r] : -fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP));
         };
         for (int iter = 0; iter < maxit; iter++) {
             STAMP_BEGIN();
@@ -1286,7 +1286,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ obstacles, const double *__restrict__ nbr_state,
                 double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,
                 const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,
-                const int *__restrict__ sel_g, const double *__restrict__ zpol_g, int zstride, double *lds)
+                const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride, double *lds)
 {
     SRB_AGENT_LAYOUT;
     double *Rt = R + rC * LDR;
@@ -1298,7 +1298,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     for (int v = tid; v < n; v += NTH) { const double xv = x_out[(size_t)agent * n + v]; xs[v] = xv; xsv[v] = xv; }
     SRB_AGENT_OBSTACLES;
     SYNC();
-    const double *zp = zpol_g + (size_t)agent * zstride;
+    const float *zp = zpol_g + (size_t)agent * zstride;
     POLDBG_IN(zp, S, xs, n);
     double Mi[NZL], dxi[NZL];
     // ---------------- active-set polish of the NLP result (oracle/nlp_ipm.c `polish`, the same rules) ----------------
@@ -1330,7 +1330,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                const double v = (t < nts && sl < S) ? zp[2 * sl + r] : 0.0;
+                const double v = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
                 q.ds[r] = (v > 0.0) ? 1.0 : 0.0;
                 q.dz[r] = fmax(v, 0.0);
                 q.s[r] = fmax(-v, 0.0);
@@ -1477,7 +1477,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
         double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
         int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,       \
-        const int *__restrict__ sel_g, double *__restrict__ zpol_g, int zstride)                               \
+        const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride)                               \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
@@ -1491,7 +1491,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const double *__restrict__ footg, const double *__restrict__ obstacles,                                 \
         const double *__restrict__ nbr_state, double *__restrict__ x_out, double *__restrict__ obj_out,          \
         int *__restrict__ status_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,     \
-        const int *__restrict__ sel_g, const double *__restrict__ zpol_g, int zstride)                         \
+        const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride)                         \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
