@@ -97,14 +97,14 @@ static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
 static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
 {
-    const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZM + 1;
+    const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZL + 1;
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
     const int q = 16 * NW;
     const int rO = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + q - 1) / q * q;   // stored term rows
     const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
-    const int part = (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 3 * NZM * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
+    const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
+    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
            (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64

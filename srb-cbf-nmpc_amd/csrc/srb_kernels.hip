@@ -160,7 +160,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 {
     const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
-    constexpr int LDH = NZM + 1;
+    constexpr int LDH = NZL + 1;            // H holds rows / columns < NZL only (the rest of the tiles are 0)
     constexpr int NT = (NZM == 16) ? 1 : 3, NTC = NZM / 16;
     const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
@@ -205,19 +205,30 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     if (RHS)
 #pragma unroll
         for (int tc = 0; tc < NTC; tc++) gs[tc] = chunk_sum16(ps[tc]);
-    if constexpr (NW == 1) {
-        if (RHS)
+    if constexpr (NW <= 2) {
+        // wave 0 stores its tiles; with two waves, wave 1 then adds its own in place (a fixed
+        // order: bit-reproducible, and no partial-Gram scratch in LDS)
+        auto put = [&](int i, int j, double v, bool add) {
+            if (i < NZL && j < NZL) H[i * LDH + j] = add ? H[i * LDH + j] + v : v;
+        };
 #pragma unroll
-            for (int tc = 0; tc < NTC; tc++)
-                if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = gs[tc];
+        for (int ph = 0; ph < NW; ph++) {
+            if (ph > 0) __syncthreads();
+            if (wv == ph) {
+                if (RHS)
 #pragma unroll
-        for (int q = 0; q < 4; q++) {
-            const int r = kq + 4 * q;
-            H[r * LDH + li] = acc[0][q];
-            if constexpr (NZM == 32) {
-                H[r * LDH + 16 + li] = acc[1][q];
-                H[(16 + li) * LDH + r] = acc[1][q];
-                H[(16 + r) * LDH + 16 + li] = acc[2][q];
+                    for (int tc = 0; tc < NTC; tc++)
+                        if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = ph ? g[16 * tc + li] + gs[tc] : gs[tc];
+#pragma unroll
+                for (int q = 0; q < 4; q++) {
+                    const int r = kq + 4 * q;
+                    put(r, li, acc[0][q], ph > 0);
+                    if constexpr (NZM == 32) {
+                        put(r, 16 + li, acc[1][q], ph > 0);
+                        put(16 + li, r, acc[1][q], ph > 0);
+                        put(16 + r, 16 + li, acc[2][q], ph > 0);
+                    }
+                }
             }
         }
     } else {
@@ -237,9 +248,9 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 #pragma unroll
             for (int w2 = 0; w2 < NW; w2++) v += part[((w2 * NT + t) * 4 + q) * 64 + ln];
             const int r = (ln >> 4) + 4 * q, cl = ln & 15;
-            if (t == 0) H[r * LDH + cl] = v;
-            else if (t == 1) { H[r * LDH + 16 + cl] = v; H[(16 + cl) * LDH + r] = v; }
-            else H[(16 + r) * LDH + 16 + cl] = v;
+            if (t == 0) { if (r < NZL && cl < NZL) H[r * LDH + cl] = v; }
+            else if (t == 1) { if (16 + cl < NZL) { H[r * LDH + 16 + cl] = v; H[(16 + cl) * LDH + r] = v; } }
+            else if (16 + r < NZL && 16 + cl < NZL) H[(16 + r) * LDH + 16 + cl] = v;
         }
         if (RHS && tid < nz) {
             double v = 0.0;
@@ -294,16 +305,22 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
         const int och = nko / NW, ob = rO + wv * och;
         range(ob, ob + och, !SRB_OBS_STORED(NZL));
     }
+    double sv[NTC];
 #pragma unroll
-    for (int tc = 0; tc < NTC; tc++) {
-        const double sv = chunk_sum16(ps[0][tc] + ps[1][tc]);
-        if constexpr (NW == 1) {
-            if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = sv;
-        } else {
-            if (kq == 0) part[wv * NZM + 16 * tc + li] = sv;
+    for (int tc = 0; tc < NTC; tc++) sv[tc] = chunk_sum16(ps[0][tc] + ps[1][tc]);
+    if constexpr (NW <= 2) {
+#pragma unroll
+        for (int ph = 0; ph < NW; ph++) {       // wave 0 stores, wave 1 adds (as gram_rhs)
+            if (ph > 0) __syncthreads();
+            if (wv == ph)
+#pragma unroll
+                for (int tc = 0; tc < NTC; tc++)
+                    if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = ph ? g[16 * tc + li] + sv[tc] : sv[tc];
         }
-    }
-    if constexpr (NW > 1) {
+    } else {
+#pragma unroll
+        for (int tc = 0; tc < NTC; tc++)
+            if (kq == 0) part[wv * NZM + 16 * tc + li] = sv[tc];
         __syncthreads();
         if (tid < nz) {
             double v = 0.0;
@@ -334,7 +351,7 @@ __device__ __forceinline__ int mrow(int lane) { return (NZL <= 16 && SRB_USE_DPP
 template <int NZL>
 __device__ __forceinline__ void gj_load(double (&A)[NZL], const double *H, const double *ZtZ, double delta, int nz, int lane)
 {
-    constexpr int LDH = ((NZL + 15) / 16) * 16 + 1;
+    constexpr int LDH = NZL + 1;
     lane = mrow<NZL>(lane);
     const int i = (lane < NZL) ? lane : 0;
 #pragma unroll
@@ -366,15 +383,15 @@ __device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, in
 #define gj_reduced gj_invert
 #endif
 
-// Newton solve in the reduced space: out = Hs^-1 g with one step of iterative refinement
+// Newton solve in the reduced space: out = (Hs + dl Zs)^-1 g with one step of iterative refinement
 // (y = M g; y += M (g - Hs y)): the explicit inverse alone is not backward stable, and near
 // the end of an interior-point solve Hs carries barrier weights of 1e8..1e12.
 // g, y, r, out: LDS vectors (zero beyond nz).  Returns out in registers (uniform).
 template <int NZL>
-__device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *Hs, const double *g, double *y,
-                                         double *r, double *out, double (&res)[NZL], int nz, int lane)
+__device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *Hs, const double *Zs, double dl, const double *g,
+                                         double *y, double *r, double *out, double (&res)[NZL], int nz, int lane)
 {
-    constexpr int LDH = ((NZL + 15) / 16) * 16 + 1;
+    constexpr int LDH = NZL + 1;
     if constexpr (NZL <= 16 && SRB_USE_DPP) {
         // rows replicated per 16-lane row: the three vector broadcasts are DPP moves, no LDS
         // round trip or barrier
@@ -389,8 +406,13 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
 #pragma unroll
         for (int it = 0; it < SRB_REFINE; it++) {
             double rr = gi;
+            if (dl != 0.0) {                 // the NLP's inertia shift, applied on the fly (H stays unshifted)
 #pragma unroll
-            for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y1, j), rr);
+                for (int j = 0; j < NZL; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), bc16(y1, j), rr);
+            } else {
+#pragma unroll
+                for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y1, j), rr);
+            }
             if (i >= nz) rr = 0.0;
 #pragma unroll
             for (int j = 0; j < NZL; j++) y1 = fma(M[j], bc16(rr, j), y1);
@@ -412,8 +434,13 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         if (lane < nz) y[lane] = y1;
         SYNC();
         double rr = (lane < nz) ? g[lane] : 0.0;
+        if (dl != 0.0) {
 #pragma unroll
-        for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
+            for (int j = 0; j < NZL; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), y[j], rr);
+        } else {
+#pragma unroll
+            for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
+        }
         if (lane < nz) r[lane] = rr;
         SYNC();
 #pragma unroll
@@ -594,7 +621,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
 //   SRB_AGENT_OUTPUTS    x, objective, alpha_COM
 #define SRB_AGENT_LAYOUT \
     constexpr int NZM = ((NZL + 15) / 16) * 16; \
-    constexpr int LDR = NZL + 1, LDH = NZM + 1; \
+    constexpr int LDR = NZL + 1, LDH = NZL + 1; \
     constexpr int NTH = 64 * NW; \
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6; \
     const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz; \
@@ -614,9 +641,8 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     double *W = p; p += TT + 1;                   /* gram weights (+ one scratch entry) */ \
     double *CF = p; p += TT + 1;                  /* rhs coefficients (+ one scratch entry) */ \
     double *OJ = p; p += SRB_OBS_STORED(NZL) ? 0 : 2 * NKP;   /* generated obstacle terms: jx, jy (gram_rhs) */ \
-    double *H0 = p; p += NZM * LDH;               /* assembled Z'HZ (delta = 0) */ \
-    double *HS = p; p += NZM * LDH;               /* Z'HZ + delta Z'Z (when delta != 0) */ \
-    double *ZZ = p; p += NZM * LDH;               /* Z'Z (NLP) */ \
+    double *H0 = p; p += NZL * LDH;               /* assembled Z'HZ (unshifted; + delta Z'Z on the fly) */ \
+    double *ZZ = p; p += NZL * LDH;               /* Z'Z (NLP) */ \
     double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM; \
     double *xs = p; p += n4; \
     double *xb = p; p += n4; \
@@ -629,7 +655,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     double *dpos = p; p += 2 * N + 1;             /* Z_x dxi, Z_y dxi per grid, dxi_s (obstacle J dx) */ \
     int *sel = (int *)p; p += (K + 1); \
     double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
-    double *part = p; p += (NW > 1) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs */ \
+    double *part = p; p += (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs (NW = 4) */ \
     do {} while (0)
 
 #define SRB_AGENT_SETUP \
@@ -809,7 +835,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 qp_flag = 1;                                  // x stays xbar (last iterate is returned)
                 continue;
             }
-            la_solve<NZL>(Mi, H0, vg, vy, vr, vd, dxi, nz, lane);
+            la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
             // x = xbar + Z xi ; zi = h - G x ; s, z shifted (Auxilary.c:716-746)
             double mn = 1e300, mx = -1e300;
 #pragma unroll
@@ -936,7 +962,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_reduced<NZL>(Mi, nz, lane, 0);
-            la_solve<NZL>(Mi, ZZ, vg, vy, vr, vd, dxi, nz, lane);
+            la_solve<NZL>(Mi, ZZ, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
@@ -1108,13 +1134,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         const double dm = (lane < nz) ? H0[lane * LDH + lane] : 1.0;
                         dstart = 1e-10 * fmax(1.0, wmax(dm));
                     }
-                    gj_load<NZL>(Mi, H0, ZZ, delta, nz, lane);
-                    if (delta != 0.0) {
-                        if (lane < nz)
-#pragma unroll
-                            for (int j = 0; j < NZL; j++) HS[lane * LDH + j] = Mi[j];
-                        SYNC();
-                    }
+                    gj_load<NZL>(Mi, H0, ZZ, delta, nz, lane);    // H0 + delta Z'Z (the solves shift on the fly too)
                     const int cf = gj_reduced<NZL>(Mi, nz, lane, !nl);
                     if (cf == 0) { ok = 1; break; }
                     delta = (delta == 0.0) ? dstart : delta * 10.0;
@@ -1123,7 +1143,6 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 if (!ok) { flag = 1; break; }
                 if (near && delta != 0.0) { flag = 4; break; }
             }
-            const double *Hsv = (delta != 0.0) ? HS : H0;
 
             // ---- predictor (pc) or centring step (Prime.c:193-196), then corrector
             double ap = 1.0, ad = 1.0;
@@ -1137,7 +1156,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
-                la_solve<NZL>(Mi, Hsv, vg, vy, vr, vd, dxi, nz, lane);
+                la_solve<NZL>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
@@ -1290,7 +1309,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
 {
     SRB_AGENT_LAYOUT;
     double *Rt = R + rC * LDR;
-    (void)HS; (void)xb; (void)th; (void)tol; (void)wv;
+    (void)xb; (void)th; (void)tol; (void)wv;
     const int st1 = status_out[2 * agent + 1];
     if (!prm.use_nlp || st1 == 1 || st1 == 3) return;          // the whole workgroup: no usable iterate to polish
     SRB_AGENT_SETUP;
@@ -1379,7 +1398,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);
                 gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
                 if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; }      // not PD: reject
-                la_solve<NZL>(Mi, H0, vg, vy, vr, vd, dxi, nz, lane);
+                la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
                 double mdx = 0.0;
 #pragma unroll
                 for (int t = 0; t < TS; t++)

@@ -1,7 +1,9 @@
 """Diagnostic: per-iteration NLP trace of chosen agents of a bench configuration's batch
 (libsrbnmpc_nlpdbg.so, make -C srb-cbf-nmpc_amd nlpdbg).
 
-    python tools/nlp_trace.py config agent [agent ...]"""
+    python tools/nlp_trace.py config agent [agent ...]
+    NLPTRACE_SPEC="N C K_obs K_nbr agents seed" python tools/nlp_trace.py custom agent ...
+    (NLPTRACE_WAVES forces the waves per agent)"""
 import ctypes
 import os
 import sys
@@ -15,12 +17,18 @@ import srbnmpc  # noqa: E402
 from srbnmpc import workload  # noqa: E402
 
 srbnmpc.LIB_PATH = os.path.join(os.path.dirname(srbnmpc.__file__), "libsrbnmpc_nlpdbg.so")
-c = int(sys.argv[1])
-cfg = bench.CONFIGS[c]
-A, N, C = cfg["agents"], cfg["N"], cfg["C"]
+if sys.argv[1] == "custom":     # NLPTRACE_SPEC="N C K_obs K_nbr agents seed" (workload.make_batch)
+    N, C, Ko, Kn, A, seed = map(int, os.environ["NLPTRACE_SPEC"].split())
+    cfg = dict(N=N, C=C, K_obs=Ko, K_nbr=Kn, agents=A)
+    b = workload.make_batch(A, N, C, seed=seed)
+else:
+    c = int(sys.argv[1])
+    cfg = bench.CONFIGS[c]
+    A, N, C = cfg["agents"], cfg["N"], cfg["C"]
+    A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
-A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 s = srbnmpc.BatchSolver(p, A)
+s.set_waves(int(os.environ.get("NLPTRACE_WAVES", "0")))
 L = srbnmpc.lib()
 L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
 buf = np.zeros(8 * 64 + 32 * 32 + 32 + 1024 + 256 + 3 * 256)
