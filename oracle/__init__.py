@@ -322,3 +322,52 @@ def ll_calc_torque(p: OrcLLParams, batch: dict, nthreads: int = 1):
                                    _ptr(out["V"]), _ptr(out["dV"]), _ptr(out["x"]), _ptr(out["status"]),
                                    _ptr(out["iters"]))
     return out
+
+
+# ------------------------------------------------------------------ SRB-12 extension mode (srb12.c)
+class Orc12Params(ctypes.Structure):
+    _fields_ = [("N", ctypes.c_int), ("K_obs", ctypes.c_int), ("K_nbr", ctypes.c_int),
+                ("Ts", ctypes.c_double), ("mass", ctypes.c_double), ("Ib", ctypes.c_double * 9),
+                ("grav", ctypes.c_double), ("mu", ctypes.c_double), ("fmax", ctypes.c_double),
+                ("q", ctypes.c_double * 12), ("qN", ctypes.c_double * 12), ("r", ctypes.c_double * 3),
+                ("Sw", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
+                ("tol", ctypes.c_double), ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int),
+                ("use_nlp", ctypes.c_int), ("z0", ctypes.c_double)]
+
+
+def params12(N: int = 10, **kw) -> Orc12Params:
+    """SRB-12 parameters (srb12.c header: constants of fast_MPC.cpp:40-43, Parameters.cpp:32-52)."""
+    p = Orc12Params()
+    lib().orc12_params_default(ctypes.byref(p), N)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    return p
+
+
+def nv12(p: Orc12Params) -> int:
+    return 24 * p.N + 1
+
+
+def dynamics12(p: Orc12Params, x0, xref, foot, contact):
+    """Per-stage A_k, B_k (N, 12, 12) and c_k (N, 12) of the SRB-12 linearisation."""
+    N = p.N
+    A = np.zeros((N, 12, 12)); B = np.zeros((N, 12, 12)); c = np.zeros((N, 12))
+    lib().orc12_dynamics(ctypes.byref(p), _ptr(_c(x0)), _ptr(_c(xref)), _ptr(_c(foot)), _ptr(_c(contact, np.int32)),
+                         _ptr(A), _ptr(B), _ptr(c))
+    return A, B, c
+
+
+def solve_batch12(p: Orc12Params, x0, xref, foot, contact, obstacles=None, nbr_state=None, agent_offset=0,
+                  nthreads=8):
+    """SRB-12 solves of a batch: x0 [A,12], xref [A,N,12], foot [A,N,4,3], contact [A,N,4] int.
+    Returns x_qp, x [A, 24N+1], obj, status [A,2], iters [A,2]."""
+    x0 = _c(x0); A_ = x0.shape[0]; nv = nv12(p)
+    ob = _c(obstacles if obstacles is not None else np.zeros((0, 2)))
+    nb = _c(nbr_state) if nbr_state is not None else None
+    out = dict(x_qp=np.zeros((A_, nv)), x=np.zeros((A_, nv)), obj=np.zeros(A_),
+               status=np.zeros((A_, 2), np.int32), iters=np.zeros((A_, 2), np.int32))
+    lib().orc12_solve_batch(ctypes.byref(p), A_, _ptr(x0), _ptr(_c(xref)), _ptr(_c(foot)), _ptr(_c(contact, np.int32)),
+                            _ptr(ob), ob.shape[0], _ptr(nb) if nb is not None else None,
+                            nb.shape[0] if nb is not None else 0, int(agent_offset), _ptr(out["x_qp"]), _ptr(out["x"]),
+                            _ptr(out["obj"]), _ptr(out["status"]), _ptr(out["iters"]), int(nthreads))
+    return out

@@ -171,6 +171,28 @@ int orc_ll_calc_torque_batch_mt(const orc_ll_params *prm, int nthreads, int n_ag
                                 double *dq_out, double *q_out, double *V, double *dV, double *x, int *status,
                                 int *iters);
 
+/* ---- SRB-12 extension mode (srb12.c; the north star's 12-state SRB model, declared but never
+ * implemented by the reference, include/fast_MPC.hpp:98-103: parity unpinned) */
+typedef struct orc12_params {
+    int N, K_obs, K_nbr;
+    double Ts, mass, Ib[9], grav, mu, fmax;
+    double q[12], qN[12], r[3], Sw;     /* stage / terminal state weights, force weights, slack weight */
+    double eps_obs, eps_nbr, tol;
+    int qp_maxit, nlp_maxit, use_nlp;
+    double z0;                          /* NLP initial duals z0 / max(s, 1) */
+} orc12_params;
+
+void orc12_params_default(orc12_params *p, int N);
+int orc12_nv(const orc12_params *p);   /* 24N + 1: X (12N) | U (12N) | s */
+void orc12_dynamics(const orc12_params *p, const double x0[12], const double *xref, const double *foot,
+                    const int *contact, double *A, double *B, double *c);
+int orc12_solve_agent(const orc12_params *p, const double x0[12], const double *xref, const double *foot,
+                      const int *contact, const double *obstacles, int n_obs, const double *nbr_state, int n_all,
+                      int self_idx, double *x_qp, double *x_out, double *obj, int status[2], int iters[2]);
+int orc12_solve_batch(const orc12_params *p, int n_agents, const double *x0, const double *xref, const double *foot,
+                      const int *contact, const double *obstacles, int n_obs, const double *nbr_state, int n_all,
+                      int agent_offset, double *x_qp, double *x_out, double *obj, int *status, int *iters, int nthreads);
+
 /* dense helpers (linalg.c) */
 int orc_chol(int n, double *A);                               /* in place, lower */
 void orc_chol_solve(int n, const double *L, double *x);

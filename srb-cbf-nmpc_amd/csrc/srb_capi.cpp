@@ -406,7 +406,17 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     HIPCHK(hipGetLastError());
     HIPCHK(hipEventRecord(c->ev[3], s));
     if (polish) {
-        hipLaunchKernelGGL(in->polish, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot,
+        // the polish kernel reads only the solve's outputs (x, status, sel, zpol by global slot
+        // index), so it runs at its own waves per agent: at least two (its registers fit two
+        // waves per SIMD, and a polish step's latency halves): configs[2] polish 0.067 -> 0.053 ms,
+        // configs[1] (solve at 4 waves) and N = 20 (2 waves) unchanged, one wave slower everywhere
+        // (profiles/r03_polish_nw_ab.txt).  SRB_POLISH_NW = 1 | 2 | 4 overrides (tuning).
+        static const int pnw_env = [] { const char *e = std::getenv("SRB_POLISH_NW"); return e ? std::atoi(e) : 0; }();
+        const int pnw = (pnw_env == 1 || pnw_env == 2 || pnw_env == 4) ? pnw_env : (in->nw < 2 ? 2 : in->nw);
+        const srb_instance *pin = pnw == in->nw ? in : pick_instance(k, pnw);
+        if (!pin || pin->nzl != in->nzl) pin = in;
+        const size_t plds = (size_t)srb_lds_doubles(k, pin->nzl, pin->nw) * sizeof(double);
+        hipLaunchKernelGGL(pin->polish, dim3(n_agents), dim3(64 * pin->nw), plds, s, k, n_agents, d->x0, d->ref, d->foot,
                            d->obstacles, d->nbr_state, d->x, d->obj, d->status, d->alpha ? d->alpha_buf : nullptr,
                            d->alpha_buf ? d->alpha : nullptr, (const int *)sel, (const float *)c->zpol, c->zstride);
         HIPCHK(hipGetLastError());

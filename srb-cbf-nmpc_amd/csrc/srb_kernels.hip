@@ -662,9 +662,11 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     const double *x0 = x0g + 4 * (size_t)agent; \
     for (int i = tid; i < 4 * N; i += NTH) ref[i] = refg[(size_t)agent * 4 * N + i]; \
     for (int i = tid; i < 2 * C * N; i += NTH) foot[i] = footg[(size_t)agent * 2 * C * N + i]; \
+    if (prm.use_nlp && tid < K) sel[tid] = sel_g[(size_t)agent * K + tid]; \
     for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0; \
     for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0; \
     SYNC(); \
+    if (prm.use_nlp) { SRB_AGENT_OBSTACLES; } \
     /* null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261) */ \
     if (tid == 0) { \
         double X[4] = {x0[0], x0[1], x0[2], x0[3]}; \
@@ -710,21 +712,30 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     do {} while (0)
 
 #define SRB_AGENT_OBSTACLES \
-            if (tid < K) sel[tid] = sel_g[(size_t)agent * K + tid]; \
-            SYNC(); \
-            for (int j = 0; j < K; j++) { \
+    /* every (grid k, row j) pair on its own lane, all loads of a lane issued before its stores */ \
+    { \
+        double ox_[TS], oy_[TS]; \
+        _Pragma("unroll") for (int t = 0; t < TS; t++) { \
+            const int e = tid + NTH * t; \
+            ox_[t] = oy_[t] = 0.0; \
+            if (e < NK) { \
+                const int k = e / K, j = e - k * K; \
                 const bool st = j < prm.K_obs; \
                 const int bi = sel[j]; \
-                if (tid < N) {         /* no selection (-1): a row 1000 m along +x, as the oracle */ \
-                    const int k = tid; \
-                    const double tt = st ? 0.0 : prm.Ts * (k + 1); \
-                    const size_t bj = (bi >= 0) ? bi : 0; \
-                    const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj; \
-                    obs[2 * (k * K + j)] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0; \
-                    obs[2 * (k * K + j) + 1] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2]; \
-                } \
-                if (tid == 0) eps[j] = st ? prm.eps_obs : prm.eps_nbr; \
+                const double tt = st ? 0.0 : prm.Ts * (k + 1); \
+                const size_t bj = (bi >= 0) ? bi : 0; \
+                const double *srcp = st ? obstacles + 2 * bj : nbr_state + 4 * bj; \
+                /* no selection (-1): a row 1000 m along +x, as the oracle */ \
+                ox_[t] = (bi >= 0) ? srcp[0] + (st ? 0.0 : srcp[2] * tt) : x0[0] + 1000.0; \
+                oy_[t] = (bi >= 0) ? srcp[1] + (st ? 0.0 : srcp[3] * tt) : x0[2]; \
             } \
+        } \
+        _Pragma("unroll") for (int t = 0; t < TS; t++) { \
+            const int e = tid + NTH * t; \
+            if (e < NK) { obs[2 * e] = ox_[t]; obs[2 * e + 1] = oy_[t]; } \
+        } \
+        if (tid < K) eps[tid] = (tid < prm.K_obs) ? prm.eps_obs : prm.eps_nbr; \
+    } \
     do {} while (0)
 
 #define SRB_AGENT_OUTPUTS \
@@ -904,8 +915,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             // generalised to K) and the K_nbr nearest other agents (get_lastState() rows),
             // predicted at constant velocity o_k = p + v Ts (k+1); query point = own CoM.
             // (selected by srb_knn_kernel, launched just before this kernel on the same stream)
-            SRB_AGENT_OBSTACLES;
-            STAMP_END(6);                                     // NLP slot 6: neighbour selection (+ positions)
+            STAMP_END(6);                                     // NLP slot 6 (obstacle positions: loaded in the setup)
             SYNC();
             // slacks: shifted h - g(x) over every NLP row; duals 1
             const double s_var = xs[n - 1];
@@ -1312,12 +1322,21 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     (void)xb; (void)th; (void)tol; (void)wv;
     const int st1 = status_out[2 * agent + 1];
     if (!prm.use_nlp || st1 == 1 || st1 == 3) return;          // the whole workgroup: no usable iterate to polish
+    // the solve's outputs first (x into xsv, which the setup does not clear; the exported active set
+    // / multipliers into registers), so their HBM latency overlaps the setup
+    const float *zp = zpol_g + (size_t)agent * zstride;
+    float zv[TS][2];
+#pragma unroll
+    for (int t = 0; t < TS; t++) {
+        const int sl = tid + NTH * t;
+#pragma unroll
+        for (int r = 0; r < 2; r++) zv[t][r] = (sl < S) ? zp[2 * sl + r] : 0.0f;
+    }
+    for (int v = tid; v < n; v += NTH) xsv[v] = x_out[(size_t)agent * n + v];
     SRB_AGENT_SETUP;
     SYNC();
-    for (int v = tid; v < n; v += NTH) { const double xv = x_out[(size_t)agent * n + v]; xs[v] = xv; xsv[v] = xv; }
-    SRB_AGENT_OBSTACLES;
+    for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];
     SYNC();
-    const float *zp = zpol_g + (size_t)agent * zstride;
     POLDBG_IN(zp, S, xs, n);
     double Mi[NZL], dxi[NZL];
     // ---------------- active-set polish of the NLP result (oracle/nlp_ipm.c `polish`, the same rules) ----------------
@@ -1349,7 +1368,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
 #pragma unroll
             for (int r = 0; r < 2; r++) {
-                const double v = (t < nts && sl < S) ? (double)zp[2 * sl + r] : 0.0;
+                const double v = (t < nts && sl < S) ? (double)zv[t][r] : 0.0;
                 q.ds[r] = (v > 0.0) ? 1.0 : 0.0;
                 q.dz[r] = fmax(v, 0.0);
                 q.s[r] = fmax(-v, 0.0);

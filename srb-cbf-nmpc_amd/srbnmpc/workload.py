@@ -74,3 +74,56 @@ def make_batch(n_agents: int, N: int = 10, C: int = 2, seed: int = 0, n_obs: int
     obstacles = make_obstacles(rng, n_obs, sc)
     nbr_state = np.stack([x0[:, 0], x0[:, 2], x0[:, 1], x0[:, 3]], 1)
     return dict(x0=x0, ref=ref.reshape(A, 4 * N), foot=foot, obstacles=obstacles, nbr_state=nbr_state)
+
+
+HCOM12 = 0.3      # SRB-12 mode: nominal CoM height of the synthetic batches
+
+
+def make_batch12(n_agents: int, N: int = 10, gait: str = "trot", seed: int = 0, n_obs: int | None = None):
+    """SRB-12 extension mode: the LIP batch's arena, starts, goal, obstacles
+    and trot schedule, lifted to the 12-state single rigid body.  Returns dict(x0 [A,12],
+    xref [A,N,12] (states x_1..x_N), foot [A,N,4,3] (world foot positions per grid),
+    contact [A,N,4] int32, obstacles [n_obs,2], nbr_state [A,4] (x, y, xdot, ydot))."""
+    rng = np.random.default_rng(seed)
+    A = int(n_agents)
+    sc = arena_scale(A)
+    if n_obs is None:
+        n_obs = int(round(20 * sc * sc))
+    p0 = np.stack([rng.uniform(0, 9.0 * sc, A), rng.uniform(-2.0 * sc, 2.0 * sc, A)], 1)
+    goal = GOAL * np.array([sc, 1.0])
+    d = goal - p0
+    d /= np.linalg.norm(d, axis=1, keepdims=True)
+    head = np.arctan2(d[:, 1], d[:, 0])
+    v0 = d * rng.uniform(0, 0.3, (A, 1)) + rng.uniform(-0.05, 0.05, (A, 2))
+    x0 = np.zeros((A, 12))
+    x0[:, 0:2] = p0
+    x0[:, 2] = HCOM12 + rng.uniform(-0.01, 0.01, A)
+    x0[:, 3:5] = rng.uniform(-0.02, 0.02, (A, 2))
+    x0[:, 5] = head + rng.uniform(-0.1, 0.1, A)
+    x0[:, 6:8] = v0
+    x0[:, 9:12] = rng.uniform(-0.05, 0.05, (A, 3))
+    k = np.arange(1, N + 1)
+    xref = np.zeros((A, N, 12))
+    xref[:, :, 0] = p0[:, None, 0] + d[:, None, 0] * VREF * TS * k
+    xref[:, :, 1] = p0[:, None, 1] + d[:, None, 1] * VREF * TS * k
+    xref[:, :, 2] = HCOM12
+    xref[:, :, 5] = head[:, None]
+    xref[:, :, 6] = d[:, None, 0] * VREF
+    xref[:, :, 7] = d[:, None, 1] * VREF
+    foot = np.zeros((A, N, 4, 3))
+    contact = np.zeros((A, N, 4), np.int32)
+    phase = rng.integers(0, 4, A)
+    c, s = np.cos(head), np.sin(head)
+    for a in range(A):
+        Rm = np.array([[c[a], -s[a]], [s[a], c[a]]])
+        off = (Rm @ STANCE).T                                   # (4, 2) stance offsets along the heading
+        for kk in range(N):
+            dom = (kk + phase[a]) // 4
+            k_start = max(4 * dom - phase[a], 0)
+            centre = p0[a] + d[a] * VREF * TS * k_start
+            foot[a, kk, :, :2] = centre[None, :] + off
+            legs = TROT_PAIRS[dom % 2] if gait == "trot" else [0, 1, 2, 3]
+            contact[a, kk, legs] = 1
+    obstacles = make_obstacles(rng, n_obs, sc)
+    nbr_state = np.stack([x0[:, 0], x0[:, 1], x0[:, 6], x0[:, 7]], 1)
+    return dict(x0=x0, xref=xref, foot=foot, contact=contact, obstacles=obstacles, nbr_state=nbr_state)
