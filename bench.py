@@ -235,6 +235,119 @@ def main_ll(args, world, rank, local_rank, dev):
     ctrl.close()
 
 
+def srb12_executed_flops(N, K, iters):
+    """Executed fp64 flops of the SRB-12 Riccati interior-point method per solve, summed over the
+    batch: per iteration the backward factorisation (G, F, Hux, A'G by their
+    structure ~ 3 x 13^2 x 8, B'F 12^2 x 8, the 12 x 12 Gauss-Jordan 2 x 12^3, the two 16x16x16
+    MFMA products 2 x 2 x 16^3) per grid, four Riccati vector solves (predictor, corrector, their
+    refinements: ~ 2 x (12 x 12 + 13 x 12) x 2 + 300 per grid each) and the row work (~40 per row)."""
+    fac = 3 * 169 * 8 + 144 * 8 + 2 * 12 ** 3 + 2 * 2 * 16 ** 3
+    sol = 2 * (144 + 156) * 2 + 300
+    rows = 40 * (24 * N + N * K)
+    it = N * (fac + 4 * sol) + rows
+    return float(np.sum(iters.sum(1) * it))
+
+
+def main_srb12(args, world, rank, local_rank, dev):
+    """SRB-12 extension mode: the north star's 12-state SRB NMPC on the
+    configs[2]-shaped swarm (1024 agents per GPU, N = 10, trot, 3 static + 8 neighbour rows);
+    its own line, not the headline."""
+    from srbnmpc import srb12
+    A_local = args.agents or 1024
+    A_total = A_local * world
+    N, Ko_, Kn_ = 10, 3, 8
+    b = workload.make_batch12(A_total, N, "trot", seed=1234)
+    lo, hi = sdist.shard_range(A_total, world, rank)
+    n_loc = hi - lo
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    x0, xref, foot = T(b["x0"][lo:hi]), T(b["xref"][lo:hi]), T(b["foot"][lo:hi])
+    contact, obst = T(b["contact"][lo:hi], torch.int32), T(b["obstacles"])
+    nbr_all = T(b["nbr_state"])
+    nbr_local = nbr_all[lo:hi].contiguous()
+    prm = srb12.default_params(N, K_obs=Ko_, K_nbr=Kn_)
+    solver = srb12.Solver12(prm, n_loc, local_rank)
+    Ko, Kn = srb12.n_selected(prm, obst.shape[0], A_total)
+    out = dict(x_qp=None, x=torch.zeros((n_loc, prm.nv), dtype=torch.float64, device=dev),
+               obj=torch.zeros(n_loc, dtype=torch.float64, device=dev),
+               status=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
+               iters=torch.zeros((n_loc, 2), dtype=torch.int32, device=dev),
+               sel=torch.zeros((n_loc, Ko + Kn), dtype=torch.int32, device=dev))
+    stream = torch.cuda.Stream(dev)
+    torch.cuda.set_stream(stream)
+    exchange = sdist.NeighbourExchange(A_total, world, rank, dev) if world > 1 else None
+
+    def step():
+        nb = exchange(nbr_local) if exchange is not None else nbr_all
+        solver.solve_device(x0, xref, foot, contact, obst, nb, out, agent_offset=lo, stream=stream.cuda_stream,
+                            obstacles_version=1)
+
+    for _ in range(args.warmup):
+        step()
+    torch.cuda.synchronize(dev)
+    kern = []
+    for _ in range(3):
+        step()
+        kern.append(solver.last_kernel_ms())
+    ev = [(torch.cuda.Event(enable_timing=True), torch.cuda.Event(enable_timing=True)) for _ in range(args.steps)]
+    if world > 1:
+        dist.barrier()
+    torch.cuda.synchronize(dev)
+    t0 = time.perf_counter()
+    for i in range(args.steps):
+        ev[i][0].record(stream)
+        step()
+        ev[i][1].record(stream)
+    torch.cuda.synchronize(dev)
+    if world > 1:
+        dist.barrier()
+    elapsed = time.perf_counter() - t0
+    per_step = np.array([a.elapsed_time(bb) for a, bb in ev])
+    if world > 1:
+        tt = torch.tensor([elapsed], dtype=torch.float64, device=dev)
+        dist.all_reduce(tt, op=dist.ReduceOp.MAX)
+        elapsed = float(tt.item())
+    status = out["status"].cpu().numpy(); iters = out["iters"].cpu().numpy()
+    sel_ms = float(np.median([k[0] for k in kern])); solve_ms = float(np.median([k[1] for k in kern]))
+    flops = srb12_executed_flops(N, Ko + Kn, iters)
+    achieved = flops / (solve_ms * 1e-3) / 1e12
+    io = n_loc * 8 * (12 + 24 * N + 12 * N + (24 * N + 1) + 1) + n_loc * 4 * (4 * N + 4)
+    line = {
+        "metric": "SRB-12 NMPC solves/sec (extension mode, DESIGN.md section 11)", "value": A_total * args.steps / elapsed,
+        "unit": "solves/s", "n_gpus": world, "steps": args.steps, "warmup": args.warmup,
+        "ms_per_step": elapsed * 1e3 / args.steps, "higher_is_better": True, "scaling": "weak", "vs_baseline": None,
+        "dtype": "f64", "data": "synthetic",
+        "config": {"workload": f"{A_local} agents/GPU, 12-state SRB, horizon {N}, trot, 3 static + 8-nearest "
+                               "inter-agent CBF, fp64", "agents_per_gpu": A_local, "agents_total": A_total,
+                   "parallelism": f"agents sharded x{world}"},
+        "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
+        "optimal_frac": float((status == 0).all(1).mean()), "iters_mean": iters.mean(0).tolist(),
+        "iters_max": iters.max(0).tolist(),
+        "roofline": {"bound": "mfma", "limiter": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "srb12_kernel",
+                     "kernel_ms": solve_ms, "select_ms": sel_ms, "io_bytes_per_launch": io,
+                     "flop_model": "bench.srb12_executed_flops (Riccati IPM, DESIGN.md 11); latency-bound"},
+        "cpu_baseline": None,
+    }
+    if rank == 0 and world == 1 and not args.no_cpu_baseline:
+        sys.path.insert(0, ROOT)
+        import oracle
+        op = oracle.params12(N, K_obs=Ko_, K_nbr=Kn_)
+        nthreads = host_threads()
+        t1 = time.perf_counter(); n = 0
+        while time.perf_counter() - t1 < args.cpu_seconds:
+            sl = slice(n % A_total, n % A_total + 32)
+            oracle.solve_batch12(op, b["x0"][sl], b["xref"][sl], b["foot"][sl], b["contact"][sl], b["obstacles"],
+                                 b["nbr_state"], agent_offset=sl.start, nthreads=nthreads)
+            n += b["x0"][sl].shape[0]
+        dt = time.perf_counter() - t1
+        line["cpu_baseline"] = {"value": n / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
+                                "sample": f"{n} solves (32-agent slices of the same batch) in {dt:.1f} s, "
+                                          f"oracle/srb12.c (dense full-space LU), {nthreads} threads"}
+    if rank == 0:
+        print(json.dumps(line), flush=True)
+    solver.close()
+
+
 def rank_batch(config, agents_per_gpu, world, rank, seed=1234):
     """The swarm of a `world`-GPU run of `config` and this rank's block of it: (A_total, the whole
     batch as host arrays, lo, hi).  Every rank generates the whole swarm identically and keeps
@@ -285,7 +398,7 @@ def plumbing(args, world, rank):
 
 def main():
     ap = argparse.ArgumentParser()
-    ap.add_argument("--path", choices=["nmpc", "ll"], default="nmpc")
+    ap.add_argument("--path", choices=["nmpc", "ll", "srb12"], default="nmpc")
     ap.add_argument("--gpus", type=int, default=1)
     ap.add_argument("--steps", type=int, default=50)
     ap.add_argument("--warmup", type=int, default=5)
@@ -324,8 +437,8 @@ def main():
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))
     torch.cuda.set_device(local_rank)
     dev = torch.device("cuda", local_rank)
-    if args.path == "ll":
-        main_ll(args, world, rank, local_rank, dev)
+    if args.path in ("ll", "srb12"):
+        (main_ll if args.path == "ll" else main_srb12)(args, world, rank, local_rank, dev)
         if world > 1:
             dist.destroy_process_group()
         return

@@ -284,6 +284,55 @@ int srb_ll_sync(srb_ll_ctx *ctx);
 /* HIP-event time of the last srb_ll_calc_torque[_device] kernel on its stream (ms) */
 int srb_ll_last_kernel_ms(srb_ll_ctx *ctx, float *ms);
 
+/* ================================================================ SRB-12 extension mode
+ * The north star's 12-state single-rigid-body NMPC (state [p, roll/pitch/yaw, v, omega], inputs the
+ * four leg forces, friction pyramid + f_z <= fmax, the obstacle rows of the LIP mode).  The
+ * reference DECLARES this solver (FastMPC::runMPC / MPC_Cost / MPC_Constraints /
+ * getLinearDynamics, include/fast_MPC.hpp:98-103) without implementing it, so these entry points
+ * replace no reference binding; the problem is stated in DESIGN.md section 11, the CPU checker is
+ * oracle/srb12.c (parity with the reference unpinned).  Constants: mass and inertia of FastMPC
+ * (src/fast_MPC.cpp:40-43), weights and mu_MPC of the default mpc_params (src/Parameters.cpp:32-52).
+ */
+typedef struct srb12_params {
+    int N, K_obs, K_nbr;          /* grids (<= 24), nearest static obstacles / neighbours (each <= 16) */
+    double Ts, mass, Ib[9], grav, mu, fmax;
+    double q[12], qN[12], r[3], Sw;     /* stage / terminal state weights, force weights (per axis), slack */
+    double eps_obs, eps_nbr, tol;
+    int qp_maxit, nlp_maxit, use_nlp;
+    double z0;                    /* NLP initial duals z0 / max(s, 1) */
+} srb12_params;
+
+void srb12_params_default(srb12_params *p, int N);
+int srb12_nv(const srb12_params *p);   /* 24N + 1: X = x_1..x_N (12N) | U = u_0..u_{N-1} (12N) | s */
+
+/* Batch buffers, agent-major fp64 (int32 where noted):
+ *   x0 [A][12]; xref [A][N][12] (x_1..x_N); foot [A][N][4][3] (world foot positions per grid, legs FR FL
+ *   RR RL); contact [A][N][4] int (1 stance); obstacles / nbr_state / n_obs / n_all / agent_offset /
+ *   sel / obstacles_version as in srb_batch (the neighbour snapshot rows are [x, y, xdot, ydot]);
+ *   outputs x_qp (may be NULL), x [A][24N+1], obj [A], status [A][2], iters [A][2] */
+typedef struct srb12_batch {
+    int struct_size;              /* sizeof(srb12_batch) (ABI check) */
+    const double *x0, *xref, *foot;
+    const int *contact;
+    const double *obstacles, *nbr_state;
+    int n_obs, n_all, agent_offset;
+    double *x_qp, *x, *obj;
+    int *status, *iters;
+    int *sel;                     /* optional [A][K_obs + K_nbr] selected rows */
+    int obstacles_version;
+} srb12_batch;
+
+typedef struct srb12_ctx srb12_ctx;
+int srb12_ctx_create(const srb12_params *p, int max_agents, int device, srb12_ctx **out);
+int srb12_ctx_destroy(srb12_ctx *ctx);
+/* host buffers: copies in, solves, copies out, synchronises */
+int srb12_solve_batch(srb12_ctx *ctx, int n_agents, const srb12_batch *host_io);
+/* device buffers, asynchronous on `stream` (NULL = the HIP null stream) */
+int srb12_solve_batch_device(srb12_ctx *ctx, int n_agents, const srb12_batch *dev_io, void *stream);
+/* HIP-event times of the last call's selection and solve kernels (ms) */
+int srb12_last_kernel_ms(srb12_ctx *ctx, float *select_ms, float *solve_ms);
+int srb12_lds_bytes(const srb12_params *p);
+
 const char *srb_last_error(void);
 
 #ifdef __cplusplus

@@ -245,7 +245,7 @@ static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
             req[r] = v;
         }
         nrd = sqrt(nrd); nrp = sqrt(nrp);
-        const double mu = sz / m;
+        const double mu = sz / (m > 0 ? m : 1);
         if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz)) { flag = 3; break; }
         if (getenv("ORC12_TRACE"))
             fprintf(stderr, "  %s it %2d |rd| %.3e (th %.3e) |rp| %.3e mu %.3e sigma %.3e\n", nl ? "nlp" : "qp ", it, nrd, th * gm, nrp, mu, sigma);
@@ -323,6 +323,7 @@ static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
             }
         }
         ap = fmin(1.0, 0.99 * ap); ad = fmin(1.0, 0.99 * ad);
+        if (getenv("ORC12_TRACE")) fprintf(stderr, "      ap %.4e ad %.4e delta %.3e\n", ap, ad, delta);
         for (int i = 0; i < n; i++) z[i] += ap * dz[i];
         for (int r = 0; r < m; r++) { s[r] += ap * ds[r]; zd[r] += ad * dzd[r]; }
     }
@@ -442,7 +443,7 @@ int orc12_solve_agent(const orc12_params *p_in, const double x0[12], const doubl
         orc_select_obstacles(&op, xl, obstacles, n_obs, nbr_state, n_all, self_idx, obs, eps);
         P.obs = obs; P.eps = eps;
         status[1] = ipm(&P, 1, z, lam, &iters[1]);
-    } else if (prm->use_nlp) {
+    } else if (prm->use_nlp && status[0] != 3) {
         P.mc = 0;
         status[1] = ipm(&P, 1, z, lam, &iters[1]);
     }

@@ -1,0 +1,784 @@
+// SRB-12 extension mode for MI355X (gfx950): the batched CBF-NMPC of the north star on the
+// 12-state single rigid body.  The reference declares this model (FastMPC::runMPC, MPC_Cost,
+// MPC_Constraints, getLinearDynamics: /root/reference/include/fast_MPC.hpp:98-103) but never
+// implements it, so the problem is stated in DESIGN.md section 11 and in oracle/srb12.c (the
+// CPU checker this kernel is tested against); parity with the reference is UNPINNED.
+//
+//   state  x = [p, Theta (roll, pitch, yaw), v, omega] (12), inputs u_k = four leg forces (12);
+//   x_{k+1} = A_k x_k + B_k u_k + c_k, the convex-MPC linearisation about the reference yaw:
+//     A_k = I + Ts E(psi_k)  (p += Ts v, Theta += Ts Rz' omega),
+//     B_k: v += Ts f / m, omega += Ts I_w^-1 (r_l x f_l) per stance leg l (W_l = Ts I_w^-1 [r_l]x);
+//   cost  sum (x - x_ref)' Q (x - x_ref) / 2 + u' R u / 2 + Sw s^2 / 2;
+//   rows  friction pyramid + f_z <= fmax per stance leg (LowLevelCtrl.cpp:158-162), and in the
+//         NLP stage the obstacle rows -|p_k - o_kj|^2 - s <= -eps_j (dec_vars_constr_cost.h:262-302).
+//
+// Execution model: one 64-lane wavefront per agent runs both interior-point stages (QP without
+// the obstacle rows, then the NLP warm-started from it), the iteration of oracle/srb12.c step for
+// step.  The Newton system is solved by a Riccati recursion over the horizon instead of the
+// oracle's dense LU -- O(N 12^3) per iteration, the structure the 12-state model has:
+//   * every inequality row is a slot owned by one lane (registers), scattered into per-grid
+//     Hessian blocks (the p_xy 2x2 block and the s border column of the obstacle rows, the 3x3
+//     friction blocks of each leg) by LDS atomics;
+//   * backward pass per grid: G = V A, F = V B (A, B applied through their structure: a few FMAs
+//     per entry), Hu = R^ + B'F inverted by the register Gauss-Jordan of the LIP kernel (its pivots
+//     are the reduced Hessian's LDL' pivots: the inertia test), Hux = B'G, and the Schur update
+//     V' = Q^ + A'G - Hux' (Hu^-1 Hux) as two 16x16x16 products on the matrix cores
+//     (v_mfma_f64_16x16x4f64: M = Hu^-1 Hux with Hu^-1 straight from the Gauss-Jordan registers,
+//     then Hux' M);
+//   * the global obstacle slack s borders the banded system: one extra right-hand side (the border
+//     column) per factorisation and a scalar Schur complement;
+//   * the dual residual uses the costates of the backward recursion lambda_k = grad_x_k L +
+//     A_k' lambda_{k+1} (the state part of r_d is zero, the input part is the reduced gradient);
+//     the primal-dual step does not depend on them (oracle, same rule).
+#include <hip/hip_runtime.h>
+#include <stdint.h>
+#include "srb_kernel_params.h"
+
+#define SYNC() __syncthreads()
+#include "srb_wave.h"
+
+namespace {
+
+struct Srb12Lds {
+    double *Wl, *cs, *ct, *Lm, *Hx, *V0, *V1, *Gt, *Ft, *Mt, *Q3, *Rh, *Z, *xr, *gX, *gU;
+    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *lam, *obs, *eps;
+    int *sel;
+};
+
+// the carve of srb12_lds_doubles (srb_kernel_params.h), same order.  State vectors carry 13 entries
+// per grid (the 12 states and the slack), input vectors 12; columns 0 (solve) and 1 (its refinement)
+__device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
+{
+    Srb12Lds L;
+    L.Wl = p; p += 36 * N;  L.cs = p; p += 2 * N;  L.ct = p; p += 4 * N;
+    L.Lm = p; p += 144 * N; L.Hx = p; p += 156 * N;
+    L.V0 = p; p += 169; L.V1 = p; p += 169;
+    L.Gt = p; p += 169; L.Ft = p; p += 156; L.Mt = p; p += 156;
+    L.Q3 = p; p += 6 * N; L.Rh = p; p += 24 * N;
+    L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N; L.gX = p; p += 13 * N; L.gU = p; p += 12 * N;
+    L.rX = p; p += 26 * N; L.rU = p; p += 24 * N; L.dX = p; p += 26 * N; L.dU = p; p += 24 * N;
+    L.gus = p; p += 24 * N; L.vv = p; p += 32; L.sc = p; p += 16; L.lam = p; p += 16;
+    L.obs = p; p += 2 * N * K; L.eps = p; p += K;
+    L.sel = (int *)p;
+    return L;
+}
+
+// Rz(psi)[a][b] from (cos, sin)
+__device__ __forceinline__ double rzab(int a, int b, double c, double s)
+{
+    return (a == 2 || b == 2) ? ((a == b) ? 1.0 : 0.0) : (a == b) ? c : (a == 0 ? -s : s);
+}
+
+// (A_k x)[i], x a 12-vector in LDS
+__device__ __forceinline__ double a_mul(int i, const double *x, double Ts, double c, double s)
+{
+    double v = x[i];
+    if (i < 3) v = fma(Ts, x[6 + i], v);
+    else if (i < 6) v = fma(Ts, rzab(0, i - 3, c, s) * x[9] + rzab(1, i - 3, c, s) * x[10] + rzab(2, i - 3, c, s) * x[11], v);
+    return v;
+}
+// (A_k' x)[i]
+__device__ __forceinline__ double at_mul(int i, const double *x, double Ts, double c, double s)
+{
+    double v = x[i];
+    if (i >= 6 && i < 9) v = fma(Ts, x[i - 6], v);
+    else if (i >= 9 && i < 12) v = fma(Ts, rzab(i - 9, 0, c, s) * x[3] + rzab(i - 9, 1, c, s) * x[4] + rzab(i - 9, 2, c, s) * x[5], v);
+    return v;
+}
+// the 13-state forms (x[12] = the slack, s_{k+1} = s_k): A~ = diag(A, 1)
+__device__ __forceinline__ double a13(int i, const double *x, double Ts, double c, double s)
+{
+    return (i == 12) ? x[12] : a_mul(i, x, Ts, c, s);
+}
+__device__ __forceinline__ double at13(int i, const double *x, double Ts, double c, double s)
+{
+    return (i == 12) ? x[12] : at_mul(i, x, Ts, c, s);
+}
+// (B_k u)[i] (i < 12); W: the grid's 4 x 9 leg blocks (contact and Ts folded in), ct: contact flags
+__device__ __forceinline__ double b_mul(int i, const double *u, const double *W, const double *ct, double tsm)
+{
+    double v = 0.0;
+    if (i >= 6 && i < 9) {
+        for (int l = 0; l < 4; l++) v = fma(ct[l] * tsm, u[3 * l + i - 6], v);
+    } else if (i >= 9 && i < 12) {
+        const int a = i - 9;
+        for (int l = 0; l < 4; l++)
+            for (int j = 0; j < 3; j++) v = fma(W[9 * l + 3 * a + j], u[3 * l + j], v);
+    }
+    return v;
+}
+// (B_k' x)[3 l + j]
+__device__ __forceinline__ double bt_mul(int e, const double *x, const double *W, const double *ct, double tsm)
+{
+    const int l = e / 3, j = e - 3 * l;
+    double v = ct[l] * tsm * x[6 + j];
+    for (int a = 0; a < 3; a++) v = fma(W[9 * l + 3 * a + j], x[9 + a], v);
+    return v;
+}
+// friction row q of a leg: coefficients on (f_x, f_y, f_z) (LowLevelCtrl.cpp:158-162, + f_z <= fmax)
+__device__ __forceinline__ void fric_coef(int q, double mus, double &c0, double &c1, double &c2)
+{
+    c0 = (q == 0) ? 1.0 : (q == 1) ? -1.0 : 0.0;
+    c1 = (q == 2) ? 1.0 : (q == 3) ? -1.0 : 0.0;
+    c2 = (q < 4) ? -mus : (q == 4) ? -1.0 : 1.0;
+}
+// index of (a, b) in a symmetric 3x3 block stored as 00 01 02 11 12 22
+__device__ __forceinline__ int sym3(int a, int b)
+{
+    const int i = a < b ? a : b, j = a < b ? b : a;
+    return (i == 0) ? j : (i == 1) ? 2 + j : 5;
+}
+
+__device__ __forceinline__ double pick4(const double (&M)[12], int kk, int q)
+{
+    // M[4 kk + q] with q lane-dependent (0..3); entries >= 12 are 0
+    const int b = 4 * kk;
+    const double v0 = (b + 0 < 12) ? M[(b + 0) % 12] : 0.0, v1 = (b + 1 < 12) ? M[(b + 1) % 12] : 0.0;
+    const double v2 = (b + 2 < 12) ? M[(b + 2) % 12] : 0.0, v3 = (b + 3 < 12) ? M[(b + 3) % 12] : 0.0;
+    return q == 0 ? v0 : q == 1 ? v1 : q == 2 ? v2 : v3;
+}
+
+} // namespace
+
+template <int TS>
+__device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, const double *__restrict__ x0g,
+        const double *__restrict__ xrefg, const double *__restrict__ footg, const int *__restrict__ contactg,
+        const double *__restrict__ obstacles, const double *__restrict__ nbr_state, const int *__restrict__ sel_g,
+        double *__restrict__ x_qp_out, double *__restrict__ x_out, double *__restrict__ obj_out,
+        int *__restrict__ status_out, int *__restrict__ iters_out, double *lds)
+{
+    const int tid = threadIdx.x, lane = tid;
+    const int N = prm.N, K = prm.K_obs + prm.K_nbr, NK = N * K, nv = 24 * N + 1;
+    const int nf = 24 * N;                                  // friction row slots
+    const double Ts = prm.Ts, tsm = prm.Ts / prm.mass, mus = prm.mus;
+    const double tol = prm.tol, th = tol / sqrt(3.0);
+    Srb12Lds L = carve12(lds, N, K);
+    double *X = L.Z, *U = L.Z + 12 * N;
+    const double *x0 = x0g + 12 * (size_t)agent;
+
+    // ---------------- inputs, per-grid model (orc12_dynamics), selected rows
+    for (int i = tid; i < 12 * N; i += 64) L.xr[i] = xrefg[(size_t)agent * 12 * N + i];
+    for (int i = tid; i < 4 * N; i += 64) L.ct[i] = contactg[(size_t)agent * 4 * N + i] ? 1.0 : 0.0;
+    if (prm.use_nlp && tid < K) L.sel[tid] = sel_g[(size_t)agent * K + tid];
+    SYNC();
+    for (int e = tid; e < 4 * N; e += 64) {              // one (grid, leg) per lane: W_l = Ts Iw^-1 [r]x
+        const int k = e >> 2, l = e & 3;
+        const double *ph = (k == 0) ? x0 : L.xr + 12 * (k - 1);
+        const double psi = ph[5], c = cos(psi), s = sin(psi);
+        double R[9], T[9], Iw[9], Iwi[9];
+        for (int a = 0; a < 3; a++) for (int b = 0; b < 3; b++) R[3 * a + b] = rzab(a, b, c, s);
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) T[3 * i + j] = R[3 * i] * prm.Ib[j] + R[3 * i + 1] * prm.Ib[3 + j] + R[3 * i + 2] * prm.Ib[6 + j];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++) Iw[3 * i + j] = T[3 * i] * R[3 * j] + T[3 * i + 1] * R[3 * j + 1] + T[3 * i + 2] * R[3 * j + 2];
+        {
+            const double a = Iw[0], b = Iw[1], cc = Iw[2], d = Iw[3], ee = Iw[4], f = Iw[5], g = Iw[6], h = Iw[7], ii = Iw[8];
+            const double A0 = ee * ii - f * h, B0 = -(d * ii - f * g), C0 = d * h - ee * g;
+            const double r = 1.0 / (a * A0 + b * B0 + cc * C0);
+            Iwi[0] = A0 * r; Iwi[1] = -(b * ii - cc * h) * r; Iwi[2] = (b * f - cc * ee) * r;
+            Iwi[3] = B0 * r; Iwi[4] = (a * ii - cc * g) * r; Iwi[5] = -(a * f - cc * d) * r;
+            Iwi[6] = C0 * r; Iwi[7] = -(a * h - b * g) * r; Iwi[8] = (a * ee - b * d) * r;
+        }
+        const double *fp = footg + (size_t)agent * 12 * N + 12 * k + 3 * l;
+        const double r0 = fp[0] - ph[0], r1 = fp[1] - ph[1], r2 = fp[2] - ph[2];
+        const double S[9] = {0, -r2, r1, r2, 0, -r0, -r1, r0, 0};
+        const double on = L.ct[4 * k + l];
+        for (int i = 0; i < 3; i++)
+            for (int j = 0; j < 3; j++)
+                L.Wl[36 * k + 9 * l + 3 * i + j] = on * (Ts * (Iwi[3 * i] * S[j] + Iwi[3 * i + 1] * S[3 + j] + Iwi[3 * i + 2] * S[6 + j]));
+        if (l == 0) { L.cs[2 * k] = c; L.cs[2 * k + 1] = s; }
+    }
+    if (prm.use_nlp) {                                   // obstacle rows: the LIP mode's selection and prediction
+        for (int e = tid; e < NK; e += 64) {
+            const int k = e / K, j = e - k * K;
+            const bool st = j < prm.K_obs;
+            const int bi = L.sel[j];
+            const double tt = st ? 0.0 : Ts * (k + 1);
+            const size_t bj = (bi >= 0) ? bi : 0;
+            const double *src = st ? obstacles + 2 * bj : nbr_state + 4 * bj;
+            L.obs[2 * e] = (bi >= 0) ? src[0] + (st ? 0.0 : src[2] * tt) : x0[0] + 1000.0;
+            L.obs[2 * e + 1] = (bi >= 0) ? src[1] + (st ? 0.0 : src[3] * tt) : x0[1];
+        }
+        if (tid < K) L.eps[tid] = (tid < prm.K_obs) ? prm.eps_obs : prm.eps_nbr;
+    }
+    // start: gravity-compensating forces on the stance legs, the dynamics rolled out, s = 0
+    for (int e = tid; e < 12 * N; e += 64) {
+        const int k = e / 12, i = e - 12 * k, l = i / 3;
+        int ns = 0;
+        for (int q = 0; q < 4; q++) ns += contactg[(size_t)agent * 4 * N + 4 * k + q] != 0;
+        U[e] = (i % 3 == 2 && ns && contactg[(size_t)agent * 4 * N + 4 * k + l]) ? prm.mass * prm.grav / ns : 0.0;
+    }
+    if (tid < 12) L.vv[tid] = x0[tid];
+    if (tid == 0) L.Z[24 * N] = 0.0;                    // s
+    SYNC();
+    for (int k = 0; k < N; k++) {                        // x_{k+1} = A_k x_k + B_k u_k + c_k
+        double v = 0.0;
+        if (tid < 12) {
+            v = a_mul(tid, L.vv, Ts, L.cs[2 * k], L.cs[2 * k + 1]) + b_mul(tid, U + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+            if (tid == 8) v -= Ts * prm.grav;
+        }
+        SYNC();
+        if (tid < 12) { L.vv[tid] = v; X[12 * k + tid] = v; }
+        SYNC();
+    }
+
+    // ---------------- slot state (registers): row t of this lane is slot id = lane + 64 t
+    double ss[TS], zz[TS], dsa[TS], dza[TS];
+    int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
+    const int nstage = prm.use_nlp ? 2 : 1;
+#pragma clang loop unroll(disable)
+    for (int stage = 0; stage < nstage; stage++) {
+        const bool nl = stage == 1;
+        const int nrow = nl ? nf + NK : nf;
+        // active row count m and the starting slacks / duals (oracle ipm(): QP s = h - g, z = 1 /
+        // max(s, 1); NLP shifted so min s = 1 when a row is violated, z = z0 / max(s, 1))
+        auto row_g = [&](int id, double &g, double &h, double &c0, double &c1, double &c2, int &kind) {
+            g = 0.0; h = 0.0; c0 = c1 = c2 = 0.0; kind = 0;
+            if (id < nf) {
+                const int k = id / 24, l = (id / 6) & 3, q = id % 6;
+                if (L.ct[4 * k + l] != 0.0) {
+                    kind = 1;
+                    fric_coef(q, mus, c0, c1, c2);
+                    const double *u = U + 12 * k + 3 * l;
+                    g = c0 * u[0] + c1 * u[1] + c2 * u[2];
+                    h = (q == 5) ? prm.fmax : 0.0;
+                }
+            } else if (id < nrow) {
+                const int e = id - nf, k = e / K, j = e - k * K;
+                kind = 2;
+                const double dx = X[12 * k] - L.obs[2 * e], dy = X[12 * k + 1] - L.obs[2 * e + 1];
+                c0 = -2.0 * dx; c1 = -2.0 * dy;
+                g = -(dx * dx + dy * dy) - L.Z[24 * N];
+                h = -L.eps[j];
+            }
+        };
+        double mcount = 0.0, mn = 1e300;
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            double g, h, c0, c1, c2; int kind;
+            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
+            ss[t] = h - g;
+            if (kind) { mcount += 1.0; mn = fmin(mn, h - g); }
+        }
+        {
+            double rv[2] = {mcount, -mn};
+            wred<2, 2u>(rv);
+            mcount = rv[0]; mn = -rv[1];
+        }
+        const double ssh = (nl && mn <= 0.0) ? 1.0 - mn : 0.0;
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            double g, h, c0, c1, c2; int kind;
+            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
+            double s = ss[t] + ssh;
+            if (!nl && s < 1e-8) s = 1e-8;
+            ss[t] = kind ? s : 1.0;
+            zz[t] = kind ? (nl ? prm.z0 : 1.0) / fmax(s, 1.0) : 0.0;
+            dsa[t] = dza[t] = 0.0;
+        }
+        const double inv_m = 1.0 / fmax(mcount, 1.0);
+        const int maxit = nl ? prm.nlp_maxit : prm.qp_maxit;
+        int flag = 2, it = 0;
+        double sigma = 0.0;
+#pragma clang loop unroll(disable)
+        for (it = 0; it < maxit; it++) {
+            // ---- gradient of f (X, U; Sw s of the slack at s_0), cleared per-grid blocks
+            for (int e = tid; e < 12 * N; e += 64) {
+                const int k = e / 12, i = e - 12 * k;
+                const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+                L.gX[13 * k + i] = w * (X[e] - L.xr[e]);
+                L.gU[e] = prm.r[i % 3] * U[e];
+            }
+            for (int k = tid; k < N; k += 64) L.gX[13 * k + 12] = 0.0;
+            for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
+            for (int e = tid; e < 24 * N; e += 64) L.Rh[e] = 0.0;
+            if (tid == 0) { L.sc[0] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }    // grad_s f, H_ss (inertia scale)
+            SYNC();
+            // ---- rows: residuals, weights, scatter of J'z and J'WJ into the per-grid blocks
+            double nrp = 0.0, sz = 0.0;
+#pragma unroll
+            for (int t = 0; t < TS; t++) {
+                const int id = lane + 64 * t;
+                double g, h, c0, c1, c2; int kind;
+                row_g(id, g, h, c0, c1, c2, kind);
+                if (!kind) continue;
+                const double rp = g + ss[t] - h, om = zz[t] / ss[t];
+                nrp = fma(rp, rp, nrp);
+                sz = fma(ss[t], zz[t], sz);
+                if (kind == 1) {
+                    const int k = id / 24, l = (id / 6) & 3;
+                    double *gu = L.gU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+                    const double cc[3] = {c0, c1, c2};
+                    for (int a = 0; a < 3; a++)
+                        if (cc[a] != 0.0) __hip_atomic_fetch_add(&gu[a], zz[t] * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    for (int a = 0; a < 3; a++)
+                        for (int b = a; b < 3; b++)
+                            if (cc[a] != 0.0 && cc[b] != 0.0)
+                                __hip_atomic_fetch_add(&rh[sym3(a, b)], om * cc[a] * cc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                } else {
+                    // obstacle row of grid k on (p_x, p_y, s): J = (c0, c1, -1), Lagrangian Hessian -2z on p_x, p_y
+                    const int k = (id - nf) / K;
+                    double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
+                    __hip_atomic_fetch_add(&gx[0], zz[t] * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&gx[1], zz[t] * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&gx[12], -zz[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * zz[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * zz[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&L.sc[1], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                }
+            }
+            SYNC();
+            // ---- costates and the dual residual (13-state: the slack rides along as x[12], s_{k+1} = s_k):
+            //      lam_{N-1} = gX_{N-1}, lam_{k-1} = gX_{k-1} + A~_k' lam_k, r_u,k = gU_k + B_k' lam_k,
+            //      r_s = Sw s + lam_0[12] (the free initial slack)
+            double nrd = 0.0, gm = 1.0;
+            for (int e = tid; e < 12 * N; e += 64) {
+                const int k = e / 12, i = e - 12 * k;
+                const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+                gm = fmax(gm, fabs(w * (X[e] - L.xr[e])));
+                gm = fmax(gm, fabs(prm.r[i % 3] * U[e]));
+            }
+            gm = fmax(gm, fabs(prm.Sw * L.Z[24 * N]));
+            if (tid < 13) L.lam[tid] = L.gX[13 * (N - 1) + tid];
+            SYNC();
+            for (int k = N - 1; k >= 0; k--) {
+                double ln = 0.0;
+                if (tid < 12) {
+                    const double ru = L.gU[12 * k + tid] + bt_mul(tid, L.lam, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+                    nrd = fma(ru, ru, nrd);
+                }
+                if (k > 0 && tid < 13) ln = L.gX[13 * (k - 1) + tid] + at13(tid, L.lam, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
+                SYNC();
+                if (k > 0 && tid < 13) L.lam[tid] = ln;
+                SYNC();
+            }
+            if (tid == 0) { const double rs = L.sc[0] + L.lam[12]; nrd = fma(rs, rs, nrd); }
+            {
+                double rv[4] = {nrd, nrp, sz, gm};
+                wred<4, 8u>(rv);
+                nrd = sqrt(rv[0]); nrp = sqrt(rv[1]); sz = rv[2]; gm = rv[3];
+            }
+            const double mu = sz * inv_m;
+            double *dbgrow = (agent == prm.dbg_agent && prm.dbg && it < 64) ? prm.dbg + 8 * (64 * stage + it) : nullptr;
+            if (dbgrow && tid == 0) { dbgrow[0] = nrd; dbgrow[1] = th * gm; dbgrow[2] = nrp; dbgrow[3] = mu; }
+            if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz)) { flag = 3; break; }
+            if (nrd < th * gm && nrp < th && mu < tol) { flag = 0; break; }
+
+            // ---- factorisation (backward Riccati over the 13-state) with the inertia shift delta (NLP)
+            double dmax = 1.0;
+            for (int e = tid; e < 12 * N; e += 64) {
+                const int k = e / 12, i = e - 12 * k;
+                const double qd = ((k == N - 1) ? prm.qN[i] : prm.q[i]) + (i < 2 ? L.Q3[6 * k + 2 * i] : 0.0);
+                const int l = i / 3, a = i % 3;
+                const double rd = prm.r[a] + L.Rh[24 * k + 6 * l + sym3(a, a)];
+                dmax = fmax(dmax, fmax(qd, rd));
+            }
+            dmax = wmax(dmax);
+            dmax = fmax(dmax, L.sc[1]);
+            const double dstart = 1e-10 * dmax;
+            // Q^_k (state block k, 13 x 13): diag(q) + delta on the 12 states, the obstacle rows' (p_x, p_y, s)
+            // block; the slack's own weight Sw + delta enters once, at s_0
+            auto qhat = [&](int k, int i, int j, double delta) {
+                double v = (i == j && i < 12) ? ((k == N - 1) ? prm.qN[i] : prm.q[i]) + delta : 0.0;
+                const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
+                if (pi && pj) {
+                    const double *q3 = L.Q3 + 6 * k;
+                    const int a = (i == 12) ? 2 : i, b = (j == 12) ? 2 : j;
+                    const int lo = a < b ? a : b, hi = a < b ? b : a;
+                    v += (lo == 0) ? (hi == 0 ? q3[0] : hi == 1 ? q3[1] : q3[3]) : (lo == 1) ? (hi == 1 ? q3[2] : q3[4]) : q3[5];
+                }
+                return v;
+            };
+            double delta = 0.0, schur = 0.0;
+            int ok = 0;
+            for (int tries = 0; tries < (nl ? 14 : 1); tries++) {
+                if (tries > 0) delta = (delta == 0.0) ? dstart : delta * 10.0;
+                int fail = 0;
+                int cur = 0;
+                for (int e = tid; e < 169; e += 64) L.V0[e] = qhat(N - 1, e / 13, e % 13, delta);
+                SYNC();
+                for (int k = N - 1; k >= 0; k--) {
+                    const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = cur ? L.V1 : L.V0;
+                    // G = V A~_k (13 x 13), F = V B~_k (13 x 12)
+                    for (int e = tid; e < 169; e += 64) {
+                        const int i = e / 13, j = e - 13 * i;
+                        const double *Vi = V + 13 * i;
+                        double g = Vi[j];
+                        if (j >= 6 && j < 9) g = fma(Ts, Vi[j - 6], g);
+                        else if (j >= 9 && j < 12) g = fma(Ts, Vi[3] * rzab(j - 9, 0, c, s) + Vi[4] * rzab(j - 9, 1, c, s) + Vi[5] * rzab(j - 9, 2, c, s), g);
+                        L.Gt[e] = g;
+                    }
+                    for (int e = tid; e < 156; e += 64) {
+                        const int i = e / 12, j = e - 12 * i, l = j / 3, jj = j - 3 * l;
+                        const double *Vi = V + 13 * i;
+                        double f = ct[l] * tsm * Vi[6 + jj];
+                        for (int a = 0; a < 3; a++) f = fma(Vi[9 + a], W[9 * l + 3 * a + jj], f);
+                        L.Ft[e] = f;
+                    }
+                    SYNC();
+                    // Hu = R^ + B'F: row i16 of every 16-lane row (replicated for the Gauss-Jordan)
+                    double Mi[12];
+                    {
+                        const int i = lane & 15;
+                        const int li = (i < 12) ? i / 3 : 0, ai = (i < 12) ? i - 3 * li : 0;
+#pragma unroll
+                        for (int j = 0; j < 12; j++) {
+                            double v = 0.0;
+                            if (i < 12) {
+                                v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
+                                for (int a = 0; a < 3; a++) v = fma(W[9 * li + 3 * a + ai], L.Ft[12 * (9 + a) + j], v);
+                                if (j == i) v += prm.r[ai] + delta;
+                                if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
+                            }
+                            Mi[j] = v;
+                        }
+                    }
+                    fail |= gj_invert<12>(Mi, 12, lane, 0);
+                    if (lane < 12)
+#pragma unroll
+                        for (int j = 0; j < 12; j++) L.Lm[144 * k + 12 * lane + j] = Mi[j];
+                    // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
+                    // V_0[12][12] is used (the initial slack's Schur complement)
+                    double *Hx = L.Hx + 156 * k, *Vn = cur ? L.V0 : L.V1;
+                    for (int e = tid; e < 156; e += 64) {
+                        const int i = e / 13, j = e - 13 * i;
+                        const int li = i / 3, ai = i - 3 * li;
+                        double hx = ct[li] * tsm * L.Gt[13 * (6 + ai) + j];
+                        for (int a = 0; a < 3; a++) hx = fma(W[9 * li + 3 * a + ai], L.Gt[13 * (9 + a) + j], hx);
+                        Hx[e] = hx;
+                    }
+                    for (int e = tid; e < 169; e += 64) {
+                        const int i = e / 13, j = e - 13 * i;
+                        double w = L.Gt[e];
+                        if (i >= 6 && i < 9) w = fma(Ts, L.Gt[13 * (i - 6) + j], w);
+                        else if (i >= 9 && i < 12)
+                            w = fma(Ts, rzab(i - 9, 0, c, s) * L.Gt[39 + j] + rzab(i - 9, 1, c, s) * L.Gt[52 + j] +
+                                            rzab(i - 9, 2, c, s) * L.Gt[65 + j], w);
+                        if (k > 0) w += qhat(k - 1, i, j, delta);
+                        Vn[e] = w;
+                    }
+                    SYNC();
+                    // S = Hux' Hu^-1 Hux = Y'Y with Y = D^-1/2 L^-1 Hux (Hu = L D L'): forward elimination of
+                    // [Hu | Hux] in registers (row i16 per lane, replicated like the Gauss-Jordan), then the
+                    // 16x16x16 product Y'Y on the matrix cores.  The product with the explicit inverse,
+                    // Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on active rows; Y'Y is
+                    // positive semi-definite by construction.
+                    {
+                        const int i16 = lane & 15, q = lane >> 4;
+                        double Ag[25];
+                        {
+                            const int li = (i16 < 12) ? i16 / 3 : 0, ai = (i16 < 12) ? i16 - 3 * li : 0;
+#pragma unroll
+                            for (int j = 0; j < 12; j++) {
+                                double v = 0.0;
+                                if (i16 < 12) {
+                                    v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
+                                    for (int aa = 0; aa < 3; aa++) v = fma(W[9 * li + 3 * aa + ai], L.Ft[12 * (9 + aa) + j], v);
+                                    if (j == i16) v += prm.r[ai] + delta;
+                                    if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
+                                }
+                                Ag[j] = v;
+                            }
+#pragma unroll
+                            for (int j = 0; j < 13; j++) Ag[12 + j] = (i16 < 12) ? Hx[13 * i16 + j] : 0.0;
+                        }
+                        double dk = 1.0;
+#pragma unroll
+                        for (int kk = 0; kk < 12; kk++) {
+                            const double piv = readlane_d(Ag[kk], kk);
+                            fail |= !(piv > 0.0);
+                            const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
+#pragma unroll
+                            for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, readlane_d(Ag[j], kk), Ag[j]);
+                            dk = (i16 == kk) ? piv : dk;
+                        }
+                        const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
+                        if (lane < 12)
+#pragma unroll
+                            for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
+                        SYNC();
+                        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                        for (int kk = 0; kk < 4; kk++) {
+                            const int kc = 4 * kk + q;
+                            const double y = (kc < 12 && i16 < 13) ? L.Mt[13 * kc + i16] : 0.0;
+                            acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, acc2, 0, 0, 0);
+                        }
+#pragma unroll
+                        for (int r = 0; r < 4; r++) {
+                            const int row = q + 4 * r;
+                            if (row < 13 && i16 < 13) Vn[13 * row + i16] -= acc2[r];
+                        }
+                    }
+                    SYNC();
+                    cur ^= 1;
+                }
+                if (fail) continue;
+                // the free initial slack closes the recursion: V_0[12][12] + Sw + delta > 0 is the last
+                // pivot of the inertia test
+                schur = (cur ? L.V1 : L.V0)[168] + prm.Sw + delta;
+                if (!(schur > 0.0)) continue;
+                ok = 1;
+                break;
+            }
+            if (!ok) { flag = 1; break; }
+            // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
+            // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free)
+            auto riccati_solve = [&](int c) {
+                const int i = lane;
+                const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
+                double *dX = L.dX + 13 * N * c, *dU = L.dU + 12 * N * c, *gus = L.gus + 12 * N * c;
+                double *v = L.vv, *pv = L.vv + 16;
+                if (i < 13) v[i] = rX[13 * (N - 1) + i];
+                SYNC();
+                for (int k = N - 1; k >= 0; k--) {
+                    if (i < 12) gus[12 * k + i] = rU[12 * k + i] + bt_mul(i, v, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+                    SYNC();
+                    if (i < 12) {
+                        const double *Lr = L.Lm + 144 * k + 12 * i;
+                        double kk = 0.0;
+                        for (int j = 0; j < 12; j++) kk = fma(-Lr[j], gus[12 * k + j], kk);
+                        dU[12 * k + i] = kk;
+                    }
+                    SYNC();
+                    double vn = 0.0;
+                    if (i < 13) {
+                        vn = ((k > 0) ? rX[13 * (k - 1) + i] : 0.0) + at13(i, v, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
+                        const double *Hx = L.Hx + 156 * k;
+                        for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], dU[12 * k + j], vn);
+                    }
+                    SYNC();
+                    if (i < 13) v[i] = vn;
+                    SYNC();
+                }
+                const double ds0 = -(v[12] + L.sc[2 + c]) / schur;
+                if (i < 13) pv[i] = (i == 12) ? ds0 : 0.0;
+                SYNC();
+                for (int k = 0; k < N; k++) {
+                    // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
+                    const double *prev = (k == 0) ? pv : dX + 13 * (k - 1);
+                    if (i < 12) {
+                        const double *Hr = L.Hx + 156 * k + 13 * i;
+                        double t = gus[12 * k + i];
+                        for (int j = 0; j < 13; j++) t = fma(Hr[j], prev[j], t);
+                        v[i] = t;
+                    }
+                    SYNC();
+                    if (i < 12) {
+                        const double *Lr = L.Lm + 144 * k + 12 * i;
+                        double du = 0.0;
+                        for (int j = 0; j < 12; j++) du = fma(-Lr[j], v[j], du);
+                        dU[12 * k + i] = du;
+                    }
+                    SYNC();
+                    if (i < 13)
+                        dX[13 * k + i] = a13(i, prev, Ts, L.cs[2 * k], L.cs[2 * k + 1]) +
+                                         ((i < 12) ? b_mul(i, dU + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm) : 0.0);
+                    SYNC();
+                }
+            };
+            // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
+            // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
+            // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s).
+            // Explicit Gauss-Jordan inverses lose digits once z / s reaches 1e7 on active rows.
+            auto refine = [&](double delta) {
+                const int i = lane;
+                const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
+                double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N, *mu = L.vv;
+                auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
+                    double v = 0.0;
+                    for (int j = 0; j < 13; j++) {
+                        const bool nz = (j == i) || ((i < 2 || i == 12) && (j < 2 || j == 12));
+                        if (nz) v = fma(qhat(k, i, j, delta), dx[j], v);
+                    }
+                    return v;
+                };
+                if (i < 13) mu[i] = qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i];
+                for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
+                SYNC();
+                for (int k = N - 1; k >= 0; k--) {
+                    double mn = 0.0;
+                    if (i < 12) {
+                        const int l = i / 3, a = i - 3 * l;
+                        const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+                        double t = fma(prm.r[a] + delta, du[a], rU[12 * k + i]);
+                        for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a, bb)], du[bb], t);
+                        tU[12 * k + i] = t + bt_mul(i, mu, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+                    }
+                    if (k > 0 && i < 13) mn = qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] + at13(i, mu, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
+                    SYNC();
+                    if (k > 0 && i < 13) mu[i] = mn;
+                    SYNC();
+                }
+                if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + mu[12];
+                SYNC();
+                riccati_solve(1);
+                for (int e = tid; e < 13 * N; e += 64) L.dX[e] += L.dX[13 * N + e];
+                for (int e = tid; e < 12 * N; e += 64) L.dU[e] += L.dU[12 * N + e];
+                SYNC();
+            };
+            // right-hand side of pass (0 predictor, 1 corrector) into column 0:
+            // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
+            auto build_rhs = [&](int pass, double smu) {
+                for (int e = tid; e < 12 * N; e += 64) {
+                    const int k = e / 12, i = e - 12 * k;
+                    const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+                    L.rX[13 * k + i] = w * (X[e] - L.xr[e]);
+                    L.rU[e] = prm.r[i % 3] * U[e];
+                }
+                for (int k = tid; k < N; k += 64) L.rX[13 * k + 12] = 0.0;
+                if (tid == 0) L.sc[2] = prm.Sw * L.Z[24 * N];
+                SYNC();
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    const int id = lane + 64 * t;
+                    double g, h, c0, c1, c2; int kind;
+                    row_g(id, g, h, c0, c1, c2, kind);
+                    if (!kind) continue;
+                    const double rp = g + ss[t] - h, om = zz[t] / ss[t];
+                    const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
+                    const double w = zz[t] + r3 / ss[t] + om * rp;
+                    if (kind == 1) {
+                        const int k = id / 24, l = (id / 6) & 3;
+                        double *ru = L.rU + 12 * k + 3 * l;
+                        const double cc[3] = {c0, c1, c2};
+                        for (int a = 0; a < 3; a++)
+                            if (cc[a] != 0.0) __hip_atomic_fetch_add(&ru[a], w * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        double *rx = L.rX + 13 * ((id - nf) / K);
+                        __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    }
+                }
+                SYNC();
+            };
+            // the rows' steps of the solved column: J dz, ds = -r_p - J dz, dz = (r3 - z ds) / s; step maxima
+            auto row_step = [&](int pass, double smu, double (&dsl)[TS], double (&dzl)[TS]) {
+                double ms = 0.0, mz = 0.0;
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    const int id = lane + 64 * t;
+                    double g, h, c0, c1, c2; int kind;
+                    row_g(id, g, h, c0, c1, c2, kind);
+                    dsl[t] = dzl[t] = 0.0;
+                    if (!kind) continue;
+                    double jd;
+                    if (kind == 1) {
+                        const int k = id / 24, l = (id / 6) & 3;
+                        const double *du = L.dU + 12 * k + 3 * l;
+                        jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
+                    } else {
+                        const double *dx = L.dX + 13 * ((id - nf) / K);
+                        jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+                    }
+                    const double rp = g + ss[t] - h;
+                    const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
+                    dsl[t] = -rp - jd; dzl[t] = (r3 - zz[t] * dsl[t]) / ss[t];
+                    ms = fmax(ms, -dsl[t] / ss[t]); mz = fmax(mz, -dzl[t] / zz[t]);
+                }
+                double rv[2] = {ms, mz};
+                wred<2, 3u>(rv);
+                return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
+            };
+            // ---- predictor
+            build_rhs(0, 0.0);
+            riccati_solve(0);
+            refine(delta);
+            double dsl[TS], dzl[TS];
+            double2 al = row_step(0, 0.0, dsl, dzl);
+#pragma unroll
+            for (int t = 0; t < TS; t++) { dsa[t] = dsl[t]; dza[t] = dzl[t]; }
+            {
+                double num = 0.0;
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    double g, h, c0, c1, c2; int kind;
+                    row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
+                    if (kind) num = fma(fma(al.x, dsa[t], ss[t]), fma(al.y, dza[t], zz[t]), num);
+                }
+                num = wsum(num);
+                const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
+                sigma = mr * mr * mr;
+            }
+            // ---- corrector
+            build_rhs(1, sigma * mu);
+            riccati_solve(0);
+            refine(delta);
+            al = row_step(1, sigma * mu, dsl, dzl);
+            const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);
+            if (dbgrow && tid == 0) { dbgrow[4] = ap; dbgrow[5] = ad; dbgrow[6] = delta; dbgrow[7] = sigma; }
+            // ---- update: x += ap dx (the slack: ds_0, carried in every grid's x[12]), rows s += ap ds, z += ad dz
+            const double dsv = L.dX[12];
+            SYNC();
+            for (int e = tid; e < 12 * N; e += 64) {
+                const int k = e / 12, i = e - 12 * k;
+                X[e] = fma(ap, L.dX[13 * k + i], X[e]);
+                U[e] = fma(ap, L.dU[e], U[e]);
+            }
+            if (tid == 0) L.Z[24 * N] = fma(ap, dsv, L.Z[24 * N]);
+#pragma unroll
+            for (int t = 0; t < TS; t++) { ss[t] = fma(ap, dsl[t], ss[t]); zz[t] = fma(ad, dzl[t], zz[t]); }
+            SYNC();
+        }
+        if (stage == 0) {
+            qp_flag = flag; qp_it = it;
+            if (x_qp_out)
+                for (int v = tid; v < nv; v += 64) x_qp_out[(size_t)agent * nv + v] = L.Z[v];
+            if (flag == 3) break;
+        } else {
+            nlp_flag = flag; nlp_it = it;
+        }
+    }
+    // ---- outputs: x and 0.5 x'Px + c'x
+    double f = 0.0;
+    for (int v = tid; v < nv; v += 64) {
+        const double xv = L.Z[v];
+        x_out[(size_t)agent * nv + v] = xv;
+        double w, cl = 0.0;
+        if (v < 12 * N) { const int k = v / 12, i = v - 12 * k; w = (k == N - 1) ? prm.qN[i] : prm.q[i]; cl = -w * L.xr[v]; }
+        else if (v < 24 * N) w = prm.r[(v - 12 * N) % 3];
+        else w = prm.Sw;
+        f += fma(0.5 * w * xv, xv, cl * xv);
+    }
+    f = wsum(f);
+    if (tid == 0) {
+        obj_out[agent] = f;
+        status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
+        iters_out[2 * agent] = qp_it; iters_out[2 * agent + 1] = nlp_it;
+    }
+}
+
+#define SRB12_KERNEL(TS)                                                                                        \
+    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TS(                                         \
+        Srb12KParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ xrefg,        \
+        const double *__restrict__ footg, const int *__restrict__ contactg, const double *__restrict__ obstacles, \
+        const double *__restrict__ nbr_state, const int *__restrict__ sel_g, double *__restrict__ x_qp_out,      \
+        double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                \
+        int *__restrict__ iters_out)                                                                          \
+    {                                                                                                          \
+        extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
+        const int agent = blockIdx.x;                                                                          \
+        if (agent >= n_agents) return;                                                                         \
+        srb12_agent<TS>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out, x_out, \
+                        obj_out, status_out, iters_out, lds);                                                  \
+    }
+SRB12_KERNEL(4)
+SRB12_KERNEL(6)
+SRB12_KERNEL(8)
+SRB12_KERNEL(12)
+
+// CoM rows [x, xdot, y, ydot] of a 12-state batch: the layout the shared selection kernel
+// (srb_knn_kernel) reads its query points from
+extern "C" __global__ void srb12_pos_kernel(int n_agents, const double *__restrict__ x0g, double *__restrict__ pos)
+{
+    const int a = blockIdx.x * blockDim.x + threadIdx.x;
+    if (a >= n_agents) return;
+    const double *x = x0g + 12 * (size_t)a;
+    pos[4 * (size_t)a] = x[0]; pos[4 * (size_t)a + 1] = x[6]; pos[4 * (size_t)a + 2] = x[1]; pos[4 * (size_t)a + 3] = x[7];
+}

@@ -334,6 +334,51 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     return SRB_OK;
 }
 
+// Obstacle / neighbour selection for a batch (srb_knn_kernel; with a uniform grid per long table,
+// srb_grid_build_kernel): K_obs, K_nbr already clamped to the tables.  x0 rows are [x, ., y, .]
+// (stride 4); shared with the SRB-12 mode (srb12_capi.cpp), which hands over its CoM positions so.
+static int launch_select(srb_ctx *c, int n_agents, const double *x0, const double *obstacles, int n_obs,
+                         const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
+                         int obstacles_version, int *sel, hipStream_t s)
+{
+    // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
+    // with the arena) get a uniform grid so each agent scans only the cells around it
+    // (a versioned static obstacle table builds its grid once, so it pays off at fewer rows;
+    // SRB_GRID_MIN_ROWS overrides both thresholds)
+    static const char *env_rows = std::getenv("SRB_GRID_MIN_ROWS");
+    static const int min_rows = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS;
+    static const int min_rows_static = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS_STATIC;
+    const bool go = K_obs > 0 && n_obs >= (obstacles_version != 0 ? min_rows_static : min_rows);
+    const bool gn = K_nbr > 0 && n_all >= min_rows;
+    if (go) { int rc = grid_reserve(c, 0, n_obs); if (rc) return rc; }
+    if (gn) { int rc = grid_reserve(c, 1, n_all); if (rc) return rc; }
+    const srb_ctx::grid_buf &G0 = c->grid[0], &G1 = c->grid[1];
+    // a static obstacle table (same version, pointer and size) keeps its grid
+    const bool go_build = go && !(obstacles_version != 0 && obstacles_version == c->grid_ver &&
+                                  obstacles == c->grid_src && n_obs == c->grid_n);
+    if (go_build || gn) {
+        hipLaunchKernelGGL(srb_grid_build_kernel, dim3(2), dim3(1024), 0, s,
+                           obstacles, 2, n_obs, go_build ? (SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
+                           nbr_state, 4, n_all, gn ? (SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
+        HIPCHK(hipGetLastError());
+    }
+    if (go_build) { c->grid_src = obstacles; c->grid_n = n_obs; c->grid_ver = obstacles_version; }
+    hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, x0, obstacles, n_obs,
+                       nbr_state, n_all, agent_offset, K_obs, K_nbr, sel,
+                       go ? (const SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
+                       gn ? (const SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
+    HIPCHK(hipGetLastError());
+    return SRB_OK;
+}
+
+int srb_internal_select(srb_ctx *c, int n_agents, const double *x0, const double *obstacles, int n_obs,
+                        const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
+                        int obstacles_version, int *sel, hipStream_t s)
+{
+    return launch_select(c, n_agents, x0, obstacles, n_obs, nbr_state, n_all, agent_offset, K_obs, K_nbr,
+                         obstacles_version, sel, s);
+}
+
 static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, int use_nlp)
 {
     if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
@@ -367,33 +412,9 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
     int *sel = d->sel ? d->sel : c->sel;
     if (use_nlp && k.K_obs + k.K_nbr > 0) {
-        // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
-        // with the arena) get a uniform grid so each agent scans only the cells around it
-        // (a versioned static obstacle table builds its grid once, so it pays off at fewer rows;
-        // SRB_GRID_MIN_ROWS overrides both thresholds)
-        static const char *env_rows = std::getenv("SRB_GRID_MIN_ROWS");
-        static const int min_rows = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS;
-        static const int min_rows_static = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS_STATIC;
-        const bool go = k.K_obs > 0 && n_obs >= (d->obstacles_version != 0 ? min_rows_static : min_rows);
-        const bool gn = k.K_nbr > 0 && n_all >= min_rows;
-        if (go) { int rc = grid_reserve(c, 0, n_obs); if (rc) return rc; }
-        if (gn) { int rc = grid_reserve(c, 1, n_all); if (rc) return rc; }
-        const srb_ctx::grid_buf &G0 = c->grid[0], &G1 = c->grid[1];
-        // a static obstacle table (same version, pointer and size) keeps its grid
-        const bool go_build = go && !(d->obstacles_version != 0 && d->obstacles_version == c->grid_ver &&
-                                      d->obstacles == c->grid_src && n_obs == c->grid_n);
-        if (go_build || gn) {
-            hipLaunchKernelGGL(srb_grid_build_kernel, dim3(2), dim3(1024), 0, s,
-                               d->obstacles, 2, n_obs, go_build ? (SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
-                               d->nbr_state, 4, n_all, gn ? (SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
-            HIPCHK(hipGetLastError());
-        }
-        if (go_build) { c->grid_src = d->obstacles; c->grid_n = n_obs; c->grid_ver = d->obstacles_version; }
-        hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, d->x0, d->obstacles, n_obs,
-                           d->nbr_state, n_all, d->agent_offset, k.K_obs, k.K_nbr, sel,
-                           go ? (const SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
-                           gn ? (const SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
-        HIPCHK(hipGetLastError());
+        int rc = launch_select(c, n_agents, d->x0, d->obstacles, n_obs, d->nbr_state, n_all, d->agent_offset, k.K_obs,
+                               k.K_nbr, d->obstacles_version, sel, s);
+        if (rc) return rc;
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
     // the solve kernel, then (NLP stage) the active-set polish of its result (srb_polish_kernel,

@@ -134,3 +134,29 @@ struct SrbLLKParams {
 // leading dimensions
 #define SRB_LL_NQ 18   // TOTAL_DOF (global_loco_opts.h:24)
 #define SRB_LL_NU 12   // TOTAL_IN  (global_loco_opts.h:25)
+
+// ---- SRB-12 extension mode (srb12_kernels.hip; the north star's 12-state single rigid body,
+// declared but never implemented by the reference, include/fast_MPC.hpp:98-103)
+struct Srb12KParams {
+    int N, K_obs, K_nbr, use_nlp;
+    int qp_maxit, nlp_maxit;
+    double Ts, mass, grav, mus, fmax, Sw, eps_obs, eps_nbr, tol, z0;
+    double Ib[9];                     // body inertia (fast_MPC.cpp:41-43)
+    double q[12], qN[12], r[3];       // stage / terminal state weights, force weights
+    int dbg_agent;                    // >= 0: that agent records a per-iteration trace into dbg
+    double *dbg;                      // [2 stages][64 iterations][8] (srb12_debug_trace)
+};
+#define SRB12_MAX_N 24
+// row slots: 6 friction rows per (grid, leg) -- masked for swing legs -- then N K obstacle rows
+static inline int srb12_slots(int N, int K) { return 24 * N + N * K; }
+// doubles of LDS one agent needs (the carve in srb12_kernels.hip)
+static inline int srb12_lds_doubles(int N, int K)
+{
+    return 36 * N + 2 * N + 4 * N + 144 * N + 156 * N     // W_l, (cos, sin) psi, contact, Hu^-1, Hux (12 x 13) per grid
+           + 2 * 169 + 169 + 2 * 156                    // V ping-pong, G (13 x 13), F, M
+           + 6 * N + 24 * N                             // (p_x, p_y, s) blocks, force blocks
+           + (24 * N + 4) + 12 * N + 13 * N + 12 * N    // iterate (X | U | s), reference, gradients
+           + 2 * 13 * N + 2 * 12 * N + 2 * 13 * N + 2 * 12 * N + 2 * 12 * N   // rhs / solution / gu columns (solve, refinement)
+           + 32 + 16 + 16                               // vectors, scalars, costates
+           + 2 * N * K + 2 * K + 2;                     // obstacle positions, eps, sel (as ints)
+}

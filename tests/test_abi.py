@@ -15,7 +15,7 @@ from srbnmpc import workload
 def _declared_functions():
     txt = open(os.path.join(ROOT, "include", "srbnmpc.h")).read()
     txt = re.sub(r"/\*.*?\*/", "", txt, flags=re.S)
-    return sorted(set(re.findall(r"\b(srb_\w+)\s*\(", txt)))
+    return sorted(set(re.findall(r"\b(srb(?:12)?_\w+)\s*\(", txt)))
 
 
 def test_library_exports_every_declared_symbol():

@@ -1,0 +1,236 @@
+"""SRB-12 extension mode: the north star's 12-state single-rigid-body
+CBF-NMPC.  The reference declares it (include/fast_MPC.hpp:98-103) and implements nothing, so
+parity with the reference is UNPINNED; the oracle (oracle/srb12.c) is pinned by a
+solver-independent KKT certificate and an independent numpy restatement of the model, and the
+GPU kernel (csrc/srb12_kernels.hip, a Riccati-based interior-point method) is checked against
+the oracle (dense full-space LU, the same iteration)."""
+import numpy as np
+import pytest
+
+import oracle
+from kkt import certify
+from srbnmpc import srb12, workload
+
+N = 10
+
+
+def _batch(A, gait, seed, Kn=8):
+    b = workload.make_batch12(A, N, gait, seed=seed)
+    p = oracle.params12(N, K_obs=3, K_nbr=Kn)
+    return b, p
+
+
+def _model_numpy(p, x0, xref, foot, contact):
+    """Independent restatement of the SRB-12 linearisation (srb12.c header): A_k, B_k, c_k."""
+    Ib = np.array(p.Ib).reshape(3, 3)
+    As, Bs, cs = [], [], []
+    for k in range(p.N):
+        ph = x0 if k == 0 else xref[k - 1]
+        c, s = np.cos(ph[5]), np.sin(ph[5])
+        Rz = np.array([[c, -s, 0], [s, c, 0], [0, 0, 1.0]])
+        Iwi = np.linalg.inv(Rz @ Ib @ Rz.T)
+        A = np.eye(12)
+        A[0:3, 6:9] += p.Ts * np.eye(3)
+        A[3:6, 9:12] += p.Ts * Rz.T
+        B = np.zeros((12, 12))
+        for l in range(4):
+            if contact[k, l]:
+                r = foot[k, l] - ph[:3]
+                S = np.array([[0, -r[2], r[1]], [r[2], 0, -r[0]], [-r[1], r[0], 0]])
+                B[6:9, 3 * l:3 * l + 3] = p.Ts / p.mass * np.eye(3)
+                B[9:12, 3 * l:3 * l + 3] = p.Ts * Iwi @ S
+        cc = np.zeros(12)
+        cc[8] = -p.Ts * p.grav
+        As.append(A); Bs.append(B); cs.append(cc)
+    return np.array(As), np.array(Bs), np.array(cs)
+
+
+def _problem(p, x0, xref, foot, contact, obs, eps):
+    """Full-space problem in numpy for the KKT certificate: Pd, c, Aeq, beq, g_and_J, h."""
+    Nn = p.N
+    n = 24 * Nn + 1
+    A, B, cvec = _model_numpy(p, x0, xref, foot, contact)
+    Pd = np.zeros(n); c = np.zeros(n)
+    for k in range(Nn):
+        w = np.array(p.qN if k == Nn - 1 else p.q)
+        Pd[12 * k:12 * k + 12] = w; c[12 * k:12 * k + 12] = -w * xref[k]
+        Pd[12 * Nn + 12 * k:12 * Nn + 12 * k + 12] = np.tile(np.array(p.r), 4)
+    Pd[-1] = p.Sw
+    Aeq = np.zeros((12 * Nn, n)); beq = np.zeros(12 * Nn)
+    for k in range(Nn):
+        Aeq[12 * k:12 * k + 12, 12 * k:12 * k + 12] = np.eye(12)
+        if k > 0:
+            Aeq[12 * k:12 * k + 12, 12 * (k - 1):12 * k] = -A[k]
+        Aeq[12 * k:12 * k + 12, 12 * Nn + 12 * k:12 * Nn + 12 * k + 12] = -B[k]
+        beq[12 * k:12 * k + 12] = cvec[k] + (A[0] @ x0 if k == 0 else 0)
+    mus = p.mu / np.sqrt(2)
+    gc = np.array([[1, 0, -mus], [-1, 0, -mus], [0, 1, -mus], [0, -1, -mus], [0, 0, -1], [0, 0, 1.0]])
+    G, h = [], []
+    for k in range(Nn):
+        for l in range(4):
+            if contact[k, l]:
+                for q in range(6):
+                    row = np.zeros(n)
+                    row[12 * Nn + 12 * k + 3 * l:12 * Nn + 12 * k + 3 * l + 3] = gc[q]
+                    G.append(row); h.append(p.fmax if q == 5 else 0.0)
+    G = np.array(G); h = np.array(h)
+    K = obs.shape[1]
+
+    def g_and_J(x):
+        go = np.zeros(Nn * K); Jo = np.zeros((Nn * K, n))
+        for k in range(Nn):
+            for j in range(K):
+                r = k * K + j
+                dx = x[12 * k] - obs[k, j, 0]; dy = x[12 * k + 1] - obs[k, j, 1]
+                go[r] = -(dx * dx + dy * dy) - x[-1]
+                Jo[r, 12 * k] = -2 * dx; Jo[r, 12 * k + 1] = -2 * dy; Jo[r, -1] = -1
+        return np.concatenate([G @ x, go]), np.vstack([G, Jo])
+
+    hh = np.concatenate([h, -np.repeat(np.asarray(eps)[None], Nn, 0).ravel()])
+    return Pd, c, Aeq, beq, g_and_J, hh
+
+
+def _obs_for(p, b, a):
+    op = oracle.params(p.N, 2, K_obs=p.K_obs, K_nbr=p.K_nbr, Ts=p.Ts, eps_obs=p.eps_obs, eps_nbr=p.eps_nbr)
+    x = b["x0"][a]
+    return oracle.select_obstacles(op, np.array([x[0], x[6], x[1], x[7]]), b["obstacles"], b["nbr_state"], a)
+
+
+def test_srb12_model_matches_numpy_restatement():
+    b, p = _batch(6, "trot", 3)
+    for a in range(6):
+        A, B, c = oracle.dynamics12(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a])
+        An, Bn, cn = _model_numpy(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a])
+        np.testing.assert_allclose(A, An, atol=1e-14)
+        np.testing.assert_allclose(B, Bn, atol=1e-12)
+        np.testing.assert_allclose(c, cn, atol=1e-15)
+
+
+@pytest.mark.parametrize("gait", ["trot", "stand"])
+def test_srb12_oracle_kkt_certificate(gait):
+    """The oracle's QP and NLP points are KKT points of the stated problem (certificate with its
+    own multipliers, bounded least squares; no solver trusted)."""
+    b, p = _batch(8, gait, 11)
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    assert (r["status"] == 0).all(), r["status"]
+    for a in range(8):
+        obs, eps = _obs_for(p, b, a)
+        Pd, c, Aeq, beq, gJ, hh = _problem(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a], obs, eps)
+        cert = certify(Pd, c, Aeq, beq, gJ, hh, r["x"][a])
+        assert cert["eq"] < 1e-9 and cert["prim"] < 1e-7, cert
+        assert cert["stat_rel"] < 1e-6, cert
+        # the dynamics hold and the swing legs carry no force
+        X, U = r["x"][a, :12 * N].reshape(N, 12), r["x"][a, 12 * N:24 * N].reshape(N, 4, 3)
+        assert np.abs(U[b["contact"][a] == 0]).max(initial=0.0) < 1e-9
+
+
+def test_srb12_oracle_qp_stage_is_optimal_without_obstacle_rows():
+    b, p = _batch(6, "trot", 5)
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    empty = np.zeros((N, 0, 2))
+    for a in range(6):
+        Pd, c, Aeq, beq, gJ, hh = _problem(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a], empty, [])
+        cert = certify(Pd, c, Aeq, beq, gJ, hh, r["x_qp"][a])
+        assert cert["stat_rel"] < 1e-6 and cert["prim"] < 1e-7 and cert["eq"] < 1e-9, cert
+
+
+def test_srb12_params_defaults_match_oracle():
+    """srb12_params_default (C ABI, no GPU) == the oracle's defaults; reference constants."""
+    pg = srb12.default_params(N)
+    po = oracle.params12(N)
+    for k, _ in srb12.Params12._fields_:
+        a, o = getattr(pg, k), getattr(po, k)
+        if hasattr(a, "__len__"):
+            assert list(a) == list(o), k
+        else:
+            assert a == o, k
+    assert pg.mass == 12.453 and abs(pg.Ib[0] - 0.01683993) < 1e-15      # fast_MPC.cpp:40-43
+    assert pg.mu == 0.7 and list(pg.q) == [1e3] * 12 and list(pg.r) == [1e-2] * 3   # Parameters.cpp:32-52
+    assert 0 < srb12.lds_bytes(pg) <= 160 * 1024
+
+
+# ------------------------------------------------------------------------------------------- GPU
+def _gpu():
+    torch = pytest.importorskip("torch")
+    if not torch.cuda.is_available():
+        pytest.skip("no GPU")
+    return torch
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("gait", ["trot", "stand"])
+def test_srb12_gpu_vs_oracle(gait):
+    _gpu()
+    A = 64
+    b, p = _batch(A, gait, 21)
+    s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
+    out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    s.close()
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    assert (r["status"] == 0).all()
+    assert (out["status"] == r["status"]).all(), [(a, out["status"][a].tolist(), r["status"][a].tolist())
+                                                   for a in range(A) if (out["status"][a] != r["status"][a]).any()]
+    same_it = (out["iters"] == r["iters"]).all(1).mean()
+    assert same_it >= 0.9, same_it
+    X, Xo = out["x"][:, :12 * N], r["x"][:, :12 * N]
+    U, Uo = out["x"][:, 12 * N:24 * N], r["x"][:, 12 * N:24 * N]
+    ex, eu, es = np.abs(X - Xo).max(), np.abs(U - Uo).max(), np.abs(out["x"][:, -1] - r["x"][:, -1]).max()
+    assert ex < 1e-6 and eu < 1e-3 and es < 1e-6, (ex, eu, es)
+    np.testing.assert_allclose(out["x_qp"][:, :12 * N], r["x_qp"][:, :12 * N], atol=1e-6)
+    np.testing.assert_allclose(out["obj"], r["obj"], rtol=1e-8)
+    # the selection is the LIP mode's (oracle.select_idx on the CoM position / velocity)
+    op = oracle.params(N, 2, K_obs=3, K_nbr=8)
+    for a in range(0, A, 7):
+        x = b["x0"][a]
+        want = oracle.select_idx(op, np.array([x[0], x[6], x[1], x[7]]), b["obstacles"], b["nbr_state"], a)
+        np.testing.assert_array_equal(out["sel"][a], want)
+
+
+@pytest.mark.gpu
+def test_srb12_device_entry_equals_host_entry():
+    torch = _gpu()
+    A = 128
+    b, _ = _batch(A, "trot", 4)
+    prm = srb12.default_params(N, K_obs=3, K_nbr=8)
+    s = srb12.Solver12(prm, A)
+    h = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    dev = torch.device("cuda:0")
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    o = dict(x_qp=torch.zeros((A, prm.nv), dtype=torch.float64, device=dev),
+             x=torch.zeros((A, prm.nv), dtype=torch.float64, device=dev),
+             obj=torch.zeros(A, dtype=torch.float64, device=dev),
+             status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+             iters=torch.zeros((A, 2), dtype=torch.int32, device=dev))
+    s.solve_device(T(b["x0"]), T(b["xref"]), T(b["foot"]), T(b["contact"], torch.int32), T(b["obstacles"]),
+                   T(b["nbr_state"]), o)
+    torch.cuda.synchronize()
+    s.close()
+    for k in ("x_qp", "x", "obj", "status", "iters"):
+        np.testing.assert_array_equal(o[k].cpu().numpy(), h[k], err_msg=k)
+
+
+@pytest.mark.gpu
+def test_srb12_full_size_properties():
+    """1024 agents (the configs[2] swarm size): statuses, dynamics, friction pyramid, force bound,
+    obstacle rows, swing legs at zero -- every agent."""
+    _gpu()
+    A = 1024
+    b, p = _batch(A, "trot", 8)
+    s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
+    out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    s.close()
+    assert (out["status"] == 0).all(1).mean() >= 0.99, np.bincount(out["status"][:, 1])
+    X, U, sl = srb12.split(p, out["x"])
+    mus = p.mu / np.sqrt(2)
+    ok = (out["status"] == 0).all(1)
+    for a in np.where(ok)[0][:256]:
+        Am, Bm, cm = oracle.dynamics12(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a])
+        prev = b["x0"][a]
+        for k in range(N):
+            assert np.abs(Am[k] @ prev + Bm[k] @ U[a, k].ravel() + cm[k] - X[a, k]).max() < 1e-8
+            prev = X[a, k]
+    st = b["contact"] == 1
+    f = U[st]
+    assert (np.abs(f[:, 0]) - mus * f[:, 2]).max() < 1e-7 and (np.abs(f[:, 1]) - mus * f[:, 2]).max() < 1e-7
+    assert f[:, 2].min() > -1e-7 and f[:, 2].max() < p.fmax + 1e-7
+    assert np.abs(U[~st]).max() < 1e-9
