@@ -211,7 +211,8 @@ def main_ll(args, world, rank, local_rank, dev):
         "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
         "optimal_frac": float((status == 0).mean()), "iters_mean": float(iters.mean()),
         "roofline": {"bound": "mfma", "achieved": achieved, "peak": FP64_PEAK_TFLOPS, "unit": "TFLOP/s",
-                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "srb_ll_kernel",
+                     "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic_from("ll", n_loc)[0],
+                     "traffic_source": traffic_from("ll", n_loc)[1], "kernel": "srb_ll_kernel",
                      "kernel_ms": kms, "flop_model": "bench.ll_executed_flops (DESIGN.md 6b); latency-bound",
                      "io_bytes_per_launch": io, "hbm_GBps": io / (kms * 1e-3) / 1e9},
         "cpu_baseline": None,
@@ -246,6 +247,19 @@ def srb12_executed_flops(N, K, iters):
     rows = 40 * (24 * N + N * K)
     it = N * (fac + 4 * sol) + rows
     return float(np.sum(iters.sum(1) * it))
+
+
+def traffic_from(name, agents):
+    """roofline.traffic of a non-default path: hbm bytes per launch of its PMC summary
+    (tools/pmc_traffic.py, profiles/r03_pmc_traffic_<name>.json) when it matches the batch."""
+    f = os.path.join(ROOT, "profiles", f"r03_pmc_traffic_{name}.json")
+    try:
+        tj = json.load(open(f))
+        if tj.get("agents") in (agents, 0):
+            return tj.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+    except Exception:
+        pass
+    return None, None
 
 
 def main_srb12(args, world, rank, local_rank, dev):

@@ -19,7 +19,7 @@ import os
 import statistics
 import sys
 
-KERNELS = ("srb_nmpc_kernel", "srb_polish_kernel", "srb_knn_kernel", "srb_grid_build_kernel", "srb_ll_kernel",
+KERNELS = ("srb_nmpc_kernel", "srb_polish_kernel", "srb12_kernel", "srb12_pos_kernel", "srb_knn_kernel", "srb_grid_build_kernel", "srb_ll_kernel",
            "calib_read8", "calib_read16", "calib_write8")
 
 
@@ -69,7 +69,7 @@ def traffic(fdir, wdir, cfg, agents, out, calib_json=None):
             e["write_bytes"] = wv / cal["write_units_per_byte_write8"]
             e["hbm_bytes"] = e["fetch_bytes"] + e["write_bytes"]
         kern[fam] = e
-    solve = kern.get("srb_nmpc_kernel", {})
+    solve = kern.get("srb_nmpc_kernel", kern.get("srb12_kernel", kern.get("srb_ll_kernel", {})))
     d = {"config": int(cfg) if cfg.lstrip("-").isdigit() else cfg, "agents": int(agents), "kernels": kern,
          "hbm_bytes_per_launch": solve.get("hbm_bytes"),
          "calibration": calib_json,
