@@ -129,14 +129,6 @@ __device__ __forceinline__ int sym3(int a, int b)
     return (i == 0) ? j : (i == 1) ? 2 + j : 5;
 }
 
-__device__ __forceinline__ double pick4(const double (&M)[12], int kk, int q)
-{
-    // M[4 kk + q] with q lane-dependent (0..3); entries >= 12 are 0
-    const int b = 4 * kk;
-    const double v0 = (b + 0 < 12) ? M[(b + 0) % 12] : 0.0, v1 = (b + 1 < 12) ? M[(b + 1) % 12] : 0.0;
-    const double v2 = (b + 2 < 12) ? M[(b + 2) % 12] : 0.0, v3 = (b + 3 < 12) ? M[(b + 3) % 12] : 0.0;
-    return q == 0 ? v0 : q == 1 ? v1 : q == 2 ? v2 : v3;
-}
 
 } // namespace
 
@@ -343,20 +335,31 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 gm = fmax(gm, fabs(prm.r[i % 3] * U[e]));
             }
             gm = fmax(gm, fabs(prm.Sw * L.Z[24 * N]));
-            if (tid < 13) L.lam[tid] = L.gX[13 * (N - 1) + tid];
-            SYNC();
-            for (int k = N - 1; k >= 0; k--) {
-                double ln = 0.0;
-                if (tid < 12) {
-                    const double ru = L.gU[12 * k + tid] + bt_mul(tid, L.lam, L.Wl + 36 * k, L.ct + 4 * k, tsm);
-                    nrd = fma(ru, ru, nrd);
+            {
+                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
+                double lam = (i < 13) ? L.gX[13 * (N - 1) + i] : 0.0;
+                for (int k = N - 1; k >= 0; k--) {
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+                    double vb[13];
+#pragma unroll
+                    for (int j = 0; j < 13; j++) vb[j] = bc16(lam, j);
+                    if (lane < 12) {
+                        double ru = L.gU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
+                        for (int a = 0; a < 3; a++) ru = fma(W[9 * l + 3 * a + jj], vb[9 + a], ru);
+                        nrd = fma(ru, ru, nrd);
+                    }
+                    if (k > 0) {
+                        const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                        double ln = lam;
+                        if (i >= 6 && i < 9) ln = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], ln);
+                        else if (i >= 9 && i < 12)
+                            ln = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], ln);
+                        lam = (i < 13) ? ln + L.gX[13 * (k - 1) + i] : 0.0;
+                    }
                 }
-                if (k > 0 && tid < 13) ln = L.gX[13 * (k - 1) + tid] + at13(tid, L.lam, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
-                SYNC();
-                if (k > 0 && tid < 13) L.lam[tid] = ln;
-                SYNC();
+                const double l12 = bc16(lam, 12);
+                if (tid == 0) { const double rs = L.sc[0] + l12; nrd = fma(rs, rs, nrd); }
             }
-            if (tid == 0) { const double rs = L.sc[0] + L.lam[12]; nrd = fma(rs, rs, nrd); }
             {
                 double rv[4] = {nrd, nrp, sz, gm};
                 wred<4, 8u>(rv);
@@ -528,68 +531,86 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             if (!ok) { flag = 1; break; }
             // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
-            // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free)
+            // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
+            // Vectors live in registers, component i = lane & 15 (each 16-lane row holds a copy), and move
+            // between lanes by DPP row broadcasts: no LDS round trip or barrier inside the recursion.
             auto riccati_solve = [&](int c) {
-                const int i = lane;
+                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
                 const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
-                double *dX = L.dX + 13 * N * c, *dU = L.dU + 12 * N * c, *gus = L.gus + 12 * N * c;
-                double *v = L.vv, *pv = L.vv + 16;
-                if (i < 13) v[i] = rX[13 * (N - 1) + i];
-                SYNC();
+                double *dX = L.dX + 13 * N * c, *dU = L.dU + 12 * N * c, *gus = L.gus;
+                double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
                 for (int k = N - 1; k >= 0; k--) {
-                    if (i < 12) gus[12 * k + i] = rU[12 * k + i] + bt_mul(i, v, L.Wl + 36 * k, L.ct + 4 * k, tsm);
-                    SYNC();
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hx = L.Hx + 156 * k;
+                    double vb[13];
+#pragma unroll
+                    for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
+                    double gu = 0.0;
                     if (i < 12) {
-                        const double *Lr = L.Lm + 144 * k + 12 * i;
-                        double kk = 0.0;
-                        for (int j = 0; j < 12; j++) kk = fma(-Lr[j], gus[12 * k + j], kk);
-                        dU[12 * k + i] = kk;
+                        gu = rU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
+                        for (int a = 0; a < 3; a++) gu = fma(W[9 * l + 3 * a + jj], vb[9 + a], gu);
                     }
-                    SYNC();
-                    double vn = 0.0;
-                    if (i < 13) {
-                        vn = ((k > 0) ? rX[13 * (k - 1) + i] : 0.0) + at13(i, v, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
-                        const double *Hx = L.Hx + 156 * k;
-                        for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], dU[12 * k + j], vn);
-                    }
-                    SYNC();
-                    if (i < 13) v[i] = vn;
-                    SYNC();
+                    if (lane < 12) gus[12 * k + i] = gu;
+                    double kk = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) kk = fma(-Lr[j], bc16(gu, j), kk);
+                    if (i >= 12) kk = 0.0;
+                    const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                    double vn = v;                                     // A~' v
+                    if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], vn);
+                    else if (i >= 9 && i < 12)
+                        vn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], vn);
+                    if (k > 0 && i < 13) vn += rX[13 * (k - 1) + i];
+                    if (i < 13)
+#pragma unroll
+                        for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], bc16(kk, j), vn);
+                    v = (i < 13) ? vn : 0.0;
                 }
-                const double ds0 = -(v[12] + L.sc[2 + c]) / schur;
-                if (i < 13) pv[i] = (i == 12) ? ds0 : 0.0;
-                SYNC();
+                const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
+                double prev = (i == 12) ? ds0 : 0.0;
                 for (int k = 0; k < N; k++) {
                     // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
-                    const double *prev = (k == 0) ? pv : dX + 13 * (k - 1);
-                    if (i < 12) {
-                        const double *Hr = L.Hx + 156 * k + 13 * i;
-                        double t = gus[12 * k + i];
-                        for (int j = 0; j < 13; j++) t = fma(Hr[j], prev[j], t);
-                        v[i] = t;
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hr = L.Hx + 156 * k + 13 * ir;
+                    double pb[13];
+#pragma unroll
+                    for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
+                    double t = gus[12 * k + ir];
+#pragma unroll
+                    for (int j = 0; j < 13; j++) t = fma(Hr[j], pb[j], t);
+                    if (i >= 12) t = 0.0;
+                    double du = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) du = fma(-Lr[j], bc16(t, j), du);
+                    if (i >= 12) du = 0.0;
+                    if (lane < 12) dU[12 * k + i] = du;
+                    double db[12];
+#pragma unroll
+                    for (int j = 0; j < 12; j++) db[j] = bc16(du, j);
+                    const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                    double dx = prev;
+                    if (i < 3) dx = fma(Ts, i == 0 ? pb[6] : i == 1 ? pb[7] : pb[8], dx);
+                    else if (i < 6)
+                        dx = fma(Ts, i == 3 ? fma(cc, pb[9], sn * pb[10]) : i == 4 ? fma(-sn, pb[9], cc * pb[10]) : pb[11], dx);
+                    else if (i < 9) {
+                        for (int ll = 0; ll < 4; ll++) dx = fma(ct[ll] * tsm, i == 6 ? db[3 * ll] : i == 7 ? db[3 * ll + 1] : db[3 * ll + 2], dx);
+                    } else if (i < 12) {
+                        const int a = i - 9;
+                        for (int ll = 0; ll < 4; ll++)
+                            for (int j = 0; j < 3; j++) dx = fma(W[9 * ll + 3 * a + j], db[3 * ll + j], dx);
                     }
-                    SYNC();
-                    if (i < 12) {
-                        const double *Lr = L.Lm + 144 * k + 12 * i;
-                        double du = 0.0;
-                        for (int j = 0; j < 12; j++) du = fma(-Lr[j], v[j], du);
-                        dU[12 * k + i] = du;
-                    }
-                    SYNC();
-                    if (i < 13)
-                        dX[13 * k + i] = a13(i, prev, Ts, L.cs[2 * k], L.cs[2 * k + 1]) +
-                                         ((i < 12) ? b_mul(i, dU + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm) : 0.0);
-                    SYNC();
+                    if (i > 12) dx = 0.0;
+                    if (lane < 13) dX[13 * k + i] = dx;
+                    prev = dx;
                 }
+                SYNC();
             };
             // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
             // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
             // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s).
             // Explicit Gauss-Jordan inverses lose digits once z / s reaches 1e7 on active rows.
             auto refine = [&](double delta) {
-                const int i = lane;
+                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
                 const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
-                double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N, *mu = L.vv;
+                double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N;
                 auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
                     double v = 0.0;
                     for (int j = 0; j < 13; j++) {
@@ -598,24 +619,32 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                     }
                     return v;
                 };
-                if (i < 13) mu[i] = qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i];
                 for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
-                SYNC();
+                double m = (i < 13) ? qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i] : 0.0;
                 for (int k = N - 1; k >= 0; k--) {
-                    double mn = 0.0;
-                    if (i < 12) {
-                        const int l = i / 3, a = i - 3 * l;
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+                    double vb[13];
+#pragma unroll
+                    for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
+                    if (lane < 12) {
                         const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                        double t = fma(prm.r[a] + delta, du[a], rU[12 * k + i]);
-                        for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a, bb)], du[bb], t);
-                        tU[12 * k + i] = t + bt_mul(i, mu, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+                        double t = fma(prm.r[a3] + delta, du[a3], rU[12 * k + i]);
+                        for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
+                        t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
+                        for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
+                        tU[12 * k + i] = t;
                     }
-                    if (k > 0 && i < 13) mn = qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] + at13(i, mu, Ts, L.cs[2 * k], L.cs[2 * k + 1]);
-                    SYNC();
-                    if (k > 0 && i < 13) mu[i] = mn;
-                    SYNC();
+                    if (k > 0) {
+                        const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                        double mn = m;
+                        if (i >= 6 && i < 9) mn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], mn);
+                        else if (i >= 9 && i < 12)
+                            mn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], mn);
+                        m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] : 0.0;
+                    }
                 }
-                if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + mu[12];
+                const double m12 = bc16(m, 12);
+                if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + m12;
                 SYNC();
                 riccati_solve(1);
                 for (int e = tid; e < 13 * N; e += 64) L.dX[e] += L.dX[13 * N + e];
@@ -687,9 +716,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
             };
             // ---- predictor
+            // (the refinement only near the optimum, mu < 1e-3: far from it the step's accuracy is not
+            // what limits progress, and it costs a solve)
+            const bool refn = mu < 1e-3;
             build_rhs(0, 0.0);
             riccati_solve(0);
-            refine(delta);
+            if (refn) refine(delta);
             double dsl[TS], dzl[TS];
             double2 al = row_step(0, 0.0, dsl, dzl);
 #pragma unroll
@@ -709,7 +741,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // ---- corrector
             build_rhs(1, sigma * mu);
             riccati_solve(0);
-            refine(delta);
+            if (refn) refine(delta);
             al = row_step(1, sigma * mu, dsl, dzl);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);
             if (dbgrow && tid == 0) { dbgrow[4] = ap; dbgrow[5] = ad; dbgrow[6] = delta; dbgrow[7] = sigma; }

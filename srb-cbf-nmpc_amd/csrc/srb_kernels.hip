@@ -459,25 +459,35 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
 // the vanishing curvature along it near convergence (both lambda bounds inactive) is held
 // exactly in Z'HZ instead of emerging from cancellation between O(1e3) terms.
 // Returns 1 when column t is that null column (lam holds it), 0 otherwise.
-__device__ __forceinline__ int lambda_basis(const double *F, int C, int t, double lam[4])
+// (every index into lam / nvec is a compile-time constant after unrolling: a runtime index would put
+// these arrays in scratch memory, 48 B per lane written back to HBM by every launch)
+__device__ __forceinline__ int lambda_basis(const double *F, int C, int t, double (&lam)[4])
 {
-    for (int i = 0; i < 4; i++) lam[i] = 0.0;
-    if (C != 4) { lam[t] = 1.0; lam[C - 1] = -1.0; return 0; }
+    if (C != 4) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) lam[i] = (i == t) ? 1.0 : (i == C - 1) ? -1.0 : 0.0;
+        return 0;
+    }
     double nvec[4];
+#pragma unroll
     for (int i = 0; i < 4; i++) {
-        int cidx[3], q = 0;
-        for (int k = 0; k < 4; k++) if (k != i) cidx[q++] = k;
+        const int c0 = (i == 0) ? 1 : 0, c1 = (i <= 1) ? 2 : 1, c2 = (i <= 2) ? 3 : 2;
         const double *r0 = F, *r1 = F + 4;
-        double det = r0[cidx[0]] * (r1[cidx[1]] - r1[cidx[2]]) - r0[cidx[1]] * (r1[cidx[0]] - r1[cidx[2]]) +
-                     r0[cidx[2]] * (r1[cidx[0]] - r1[cidx[1]]);
+        double det = r0[c0] * (r1[c1] - r1[c2]) - r0[c1] * (r1[c0] - r1[c2]) + r0[c2] * (r1[c0] - r1[c1]);
         nvec[i] = (i & 1) ? -det : det;
     }
     int istar = 0;
-    for (int i = 1; i < 3; i++) if (fabs(nvec[i]) > fabs(nvec[istar])) istar = i;
-    double sc = 1.0 / nvec[istar];
-    if (t == 2) { for (int i = 0; i < 4; i++) lam[i] = nvec[i] * sc; return 1; }
-    int i = (t < istar) ? t : t + 1;
-    lam[i] = 1.0; lam[3] = -1.0;
+    if (fabs(nvec[1]) > fabs(nvec[istar])) istar = 1;
+    if (fabs(nvec[2]) > fabs(istar == 1 ? nvec[1] : nvec[0])) istar = 2;
+    const double sc = 1.0 / (istar == 0 ? nvec[0] : istar == 1 ? nvec[1] : nvec[2]);
+    if (t == 2) {
+#pragma unroll
+        for (int i = 0; i < 4; i++) lam[i] = nvec[i] * sc;
+        return 1;
+    }
+    const int ii = (t < istar) ? t : t + 1;
+#pragma unroll
+    for (int j = 0; j < 4; j++) lam[j] = (j == ii) ? 1.0 : (j == 3) ? -1.0 : 0.0;
     return 0;
 }
 
@@ -688,8 +698,9 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
         const int is_null = lambda_basis(foot + j * 2 * C, C, t, lam); \
         double g0 = 0.0, g1 = 0.0; \
         if (!is_null) \
-            for (int i = 0; i < C; i++) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; } \
-        for (int i = 0; i < C; i++) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i]; \
+            _Pragma("unroll") for (int i = 0; i < 4; i++) \
+                if (i < C) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; } \
+        _Pragma("unroll") for (int i = 0; i < 4; i++) if (i < C) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i]; \
         R[TL.zr(4 * N + 2 * j) * LDR + col] = g0; \
         R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = g1; \
         double v[4]; \
