@@ -1060,15 +1060,16 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             STAMP_END(3);
             if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
             // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
-            const double thx = nl ? th * gm : th;
+            const double thx = nl ? SRB_NLP_EXITF * th * gm : th;
+            const double mtol = nl ? SRB_NLP_EXITF * tol : tol;
             NLPDBG(iter, 0, nrx); NLPDBG(iter, 1, thx); NLPDBG(iter, 2, nrz); NLPDBG(iter, 3, sz * inv_m);
-            const bool pass = nrx < thx && nrz < th && sz * inv_m < tol;
+            const bool pass = nrx < thx && nrz < th && sz * inv_m < mtol;
             if (pass && (!nl || dxm < SRB_NLP_DXTOL)) { flag = 0; break; }
             // NLP near the optimum (primal and complementarity met, dual residual within 100x):
             // an inertia shift or a blocked step from here is round-off of the condensed
             // system (W = z/s ~ 1e14 swamps the soft curvature in Z'HZ), not progress -> exit
             // ACCEPTABLE (4) at this iterate (oracle/nlp_ipm.c, the same rule)
-            const bool near = nl && nrz < th && sz * inv_m < tol && nrx < 100.0 * thx;
+            const bool near = nl && nrz < th && sz * inv_m < mtol && nrx < 100.0 * thx;
             // a solve that reached the near-optimal region and then left it is past its round-off
             // floor: ACCEPTABLE at the best near-optimal iterate (oracle, same rule)
             if (nl && saved && !near) { restore = true; flag = 4; break; }
@@ -1395,6 +1396,18 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 SYNC();                                      // xs of the previous step / pass
                 polish_rows<NZL, TS, NW>(P, nts, xs, OJ, zo, n, rO, R, nz);      // q.jd = g(x), M_o (OJ), zo = z_A
                 SYNC();                                      // R rows, zo
+                if (pit > 0) {                               // converged after a small step (oracle, same rule)
+                    double cm = 0.0;
+#pragma unroll
+                    for (int t = 0; t < TS; t++)
+                        if (t < nts) {
+                            const Slot &q = P[t];
+                            cm = fmax(cm, fmax(q.ds[0] * fabs(q.jd - q.h[0]), q.ds[1] * fabs(q.jd + q.h[1])));
+                        }
+                    double rv[1] = {cm};
+                    wred_x<1, 1u, NW>(rv, red + 6 * 8 * NW, tid);
+                    if (lastdx <= SRB_POLISH_DX1 && rv[0] <= SRB_POLISH_CTOL) { lastdx = 0.0; break; }
+                }
 #pragma unroll
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
