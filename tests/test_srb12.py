@@ -234,3 +234,61 @@ def test_srb12_full_size_properties():
     assert (np.abs(f[:, 0]) - mus * f[:, 2]).max() < 1e-7 and (np.abs(f[:, 1]) - mus * f[:, 2]).max() < 1e-7
     assert f[:, 2].min() > -1e-7 and f[:, 2].max() < p.fmax + 1e-7
     assert np.abs(U[~st]).max() < 1e-9
+
+
+@pytest.mark.gpu
+def test_srb12_shards_bit_identical_to_full_batch():
+    """An 8-way sharded swarm (each block solved with agent_offset against the whole snapshot, as
+    one rank of an 8-GPU run) gives bit-identical results to the single batch."""
+    torch = _gpu()
+    A = 256
+    b, _ = _batch(A, "trot", 13)
+    prm = srb12.default_params(N, K_obs=3, K_nbr=8)
+    s = srb12.Solver12(prm, A)
+    full = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    for lo in range(0, A, A // 8):
+        hi = lo + A // 8
+        part = s.solve(b["x0"][lo:hi], b["xref"][lo:hi], b["foot"][lo:hi], b["contact"][lo:hi], b["obstacles"],
+                       b["nbr_state"], agent_offset=lo)
+        for k in ("x", "x_qp", "status", "iters", "sel"):
+            np.testing.assert_array_equal(part[k], full[k][lo:hi], err_msg=k)
+    s.close()
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("Nh,Ko,Kn,use_nlp", [(20, 3, 8, 1), (6, 0, 0, 1), (10, 3, 8, 0)])
+def test_srb12_variants_vs_oracle(Nh, Ko, Kn, use_nlp):
+    """Horizon 20 (two slot trips more), no obstacle rows at all, and the QP stage alone."""
+    _gpu()
+    A = 32
+    b = workload.make_batch12(A, Nh, "trot", seed=31)
+    p = oracle.params12(Nh, K_obs=Ko, K_nbr=Kn, use_nlp=use_nlp)
+    s = srb12.Solver12(srb12.default_params(Nh, K_obs=Ko, K_nbr=Kn, use_nlp=use_nlp), A)
+    out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    s.close()
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    assert (r["status"] == 0).all() and (out["status"] == r["status"]).all()
+    np.testing.assert_allclose(out["x"][:, :12 * Nh], r["x"][:, :12 * Nh], atol=1e-6)
+    np.testing.assert_allclose(out["x"][:, 12 * Nh:], r["x"][:, 12 * Nh:], atol=1e-3)
+
+
+def test_srb12_abi_rejects_bad_arguments():
+    """Parameter validation and the struct_size check run without a GPU (no context needed)."""
+    import ctypes
+    L = srb12._lib()
+    b = srb12.Batch12()
+    b.struct_size = 4
+    assert L.srb12_solve_batch_device(None, 1, ctypes.byref(b), None) == -1
+    assert b"struct_size" in srbnmpc_last_error()
+    p = srb12.default_params(N)
+    p.N = 99
+    h = ctypes.c_void_p()
+    assert L.srb12_ctx_create(ctypes.byref(p), 4, 0, ctypes.byref(h)) == -3        # SRB_ERR_SIZE
+    p = srb12.default_params(N)
+    p.r[1] = 0.0
+    assert L.srb12_ctx_create(ctypes.byref(p), 4, 0, ctypes.byref(h)) == -1        # SRB_ERR_ARG
+
+
+def srbnmpc_last_error():
+    import srbnmpc
+    return srbnmpc.lib().srb_last_error()
