@@ -20,13 +20,12 @@
 //     Hessian blocks (the p_xy 2x2 block and the s border column of the obstacle rows, the 3x3
 //     friction blocks of each leg) by LDS atomics;
 //   * backward pass per grid: G = V A, F = V B (A, B applied through their structure: a few FMAs
-//     per entry), Hu = R^ + B'F inverted by the register Gauss-Jordan of the LIP kernel (its pivots
-//     are the reduced Hessian's LDL' pivots: the inertia test), Hux = B'G, and the Schur update
-//     V' = Q^ + A'G - Hux' (Hu^-1 Hux) as two 16x16x16 products on the matrix cores
-//     (v_mfma_f64_16x16x4f64: M = Hu^-1 Hux with Hu^-1 straight from the Gauss-Jordan registers,
-//     then Hux' M);
-//   * the global obstacle slack s borders the banded system: one extra right-hand side (the border
-//     column) per factorisation and a scalar Schur complement;
+//     per entry), Hu = R^ + B'F = L D L' by a register forward elimination of [Hu | Hux | I] (its
+//     pivots are the reduced Hessian's: the inertia test), Z = D^-1/2 L^-1 kept for the solves
+//     (Hu^-1 = Z'Z), and the Schur update V' = Q^ + A'G - Y'Y, Y = Z Hux, as a 16x16x16 product on
+//     the matrix cores (v_mfma_f64_16x16x4f64), positive semi-definite by construction;
+//   * the obstacle slack s rides along as a 13th state (s_{k+1} = s_k, s_0 free), so the stiff
+//     obstacle rows stay inside one grid's block;
 //   * the dual residual uses the costates of the backward recursion lambda_k = grad_x_k L +
 //     A_k' lambda_{k+1} (the state part of r_d is zero, the input part is the reduced gradient);
 //     the primal-dual step does not depend on them (oracle, same rule).
@@ -424,27 +423,6 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         L.Ft[e] = f;
                     }
                     SYNC();
-                    // Hu = R^ + B'F: row i16 of every 16-lane row (replicated for the Gauss-Jordan)
-                    double Mi[12];
-                    {
-                        const int i = lane & 15;
-                        const int li = (i < 12) ? i / 3 : 0, ai = (i < 12) ? i - 3 * li : 0;
-#pragma unroll
-                        for (int j = 0; j < 12; j++) {
-                            double v = 0.0;
-                            if (i < 12) {
-                                v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
-                                for (int a = 0; a < 3; a++) v = fma(W[9 * li + 3 * a + ai], L.Ft[12 * (9 + a) + j], v);
-                                if (j == i) v += prm.r[ai] + delta;
-                                if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
-                            }
-                            Mi[j] = v;
-                        }
-                    }
-                    fail |= gj_invert<12>(Mi, 12, lane, 0);
-                    if (lane < 12)
-#pragma unroll
-                        for (int j = 0; j < 12; j++) L.Lm[144 * k + 12 * lane + j] = Mi[j];
                     // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
                     // V_0[12][12] is used (the initial slack's Schur complement)
                     double *Hx = L.Hx + 156 * k, *Vn = cur ? L.V0 : L.V1;
@@ -466,14 +444,15 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         Vn[e] = w;
                     }
                     SYNC();
-                    // S = Hux' Hu^-1 Hux = Y'Y with Y = D^-1/2 L^-1 Hux (Hu = L D L'): forward elimination of
-                    // [Hu | Hux] in registers (row i16 per lane, replicated like the Gauss-Jordan), then the
-                    // 16x16x16 product Y'Y on the matrix cores.  The product with the explicit inverse,
-                    // Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on active rows; Y'Y is
-                    // positive semi-definite by construction.
+                    // Hu = R^ + B'F = L D L' by a forward elimination of [Hu | Hux | I] in registers (row i16
+                    // per lane, replicated in every 16-lane row): its pivots are the inertia test, Z = D^-1/2 L^-1
+                    // (stored: the solves apply Hu^-1 = Z'Z) and Y = Z Hux, so the Schur update
+                    // S = Hux' Hu^-1 Hux = Y'Y is one 16x16x16 product on the matrix cores.  The product with
+                    // an explicit inverse, Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on
+                    // active rows; Y'Y is positive semi-definite by construction.
                     {
                         const int i16 = lane & 15, q = lane >> 4;
-                        double Ag[25];
+                        double Ag[37];
                         {
                             const int li = (i16 < 12) ? i16 / 3 : 0, ai = (i16 < 12) ? i16 - 3 * li : 0;
 #pragma unroll
@@ -489,6 +468,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                             }
 #pragma unroll
                             for (int j = 0; j < 13; j++) Ag[12 + j] = (i16 < 12) ? Hx[13 * i16 + j] : 0.0;
+#pragma unroll
+                            for (int j = 0; j < 12; j++) Ag[25 + j] = (i16 == j) ? 1.0 : 0.0;
                         }
                         double dk = 1.0;
 #pragma unroll
@@ -498,12 +479,17 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                             const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
 #pragma unroll
                             for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, readlane_d(Ag[j], kk), Ag[j]);
+#pragma unroll
+                            for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, readlane_d(Ag[25 + j], kk), Ag[25 + j]);
                             dk = (i16 == kk) ? piv : dk;
                         }
                         const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
-                        if (lane < 12)
+                        if (lane < 12) {
 #pragma unroll
                             for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
+#pragma unroll
+                            for (int j = 0; j < 12; j++) L.Lm[144 * k + 12 * lane + j] = Ag[25 + j] * sc_;
+                        }
                         SYNC();
                         d4 acc2 = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
@@ -541,6 +527,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
                 for (int k = N - 1; k >= 0; k--) {
                     const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hx = L.Hx + 156 * k;
+                    const double *Lc = L.Lm + 144 * k + ir;
                     double vb[13];
 #pragma unroll
                     for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
@@ -550,9 +537,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         for (int a = 0; a < 3; a++) gu = fma(W[9 * l + 3 * a + jj], vb[9 + a], gu);
                     }
                     if (lane < 12) gus[12 * k + i] = gu;
-                    double kk = 0.0;
+                    double w = 0.0, kk = 0.0;                        // kk = -Z'(Z gu)
 #pragma unroll
-                    for (int j = 0; j < 12; j++) kk = fma(-Lr[j], bc16(gu, j), kk);
+                    for (int j = 0; j < 12; j++) w = fma(Lr[j], bc16(gu, j), w);
+                    if (i >= 12) w = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) kk = fma(-Lc[12 * j], bc16(w, j), kk);
                     if (i >= 12) kk = 0.0;
                     const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
                     double vn = v;                                     // A~' v
@@ -570,6 +560,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 for (int k = 0; k < N; k++) {
                     // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
                     const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hr = L.Hx + 156 * k + 13 * ir;
+                    const double *Lc = L.Lm + 144 * k + ir;
                     double pb[13];
 #pragma unroll
                     for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
@@ -577,9 +568,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
                     for (int j = 0; j < 13; j++) t = fma(Hr[j], pb[j], t);
                     if (i >= 12) t = 0.0;
-                    double du = 0.0;
+                    double w = 0.0, du = 0.0;                        // du = -Z'(Z t)
 #pragma unroll
-                    for (int j = 0; j < 12; j++) du = fma(-Lr[j], bc16(t, j), du);
+                    for (int j = 0; j < 12; j++) w = fma(Lr[j], bc16(t, j), w);
+                    if (i >= 12) w = 0.0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) du = fma(-Lc[12 * j], bc16(w, j), du);
                     if (i >= 12) du = 0.0;
                     if (lane < 12) dU[12 * k + i] = du;
                     double db[12];
