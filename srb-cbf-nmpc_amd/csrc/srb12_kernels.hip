@@ -39,8 +39,8 @@
 namespace {
 
 struct Srb12Lds {
-    double *Wl, *cs, *ct, *Lm, *Hx, *V0, *V1, *Gt, *Ft, *Mt, *Q3, *Rh, *Z, *xr, *gX, *gU;
-    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *lam, *obs, *eps;
+    double *Wl, *cs, *ct, *Lm, *Hx, *V0, *Gt, *Ft, *Mt, *Q3, *Rh, *Z, *xr, *gX, *gU;
+    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *obs, *eps;
     int *sel;
 };
 
@@ -50,13 +50,14 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
 {
     Srb12Lds L;
     L.Wl = p; p += 36 * N;  L.cs = p; p += 2 * N;  L.ct = p; p += 4 * N;
-    L.Lm = p; p += 144 * N; L.Hx = p; p += 156 * N;
-    L.V0 = p; p += 169; L.V1 = p; p += 169;
-    L.Gt = p; p += 169; L.Ft = p; p += 156; L.Mt = p; p += 156;
+    L.Lm = p; p += 78 * N; L.Hx = p; p += 156 * N;          // Z = D^-1/2 L^-1 packed lower triangle, Hux
+    L.V0 = p; p += 169;                                     // V (the update is written over it)
+    L.Gt = p; p += 169; L.Ft = p; p += 156; L.Mt = L.Ft;    // Y reuses F's storage (single wave, in order)
     L.Q3 = p; p += 6 * N; L.Rh = p; p += 24 * N;
-    L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N; L.gX = p; p += 13 * N; L.gU = p; p += 12 * N;
-    L.rX = p; p += 26 * N; L.rU = p; p += 24 * N; L.dX = p; p += 26 * N; L.dU = p; p += 24 * N;
-    L.gus = p; p += 24 * N; L.vv = p; p += 32; L.sc = p; p += 16; L.lam = p; p += 16;
+    L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N;
+    L.rX = p; p += 26 * N; L.rU = p; p += 24 * N; L.dX = p; p += 13 * N; L.dU = p; p += 12 * N;
+    L.gX = L.rX + 13 * N; L.gU = L.rU + 12 * N;              // gradients: column 1 (free until the refinement)
+    L.gus = p; p += 12 * N; L.vv = p; p += 16; L.sc = p; p += 16;
     L.obs = p; p += 2 * N * K; L.eps = p; p += K;
     L.sel = (int *)p;
     return L;
@@ -400,12 +401,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             for (int tries = 0; tries < (nl ? 14 : 1); tries++) {
                 if (tries > 0) delta = (delta == 0.0) ? dstart : delta * 10.0;
                 int fail = 0;
-                int cur = 0;
                 for (int e = tid; e < 169; e += 64) L.V0[e] = qhat(N - 1, e / 13, e % 13, delta);
                 SYNC();
                 for (int k = N - 1; k >= 0; k--) {
                     const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = cur ? L.V1 : L.V0;
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = L.V0;
                     // G = V A~_k (13 x 13), F = V B~_k (13 x 12)
                     for (int e = tid; e < 169; e += 64) {
                         const int i = e / 13, j = e - 13 * i;
@@ -425,7 +425,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                     SYNC();
                     // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
                     // V_0[12][12] is used (the initial slack's Schur complement)
-                    double *Hx = L.Hx + 156 * k, *Vn = cur ? L.V0 : L.V1;
+                    double *Hx = L.Hx + 156 * k, *Vn = L.V0;
                     for (int e = tid; e < 156; e += 64) {
                         const int i = e / 13, j = e - 13 * i;
                         const int li = i / 3, ai = i - 3 * li;
@@ -488,7 +488,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
                             for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
 #pragma unroll
-                            for (int j = 0; j < 12; j++) L.Lm[144 * k + 12 * lane + j] = Ag[25 + j] * sc_;
+                            for (int j = 0; j < 12; j++)
+                                if (j <= lane) L.Lm[78 * k + (lane * (lane + 1)) / 2 + j] = Ag[25 + j] * sc_;
                         }
                         SYNC();
                         d4 acc2 = {0.0, 0.0, 0.0, 0.0};
@@ -505,12 +506,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         }
                     }
                     SYNC();
-                    cur ^= 1;
                 }
                 if (fail) continue;
                 // the free initial slack closes the recursion: V_0[12][12] + Sw + delta > 0 is the last
                 // pivot of the inertia test
-                schur = (cur ? L.V1 : L.V0)[168] + prm.Sw + delta;
+                schur = L.V0[168] + prm.Sw + delta;
                 if (!(schur > 0.0)) continue;
                 ok = 1;
                 break;
@@ -520,14 +520,13 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
             // Vectors live in registers, component i = lane & 15 (each 16-lane row holds a copy), and move
             // between lanes by DPP row broadcasts: no LDS round trip or barrier inside the recursion.
-            auto riccati_solve = [&](int c) {
-                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
+            auto riccati_solve = [&](int c, bool acc) {
+                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l, tri = (ir * (ir + 1)) / 2;
                 const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
-                double *dX = L.dX + 13 * N * c, *dU = L.dU + 12 * N * c, *gus = L.gus;
+                double *dX = L.dX, *dU = L.dU, *gus = L.gus;      // acc: the refinement's correction adds in
                 double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
                 for (int k = N - 1; k >= 0; k--) {
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hx = L.Hx + 156 * k;
-                    const double *Lc = L.Lm + 144 * k + ir;
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hx = L.Hx + 156 * k;
                     double vb[13];
 #pragma unroll
                     for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
@@ -539,10 +538,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                     if (lane < 12) gus[12 * k + i] = gu;
                     double w = 0.0, kk = 0.0;                        // kk = -Z'(Z gu)
 #pragma unroll
-                    for (int j = 0; j < 12; j++) w = fma(Lr[j], bc16(gu, j), w);
+                    for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(gu, j), w);
                     if (i >= 12) w = 0.0;
 #pragma unroll
-                    for (int j = 0; j < 12; j++) kk = fma(-Lc[12 * j], bc16(w, j), kk);
+                    for (int j = 0; j < 12; j++) kk = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), kk);
                     if (i >= 12) kk = 0.0;
                     const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
                     double vn = v;                                     // A~' v
@@ -559,8 +558,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 double prev = (i == 12) ? ds0 : 0.0;
                 for (int k = 0; k < N; k++) {
                     // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Lr = L.Lm + 144 * k + 12 * ir, *Hr = L.Hx + 156 * k + 13 * ir;
-                    const double *Lc = L.Lm + 144 * k + ir;
+                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hr = L.Hx + 156 * k + 13 * ir;
                     double pb[13];
 #pragma unroll
                     for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
@@ -570,12 +568,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                     if (i >= 12) t = 0.0;
                     double w = 0.0, du = 0.0;                        // du = -Z'(Z t)
 #pragma unroll
-                    for (int j = 0; j < 12; j++) w = fma(Lr[j], bc16(t, j), w);
+                    for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(t, j), w);
                     if (i >= 12) w = 0.0;
 #pragma unroll
-                    for (int j = 0; j < 12; j++) du = fma(-Lc[12 * j], bc16(w, j), du);
+                    for (int j = 0; j < 12; j++) du = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), du);
                     if (i >= 12) du = 0.0;
-                    if (lane < 12) dU[12 * k + i] = du;
+                    if (lane < 12) dU[12 * k + i] = acc ? dU[12 * k + i] + du : du;
                     double db[12];
 #pragma unroll
                     for (int j = 0; j < 12; j++) db[j] = bc16(du, j);
@@ -592,7 +590,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                             for (int j = 0; j < 3; j++) dx = fma(W[9 * ll + 3 * a + j], db[3 * ll + j], dx);
                     }
                     if (i > 12) dx = 0.0;
-                    if (lane < 13) dX[13 * k + i] = dx;
+                    if (lane < 13) dX[13 * k + i] = acc ? dX[13 * k + i] + dx : dx;
                     prev = dx;
                 }
                 SYNC();
@@ -640,10 +638,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double m12 = bc16(m, 12);
                 if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + m12;
                 SYNC();
-                riccati_solve(1);
-                for (int e = tid; e < 13 * N; e += 64) L.dX[e] += L.dX[13 * N + e];
-                for (int e = tid; e < 12 * N; e += 64) L.dU[e] += L.dU[12 * N + e];
-                SYNC();
+                riccati_solve(1, true);
             };
             // right-hand side of pass (0 predictor, 1 corrector) into column 0:
             // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
@@ -714,7 +709,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // what limits progress, and it costs a solve)
             const bool refn = mu < 1e-3;
             build_rhs(0, 0.0);
-            riccati_solve(0);
+            riccati_solve(0, false);
             if (refn) refine(delta);
             double dsl[TS], dzl[TS];
             double2 al = row_step(0, 0.0, dsl, dzl);
@@ -734,7 +729,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             // ---- corrector
             build_rhs(1, sigma * mu);
-            riccati_solve(0);
+            riccati_solve(0, false);
             if (refn) refine(delta);
             al = row_step(1, sigma * mu, dsl, dzl);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);

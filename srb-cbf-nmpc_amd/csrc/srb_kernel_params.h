@@ -160,11 +160,11 @@ static inline int srb12_slots(int N, int K) { return 24 * N + N * K; }
 // doubles of LDS one agent needs (the carve in srb12_kernels.hip)
 static inline int srb12_lds_doubles(int N, int K)
 {
-    return 36 * N + 2 * N + 4 * N + 144 * N + 156 * N     // W_l, (cos, sin) psi, contact, Hu^-1, Hux (12 x 13) per grid
-           + 2 * 169 + 169 + 2 * 156                    // V ping-pong, G (13 x 13), F, M
+    return 36 * N + 2 * N + 4 * N + 78 * N + 156 * N      // W_l, (cos, sin) psi, contact, Z (packed), Hux per grid
+           + 169 + 169 + 156                            // V, G, F (Y reuses F)
            + 6 * N + 24 * N                             // (p_x, p_y, s) blocks, force blocks
-           + (24 * N + 4) + 12 * N + 13 * N + 12 * N    // iterate (X | U | s), reference, gradients
-           + 2 * 13 * N + 2 * 12 * N + 2 * 13 * N + 2 * 12 * N + 2 * 12 * N   // rhs / solution / gu columns (solve, refinement)
-           + 32 + 16 + 16                               // vectors, scalars, costates
+           + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
+           + 2 * 13 * N + 2 * 12 * N + 13 * N + 12 * N + 12 * N   // rhs columns (solve, refinement / gradients), solution, gu
+           + 16 + 16                                    // vector, scalars
            + 2 * N * K + 2 * K + 2;                     // obstacle positions, eps, sel (as ints)
 }
