@@ -42,9 +42,14 @@ def make_obstacles(rng, n_obs: int = 20, scale: float = 1.0):
     return np.stack([rx, ry], 1)
 
 
-def make_batch(n_agents: int, N: int = 10, C: int = 2, seed: int = 0, n_obs: int | None = None):
+def make_batch(n_agents: int, N: int = 10, C: int = 2, seed: int = 0, n_obs: int | None = None,
+               velocity: str = "goal"):
     """Returns dict(x0 [A,4], ref [A,4N], foot [A,N,2,C], obstacles [n_obs,2],
-    nbr_state [A,4] (x, y, xdot, ydot of every agent, the get_lastState layout))."""
+    nbr_state [A,4] (x, y, xdot, ydot of every agent, the get_lastState layout)).
+    velocity "goal" (default): initial velocities drawn toward the goal (the documented deviation);
+    "free": U[-0.3, 0.3] per axis, uncorrelated with the goal and the trot support, which leaves
+    some instances' CoM-CoP rows infeasible -- the hard workload of tests/test_gpu_parity.py
+    (statuses other than OPTIMAL must agree with the oracle's too)."""
     rng = np.random.default_rng(seed)
     A = int(n_agents)
     sc = arena_scale(A)
@@ -55,6 +60,8 @@ def make_batch(n_agents: int, N: int = 10, C: int = 2, seed: int = 0, n_obs: int
     d = goal - p0
     d /= np.linalg.norm(d, axis=1, keepdims=True)
     v0 = d * rng.uniform(0, 0.3, (A, 1)) + rng.uniform(-0.05, 0.05, (A, 2))
+    if velocity == "free":
+        v0 = rng.uniform(-0.3, 0.3, (A, 2))
     x0 = np.stack([p0[:, 0], v0[:, 0], p0[:, 1], v0[:, 1]], 1)
     k = np.arange(N)
     ref = np.zeros((A, N, 4))
