@@ -132,3 +132,33 @@ def test_rank_shard_of_8gpu_swarm_vs_oracle(config, rank):
     # 4. the fused Bezier epilogue on the shard (alpha_COM of the start buffer)
     X = x[:, :16].reshape(n, 4, 4)
     np.testing.assert_allclose(out["alpha"].reshape(n, 4, 5)[:, :, 4], X[:, 3], atol=1e-9)
+
+
+def test_rccl_backend_all_gather_round_trip():
+    """The RCCL path of the neighbour exchange on this box's one GPU: a one-rank "nccl" (RCCL)
+    process group, NeighbourExchange's flat mode, and the all_gather_into_tensor call it issues
+    per cycle, in a child process (the group must not outlive the test)."""
+    import socket
+    import subprocess
+    with socket.socket() as sk:
+        sk.bind(("127.0.0.1", 0))
+        port = sk.getsockname()[1]
+    code = f"""
+import os, sys, torch, torch.distributed as dist
+sys.path.insert(0, {os.path.join(ROOT, 'srb-cbf-nmpc_amd')!r})
+from srbnmpc import dist as sd
+os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{port}")
+dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
+assert dist.get_backend() == "nccl"
+x = torch.arange(1024 * 4, dtype=torch.float64, device="cuda").view(1024, 4)
+ex = sd.NeighbourExchange(1024, 1, 0, x.device)
+assert ex.flat
+recv = torch.zeros_like(x)
+dist.all_gather_into_tensor(recv, x)
+torch.cuda.synchronize()
+assert torch.equal(recv, x)
+dist.destroy_process_group()
+print("rccl ok")
+"""
+    r = subprocess.run([sys.executable, "-c", code], timeout=150, capture_output=True, text=True)
+    assert r.returncode == 0 and "rccl ok" in r.stdout, (r.stdout[-2000:], r.stderr[-2000:])
