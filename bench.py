@@ -337,7 +337,8 @@ def main_srb12(args, world, rank, local_rank, dev):
         "optimal_frac": float((status == 0).all(1).mean()), "iters_mean": iters.mean(0).tolist(),
         "iters_max": iters.max(0).tolist(),
         "roofline": {"bound": "mfma", "limiter": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
-                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": None, "kernel": "srb12_kernel",
+                     "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic_from("s12", n_loc)[0],
+                     "traffic_source": traffic_from("s12", n_loc)[1], "kernel": "srb12_kernel",
                      "kernel_ms": solve_ms, "select_ms": sel_ms, "io_bytes_per_launch": io,
                      "flop_model": "bench.srb12_executed_flops (Riccati IPM, DESIGN.md 11); latency-bound"},
         "cpu_baseline": None,
