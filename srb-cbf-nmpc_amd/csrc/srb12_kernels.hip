@@ -77,23 +77,6 @@ __device__ __forceinline__ double a_mul(int i, const double *x, double Ts, doubl
     else if (i < 6) v = fma(Ts, rzab(0, i - 3, c, s) * x[9] + rzab(1, i - 3, c, s) * x[10] + rzab(2, i - 3, c, s) * x[11], v);
     return v;
 }
-// (A_k' x)[i]
-__device__ __forceinline__ double at_mul(int i, const double *x, double Ts, double c, double s)
-{
-    double v = x[i];
-    if (i >= 6 && i < 9) v = fma(Ts, x[i - 6], v);
-    else if (i >= 9 && i < 12) v = fma(Ts, rzab(i - 9, 0, c, s) * x[3] + rzab(i - 9, 1, c, s) * x[4] + rzab(i - 9, 2, c, s) * x[5], v);
-    return v;
-}
-// the 13-state forms (x[12] = the slack, s_{k+1} = s_k): A~ = diag(A, 1)
-__device__ __forceinline__ double a13(int i, const double *x, double Ts, double c, double s)
-{
-    return (i == 12) ? x[12] : a_mul(i, x, Ts, c, s);
-}
-__device__ __forceinline__ double at13(int i, const double *x, double Ts, double c, double s)
-{
-    return (i == 12) ? x[12] : at_mul(i, x, Ts, c, s);
-}
 // (B_k u)[i] (i < 12); W: the grid's 4 x 9 leg blocks (contact and Ts folded in), ct: contact flags
 __device__ __forceinline__ double b_mul(int i, const double *u, const double *W, const double *ct, double tsm)
 {
@@ -105,14 +88,6 @@ __device__ __forceinline__ double b_mul(int i, const double *u, const double *W,
         for (int l = 0; l < 4; l++)
             for (int j = 0; j < 3; j++) v = fma(W[9 * l + 3 * a + j], u[3 * l + j], v);
     }
-    return v;
-}
-// (B_k' x)[3 l + j]
-__device__ __forceinline__ double bt_mul(int e, const double *x, const double *W, const double *ct, double tsm)
-{
-    const int l = e / 3, j = e - 3 * l;
-    double v = ct[l] * tsm * x[6 + j];
-    for (int a = 0; a < 3; a++) v = fma(W[9 * l + 3 * a + j], x[9 + a], v);
     return v;
 }
 // friction row q of a leg: coefficients on (f_x, f_y, f_z) (LowLevelCtrl.cpp:158-162, + f_z <= fmax)
