@@ -354,7 +354,6 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         const double ga = (af == 0) ? g0 : g1;
         return fma(fla, u2, ga * fia);
     };
-    double Si[NQ];
     // om: inverse weights z/s of every inequality row, in sh.vt (row-indexed); wc = s/z of the CLF row
     auto factor = [&](double wc) -> int {
         // friction LDL' per stance leg: H = [a 0 p; 0 b q; p q c]
@@ -423,9 +422,15 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         SYNC();
         LLST(4);   // S
         const int i = ise ? lane : 0;
+        double Si[NQ];
 #pragma unroll
         for (int j = 0; j < NQ; j++) Si[j] = ise ? sh.u.ip.S[i * LDJ + j] : ((lane == j) ? 1.0 : 0.0);
         const int gjf = gj_invert<NQ>(Si, NQ, lane, 0);
+        // S^-1 goes back to LDS (row per equality lane): 36 VGPRs kept free across the loop
+        if (ise) {
+#pragma unroll
+            for (int j = 0; j < NQ; j++) sh.u.ip.S[i * LDJ + j] = Si[j];
+        }
         LLST(5);   // Gauss-Jordan
         return gjf;
     };
@@ -460,8 +465,11 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         if (ise) sh.ve[lane] = arow(sh.vx) - r2;
         SYNC();
         double dyk = 0.0;
+        if (ise) {
+            const double *Sr = sh.u.ip.S + lane * LDJ;
 #pragma unroll
-        for (int j = 0; j < NQ; j++) dyk = fma(Si[j], sh.ve[j], dyk);
+            for (int j = 0; j < NQ; j++) dyk = fma(Sr[j], sh.ve[j], dyk);
+        }
         SYNC();
         if (ise) sh.ve[lane] = dyk;
         SYNC();
@@ -706,6 +714,9 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
                 J[a][b] = gJt[(6 + 3 * L + b) * NU + 3 * L + a] - gJh[(6 + 3 * L + b) * NU + 3 * L + a];
             }
             r[a] = dxde + 20.0 * (xde - xe) - jt;
+            // one row's loads at a time: hoisting all three rows' loads spilled 12 VGPRs to scratch,
+            // whose write-back tripled the kernel's HBM writes
+            __builtin_amdgcn_sched_barrier(0);
         }
         // Cramer's rule on the 3x3 leg block
         const double c00 = J[1][1] * J[2][2] - J[1][2] * J[2][1], c01 = J[1][2] * J[2][0] - J[1][0] * J[2][2],
