@@ -63,6 +63,17 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     return L;
 }
 
+// pivot-row entries of the forward elimination: every 16-lane row holds the whole matrix, so a DPP
+// row broadcast (SRB12_ELIM_DPP=1) or a readlane of lane kk (0) give the same value
+#ifndef SRB12_ELIM_DPP
+#define SRB12_ELIM_DPP 0
+#endif
+#if SRB12_ELIM_DPP
+#define SRB12_PIVROW(v, kk) bc16((v), (kk))
+#else
+#define SRB12_PIVROW(v, kk) readlane_d((v), (kk))
+#endif
+
 // Rz(psi)[a][b] from (cos, sin)
 __device__ __forceinline__ double rzab(int a, int b, double c, double s)
 {
@@ -453,9 +464,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                             fail |= !(piv > 0.0);
                             const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
 #pragma unroll
-                            for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, readlane_d(Ag[j], kk), Ag[j]);
+                            for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, SRB12_PIVROW(Ag[j], kk), Ag[j]);
 #pragma unroll
-                            for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, readlane_d(Ag[25 + j], kk), Ag[25 + j]);
+                            for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, SRB12_PIVROW(Ag[25 + j], kk), Ag[25 + j]);
                             dk = (i16 == kk) ? piv : dk;
                         }
                         const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
