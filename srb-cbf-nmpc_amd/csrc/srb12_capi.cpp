@@ -149,7 +149,7 @@ extern "C" int srb12_ctx_create(const srb12_params *p, int max_agents, int devic
     H12CHK(hipMalloc(&c->obj, A * sizeof(double)));
     H12CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     H12CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
-    H12CHK(hipMalloc(&c->dbg, 2 * 64 * 8 * sizeof(double)));
+    H12CHK(hipMalloc(&c->dbg, (2 * 64 * 8 + 16) * sizeof(double)));
     c->dbg_agent = -1;
     *out = c;
     return SRB_OK;
@@ -314,16 +314,16 @@ extern "C" int srb12_last_kernel_ms(srb12_ctx *c, float *select_ms, float *solve
 
 // diagnostics (not in the public header): agent >= 0 records a per-iteration trace on the next
 // calls (|r_d|, its threshold, |r_p|, mu, ap, ad, delta, sigma per iteration, QP then NLP);
-// out != NULL copies the last trace [2][64][8] to the host
+// out != NULL copies the last trace [2][64][8] + 16 phase-cycle sums (-DSRB12_STAMPS builds) to the host
 extern "C" int srb12_debug_trace(srb12_ctx *c, int agent, double *out)
 {
     if (!c) return srb_internal_fail(SRB_ERR_ARG, "null ctx");
     H12CHK(hipSetDevice(c->device));
     if (out) {
         if (c->any) H12CHK(hipEventSynchronize(c->done));
-        H12CHK(hipMemcpy(out, c->dbg, 2 * 64 * 8 * sizeof(double), hipMemcpyDeviceToHost));
+        H12CHK(hipMemcpy(out, c->dbg, (2 * 64 * 8 + 16) * sizeof(double), hipMemcpyDeviceToHost));
     }
     c->dbg_agent = agent;
-    H12CHK(hipMemset(c->dbg, 0, 2 * 64 * 8 * sizeof(double)));
+    H12CHK(hipMemset(c->dbg, 0, (2 * 64 * 8 + 16) * sizeof(double)));
     return SRB_OK;
 }

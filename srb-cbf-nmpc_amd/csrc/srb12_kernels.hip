@@ -74,6 +74,24 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
 #define SRB12_PIVROW(v, kk) readlane_d((v), (kk))
 #endif
 
+// per-phase cycle stamps of the traced agent (diagnostic build -DSRB12_STAMPS, libsrbnmpc_s12st.so):
+// s_memtime deltas accumulated into prm.dbg[SRB12_DBG_TRACE + slot], read by srb12_debug_trace
+#define SRB12_DBG_TRACE (2 * 64 * 8)
+#ifdef SRB12_STAMPS
+#define S12ST(slot)                                                                                  \
+    do {                                                                                             \
+        if (dstamp) {                                                                                \
+            __builtin_amdgcn_sched_barrier(0);                                                       \
+            const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
+            __builtin_amdgcn_sched_barrier(0);                                                       \
+            if (tid == 0) prm.dbg[SRB12_DBG_TRACE + (slot)] += (double)(t_ - tprev);                  \
+            tprev = t_;                                                                              \
+        }                                                                                            \
+    } while (0)
+#else
+#define S12ST(slot) do { } while (0)
+#endif
+
 // Rz(psi)[a][b] from (cos, sin)
 __device__ __forceinline__ double rzab(int a, int b, double c, double s)
 {
@@ -133,6 +151,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     Srb12Lds L = carve12(lds, N, K);
     double *X = L.Z, *U = L.Z + 12 * N;
     const double *x0 = x0g + 12 * (size_t)agent;
+#ifdef SRB12_STAMPS
+    const bool dstamp = agent == prm.dbg_agent && prm.dbg != nullptr;
+    unsigned long long tprev = dstamp ? __builtin_amdgcn_s_memtime() : 0ull;
+#endif
 
     // ---------------- inputs, per-grid model (orc12_dynamics), selected rows
     for (int i = tid; i < 12 * N; i += 64) L.xr[i] = xrefg[(size_t)agent * 12 * N + i];
@@ -204,6 +226,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     double ss[TS], zz[TS], dsa[TS], dza[TS];
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
+    S12ST(0);   // inputs, model, rollout
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
@@ -355,6 +378,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             double *dbgrow = (agent == prm.dbg_agent && prm.dbg && it < 64) ? prm.dbg + 8 * (64 * stage + it) : nullptr;
             if (dbgrow && tid == 0) { dbgrow[0] = nrd; dbgrow[1] = th * gm; dbgrow[2] = nrp; dbgrow[3] = mu; }
             if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz)) { flag = 3; break; }
+            S12ST(1);   // residuals, weights, scatter, costates
             if (nrd < th * gm && nrp < th && mu < tol) { flag = 0; break; }
 
             // ---- factorisation (backward Riccati over the 13-state) with the inertia shift delta (NLP)
@@ -501,6 +525,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 ok = 1;
                 break;
             }
+            S12ST(2);   // Riccati factor (all tries)
             if (!ok) { flag = 1; break; }
             // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
             // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
@@ -690,6 +715,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 wred<2, 3u>(rv);
                 return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
             };
+            S12ST(3);   // between factor and predictor
             // ---- predictor
             // (the refinement only near the optimum, mu < 1e-3: far from it the step's accuracy is not
             // what limits progress, and it costs a solve)
@@ -697,6 +723,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             build_rhs(0, 0.0);
             riccati_solve(0, false);
             if (refn) refine(delta);
+            S12ST(4);   // predictor rhs + solve (+ refinement)
             double dsl[TS], dzl[TS];
             double2 al = row_step(0, 0.0, dsl, dzl);
 #pragma unroll
@@ -713,10 +740,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
                 sigma = mr * mr * mr;
             }
+            S12ST(5);   // predictor row step, sigma
             // ---- corrector
             build_rhs(1, sigma * mu);
             riccati_solve(0, false);
             if (refn) refine(delta);
+            S12ST(6);   // corrector rhs + solve (+ refinement)
             al = row_step(1, sigma * mu, dsl, dzl);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);
             if (dbgrow && tid == 0) { dbgrow[4] = ap; dbgrow[5] = ad; dbgrow[6] = delta; dbgrow[7] = sigma; }
@@ -732,6 +761,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
             for (int t = 0; t < TS; t++) { ss[t] = fma(ap, dsl[t], ss[t]); zz[t] = fma(ad, dzl[t], zz[t]); }
             SYNC();
+            S12ST(7);   // corrector row step + update
         }
         if (stage == 0) {
             qp_flag = flag; qp_it = it;

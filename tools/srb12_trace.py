@@ -18,7 +18,7 @@ b = workload.make_batch12(A, N, gait, seed=seed)
 s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
 L = srb12._lib()
 L.srb12_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
-buf = np.zeros(2 * 64 * 8)
+buf = np.zeros(2 * 64 * 8 + 16)
 p = oracle.params12(N, K_obs=3, K_nbr=8)
 for ag in map(int, sys.argv[4:]):
     L.srb12_debug_trace(s._h, ag, None)
