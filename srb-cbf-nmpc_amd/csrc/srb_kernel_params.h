@@ -82,10 +82,17 @@ struct SrbKParams {
 #ifdef SRB_DEV_INSTANCES          // register-tuning builds of a few instances (make dev)
 #define SRB_KERNEL_INSTANCES(X) SRB_DEV_INSTANCES(X)
 #else
+// the host picks the first fitting instance of this list (srb_capi.cpp), so its order matters
 #define SRB_KERNEL_INSTANCES(X) \
     X(8, 1, 1) X(16, 1, 1) X(12, 3, 1) X(12, 4, 1) X(16, 4, 1) X(24, 5, 1) X(24, 8, 1) X(32, 4, 1) X(32, 8, 1) \
     X(8, 1, 4) X(12, 1, 4) X(16, 1, 4) X(16, 2, 4) X(32, 2, 4) \
     X(12, 2, 2) X(16, 2, 2) X(24, 4, 2) X(24, 2, 4)
+// the same instances in four parts of about equal compile time: the product build compiles
+// srb_kernels.hip once per part (-DSRB_PART=0..3, in parallel)
+#define SRB_KI_PART0(X) X(12, 4, 1) X(8, 1, 1) X(16, 1, 1) X(12, 3, 1) X(8, 1, 4)
+#define SRB_KI_PART1(X) X(24, 4, 2) X(12, 1, 4) X(16, 4, 1) X(12, 2, 2)
+#define SRB_KI_PART2(X) X(24, 5, 1) X(24, 8, 1) X(16, 1, 4) X(16, 2, 4) X(16, 2, 2)
+#define SRB_KI_PART3(X) X(32, 4, 1) X(32, 8, 1) X(32, 2, 4) X(24, 2, 4)
 #endif
 static inline int srb_slots(int N, int C, int K) { return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K; }
 

@@ -1562,7 +1562,21 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                                   status_out, alpha_buf, alpha_out, sel_g, zpol_g, zstride, lds);             \
     }
 
+#if defined(SRB_PART) && !defined(SRB_DEV_INSTANCES)
+#if SRB_PART == 0
+SRB_KI_PART0(SRB_NMPC_KERNEL)
+#elif SRB_PART == 1
+SRB_KI_PART1(SRB_NMPC_KERNEL)
+#elif SRB_PART == 2
+SRB_KI_PART2(SRB_NMPC_KERNEL)
+#else
+SRB_KI_PART3(SRB_NMPC_KERNEL)
+#endif
+#else
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
+#endif
+
+#if !defined(SRB_PART) || SRB_PART == 0
 
 // Obstacle and neighbour selection (MPC_dist.cpp:371-396, generalised to K): one workgroup per
 // agent, the K_obs nearest static obstacles (with the reference's 1000 m sentinel) and the
@@ -1681,3 +1695,4 @@ extern "C" __global__ void __launch_bounds__(1024) srb_grid_build_kernel(
         *g = r;
     }
 }
+#endif   // SRB_PART 0: selection kernels
