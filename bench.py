@@ -43,7 +43,6 @@ from srbnmpc import dist as sdist, workload  # noqa: E402
 METRIC = "NMPC solves/sec (whole node) + p99 solve latency, N-agent batch horizon=10"
 FP64_PEAK_TFLOPS = 78.6      # MI355X FP64 (vector and matrix) dense peak, spec
 SCLK_GHZ = 2.4               # MI355X peak engine clock (MI355X_MICROARCH.md)
-CALIBRATION = os.path.join(ROOT, "profiles", "r02_cpu_calibration.json")
 CONFIGS = {
     1: dict(agents=1, N=4, C=4, K_obs=1, K_nbr=0, name="1 agent, N=4, stand (reference mode, KAT-2 shape)"),
     2: dict(agents=64, N=10, C=2, K_obs=3, K_nbr=0, name="64 agents/GPU, horizon 10, trot, 3 static CBF obstacles, fp64"),
@@ -93,38 +92,95 @@ def host_threads():
 
 
 def cpu_baseline(cfg, b, budget_s):
-    """Oracle (CPU restatement of the same algorithm, oracle/) timed on this host's cores
-    on a bounded sample of the same workload, with its calibration against the genuine
-    vendored iSWIFT (tools/calibrate_cpu.py -> profiles/r02_cpu_calibration.json): the
-    reference's own QP solver on the same QP-stage instances, single thread, so that the
-    oracle's dense-LU rate can be read against the reference's sparse-LDL' rate."""
+    """CPU baselines on this host's cores, on bounded samples of the same workload, in this run:
+      * the port (oracle/: the same QP + NLP algorithm in C, dense LU on the full-space KKT),
+        "kind" "port" -- the headline cpu_baseline value (the reference's NLP solver, SNOPT, is
+        proprietary and absent: there is no reference QP + NLP rate to time);
+      * reference_qp: the reference's OWN QP solver -- the vendored iSWIFT compiled unchanged from
+        /root/reference (oracle/_ref/libiswift_ref.so, iswift_qp.cpp:44-162 / Prime.c:127-230 with
+        its dense -> CCS conversion and a fill-reducing ordering of the full KKT every call, as the
+        Eigen wrapper does) on the QP stage of the same instances, same threads ("kind" "reference");
+      * port_qp: the port's QP stage alone on those instances (the like-for-like ratio to
+        reference_qp; replaces round 2's build-container calibration)."""
     sys.path.insert(0, ROOT)
     import oracle
+    from concurrent.futures import ThreadPoolExecutor
     nthreads = host_threads()
     p = oracle.params(cfg["N"], cfg["C"], K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"])
     A = b["x0"].shape[0]
     sample = min(A, max(nthreads * 2, 16))
-    t0 = time.perf_counter(); solved = 0
-    while True:
+
+    def timed(fn, budget):
+        t0 = time.perf_counter(); done = 0
+        while True:
+            done += fn()
+            if time.perf_counter() - t0 > budget:
+                return done, time.perf_counter() - t0
+
+    def port_batch():
         oracle.solve_batch(p, b["x0"][:sample], b["ref"][:sample], b["foot"][:sample], b["obstacles"],
                            b["nbr_state"], nthreads=nthreads)
-        solved += sample
-        if time.perf_counter() - t0 > budget_s:
-            break
-    dt = time.perf_counter() - t0
+        return sample
+    solved, dt = timed(port_batch, budget_s)
     line = {"value": solved / dt, "unit": "solves/s", "cores": nthreads, "kind": "port",
             "sample": f"{solved} solves ({sample}-agent slices of the same batch) in {dt:.1f} s, QP+NLP, "
                       f"{nthreads} threads"}
+    # the QP stage (a few ms per solve, so larger slices keep the per-call thread start-up out of the
+    # rate): the port (use_nlp = 0) and the genuine iSWIFT on the same instances
+    qs = min(A, 32 * nthreads)
+    pq = oracle.params(cfg["N"], cfg["C"], K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=0)
+
+    def port_qp():
+        oracle.solve_batch(pq, b["x0"][:qs], b["ref"][:qs], b["foot"][:qs], b["obstacles"], b["nbr_state"],
+                           nthreads=nthreads)
+        return qs
+    qsolved, qdt = timed(port_qp, budget_s / 3)
+    line["port_qp"] = {"value": qsolved / qdt, "unit": "QP-stage solves/s", "cores": nthreads, "kind": "port",
+                       "sample": f"{qsolved} QP stages ({qs}-agent slices of the same batch) in {qdt:.1f} s"}
     try:
-        cal = json.load(open(CALIBRATION))
-        key = f"N{cfg['N']}_C{cfg['C']}"
-        if key in cal.get("cases", {}):
-            c = cal["cases"][key]
-            line["iswift_ratio"] = c["oracle_over_iswift"]
-            line["iswift_calibration"] = (f"QP stage on {c['instances']} instances, 1 thread: oracle {c['oracle_us']:.0f} us, "
-                                          f"genuine iSWIFT {c['iswift_us']:.0f} us per solve ({CALIBRATION[len(ROOT) + 1:]})")
-    except (OSError, ValueError, KeyError):
-        pass
+        R = oracle.ref_lib()
+    except OSError as e:                       # oracle/_ref not built (no /root/reference where it was built)
+        line["reference_qp"] = {"value": None, "error": f"oracle/_ref/libiswift_ref.so unavailable: {e}"}
+        return line
+    import ctypes
+    import scipy.sparse as sps
+    ip, dp = ctypes.POINTER(ctypes.c_int), ctypes.POINTER(ctypes.c_double)
+    probs = []
+    for a in range(qs):          # dense QPs (MPC_dist.cpp:135-321) -> CCS, built once, untimed
+        Pd, c, Aq, bq, G, h = oracle.build_qp(p, b["x0"][a], b["ref"][a], b["foot"][a])
+        n, m, pp = Pd.size, G.shape[0], Aq.shape[0]
+        keep = []
+        for M in (np.diag(Pd), Aq, G):
+            S = sps.csc_matrix(M); S.eliminate_zeros(); S.sort_indices()
+            keep += [np.ascontiguousarray(S.indptr, np.int32), np.ascontiguousarray(S.indices, np.int32),
+                     np.ascontiguousarray(S.data, np.float64)]
+        # elimination order z | x | y: quasi-definite, so no pivot needs iSWIFT's regularisation (the
+        # reference's Eigen AMD order is a one-off symbolic cost next to QP_SETUP's factorisation)
+        perm = np.r_[np.arange(n + pp, n + pp + m), np.arange(n), np.arange(n, n + pp)].astype(np.int32)
+        vecs = [np.ascontiguousarray(v, np.float64).copy() for v in (c, h, bq)]
+        args = [v.ctypes.data_as(ip if v.dtype == np.int32 else dp) for v in keep] + \
+               [v.ctypes.data_as(dp) for v in vecs] + [perm.ctypes.data_as(ip)]
+        probs.append((n, m, pp, args, np.zeros(n), keep, vecs, perm))
+    flags = []
+
+    def solve_range(lo, hi):
+        it = ctypes.c_int()
+        for k in range(lo, hi):
+            n, m, pp, args, x = probs[k][:5]
+            flags.append(R.iswift_ref_solve_ccs(n, m, pp, *args, x.ctypes.data_as(dp), ctypes.byref(it)))
+        return hi - lo
+    cuts = [qs * t // nthreads for t in range(nthreads + 1)]
+    with ThreadPoolExecutor(nthreads) as ex:  # ctypes releases the GIL: one host thread per slice
+        def ref_batch():
+            return sum(ex.map(lambda t: solve_range(cuts[t], cuts[t + 1]), range(nthreads)))
+        rsolved, rdt = timed(ref_batch, budget_s / 3)
+    line["reference_qp"] = {
+        "value": rsolved / rdt, "unit": "QP-stage solves/s", "cores": nthreads, "kind": "reference",
+        "sample": f"{rsolved} QP stages ({qs}-agent slices, as port_qp) in {rdt:.1f} s: the genuine vendored iSWIFT "
+                  f"(oracle/_ref; QP_SETUP + QP_SOLVE + QP_CLEANUP per call as iswift_qp.cpp:78-162 does, "
+                  f"CCS inputs and a quasi-definite elimination order prepared once), "
+                  f"{sum(f == 0 for f in flags)}/{len(flags)} OPTIMAL"}
+    line["port_qp_over_reference_qp"] = line["port_qp"]["value"] / line["reference_qp"]["value"]
     return line
 
 

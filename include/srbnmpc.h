@@ -42,7 +42,7 @@ extern "C" {
  * the SRB_ABI_VERSION the library was built with (bumped on any layout change).
  *   srb_batch b = {sizeof(srb_batch)};      (C)      srb_batch b{}; b.struct_size = sizeof b;  (C++)
  */
-#define SRB_ABI_VERSION 3
+#define SRB_ABI_VERSION 4
 int srb_abi_version(void);
 
 /* solver exit codes (iSWIFT GlobalOptions.h:31-34) */
@@ -87,7 +87,10 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *   status    [A][2] int    QP, NLP exit codes: 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL (iSWIFT's);
  *                           NLP also 4 ACCEPTABLE: stopped at a near-optimal iterate (primal and
  *                           complementarity met, dual residual within 100x of its threshold)
- *                           whose next step was blocked or needed an inertia shift
+ *                           whose next step was blocked or needed an inertia shift, or met only
+ *                           the loosened exit tests the polish relies on and was not polished
+ *                           (rejected, or SRB_OPT_POLISH = 0); 3 FATAL also when a dual passes 1e10
+ *                           (infeasible rows) -- the iterate returned is finite in every case
  *   iters     [A][2] int    QP, NLP interior-point iterations
  * Bezier fit of the predicted CoM (fitComTrajectory_eventbase, MPC_dist.cpp:784-855), fused
  * into the solve; both NULL = not fitted (needs N >= 4):
@@ -129,6 +132,23 @@ int srb_ctx_destroy(srb_ctx *ctx);
  * srb_ctx_waves() returns the count the last launch used. */
 int srb_ctx_set_waves(srb_ctx *ctx, int nw);
 int srb_ctx_waves(srb_ctx *ctx);
+
+/* Context options (no environment variable changes what the library computes; every knob is one
+ * of these, per context).  set returns SRB_ERR_ARG for an unknown option or a value out of range.
+ *   SRB_OPT_POLISH               1 (default) polish the NLP result to the exact KKT point of its active
+ *                                set, 0 off: results that met only the loosened NLP exit
+ *                                tests then stay ACCEPTABLE (4)
+ *   SRB_OPT_POLISH_RHO           the polish's regularisation 1 / rho (default 1e9; 1e3 .. 1e12)
+ *   SRB_OPT_POLISH_WAVES         waves per agent of the polish kernel: 0 automatic (default), 1, 2, 4
+ *   SRB_OPT_GRID_MIN_ROWS        tables of this many rows or more get a selection grid (default 8192)
+ *   SRB_OPT_GRID_MIN_ROWS_STATIC the same for a versioned static obstacle table (default 4096) */
+#define SRB_OPT_POLISH 1
+#define SRB_OPT_POLISH_RHO 2
+#define SRB_OPT_POLISH_WAVES 3
+#define SRB_OPT_GRID_MIN_ROWS 4
+#define SRB_OPT_GRID_MIN_ROWS_STATIC 5
+int srb_ctx_set_option(srb_ctx *ctx, int opt, double value);
+int srb_ctx_get_option(srb_ctx *ctx, int opt, double *value);
 
 /* QP-stage starting point: 1 (default) the scaled start s = max(h - Gx, 0.1), z = 1/s from the
  * least-squares x of iSWIFT's kkt_initialize (Auxilary.c:680-755); 0 iSWIFT's own shifted start
@@ -300,6 +320,11 @@ typedef struct srb12_params {
     double eps_obs, eps_nbr, tol;
     int qp_maxit, nlp_maxit, use_nlp;
     double z0;                    /* NLP initial duals z0 / max(s, 1) */
+    double tol_final;             /* complementarity s'z/m < tol_final ends the LAST stage (the NLP, or the QP when
+                                     use_nlp = 0; default 1e-9): with tol = 1e-6 there the forces stop up to 3e-2 N
+                                     from the exact optimum, with 1e-9 within 1e-5 N */
+    int polish;                   /* 1 (default): the last stage's result is polished to the exact KKT point of
+                                     its active set (forces within 1e-4 N of the optimum); 0 off */
 } srb12_params;
 
 void srb12_params_default(srb12_params *p, int N);
@@ -309,7 +334,8 @@ int srb12_nv(const srb12_params *p);   /* 24N + 1: X = x_1..x_N (12N) | U = u_0.
  *   x0 [A][12]; xref [A][N][12] (x_1..x_N); foot [A][N][4][3] (world foot positions per grid, legs FR FL
  *   RR RL); contact [A][N][4] int (1 stance); obstacles / nbr_state / n_obs / n_all / agent_offset /
  *   sel / obstacles_version as in srb_batch (the neighbour snapshot rows are [x, y, xdot, ydot]);
- *   outputs x_qp (may be NULL), x [A][24N+1], obj [A], status [A][2], iters [A][2] */
+ *   outputs x_qp (may be NULL), x [A][24N+1], obj [A], status [A][2], iters [A][2]; a FATAL (3) QP stage ends the
+ *   solve before the NLP stage, whose status then reads FATAL as well (use_nlp = 1) */
 typedef struct srb12_batch {
     int struct_size;              /* sizeof(srb12_batch) (ABI check) */
     const double *x0, *xref, *foot;

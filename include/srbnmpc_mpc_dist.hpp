@@ -76,11 +76,20 @@ using Vec4 = Mat;
 constexpr int NDOMAIN = 4;
 constexpr double INIT_FOOTPRINT[4][2] = {{0.2188, -0.1320}, {0.2188, 0.1320}, {-0.1472, -0.1320}, {-0.1472, 0.1320}};
 
+/* Horizon: the reference hard-codes N = NDOMAIN = 4 grids (MPC_dist.cpp:92, :104).  The second
+ * constructor argument generalises it (BASELINE configs[0]: horizon 10): the reference window still
+ * starts at column NDOMAIN * gaitDomain_ (a gait domain is NDOMAIN grids) and spans N columns, every
+ * grid gets the domain's footholds, get_MPCsol() is 4N x 1 and the Bezier fit keeps using X_0..X_3;
+ * the default N = NDOMAIN is the reference exactly. */
 class MPC_dist {
 public:
     bool use_snopt = false;       /* MPC_dist.hpp:139: false -> QP stage only (srb_solve_qp) */
 
-    explicit MPC_dist(int device = 0) : device_(device) {}
+    explicit MPC_dist(int device = 0, int horizon = NDOMAIN) : device_(device), N_(horizon)
+    {
+        if (horizon < NDOMAIN || horizon > 33) throw std::runtime_error("MPC_dist: horizon must be in [4, 33]");
+        X_.assign((size_t)(4 * N_), 0.0);
+    }
     MPC_dist(const MPC_dist &) = delete;
     MPC_dist &operator=(const MPC_dist &) = delete;
     ~MPC_dist()
@@ -146,9 +155,9 @@ public:
     /* MPC_dist.cpp:81-454 with the QP/NLP solve on the GPU (batch of one). */
     void run_NMPC()
     {
-        const int N = NDOMAIN;
-        double ref[4 * N];
-        copPlanner_eventbase(ref);
+        const int N = N_;
+        std::vector<double> ref((size_t)(4 * N));
+        copPlanner_eventbase(ref.data());
         std::vector<double> F;                       /* 2 x C, row-major */
         const int C = footholdsPlanner(F);
         std::vector<double> foot((size_t)N * 2 * C); /* same block every grid (:1256-1260) */
@@ -164,7 +173,7 @@ public:
         double obj = 0.0;
         srb_batch b{};
         b.struct_size = sizeof b;            /* ABI check (SRB_ABI_VERSION) */
-        b.x0 = x0; b.ref = ref; b.foot = foot.data();
+        b.x0 = x0; b.ref = ref.data(); b.foot = foot.data();
         b.obstacles = pobs_real_.empty() ? nullptr : pobs_real_.data();
         b.n_obs = (int)(pobs_real_.size() / 2);
         b.nbr_state = nullptr; b.n_all = 0; b.agent_offset = 0;
@@ -175,8 +184,7 @@ public:
         if (rc != SRB_OK) throw std::runtime_error(std::string("srb_solve_batch: ") + srb_last_error());
         /* copy-out :431-440, buffer update :798 */
         for (int i = 0; i < 4 * N; i++) X_[(size_t)i] = x_[(size_t)i];
-        for (int i = 0; i < N; i++) U0_[(size_t)i] = x_[(size_t)(4 * N + 2 * i)];
-        for (int d = 0; d < 4; d++) alpha_buffer_[(size_t)d] = X_[(size_t)(12 + d)];
+        for (int d = 0; d < 4; d++) alpha_buffer_[(size_t)d] = X_[(size_t)(4 * (NDOMAIN - 1) + d)];   /* the domain's end */
         gaitDomain_++;
     }
 
@@ -188,10 +196,10 @@ public:
             for (int j = 0; j < 5; j++) a(d, j) = alpha_[(size_t)(d * 5 + j)];
         return a;
     }
-    Mat get_MPCsol() const                         /* 16 x 1 predicted X (MPC_dist.hpp:179) */
+    Mat get_MPCsol() const                         /* 4N x 1 predicted X (16 x 1 in the reference, MPC_dist.hpp:179) */
     {
-        Mat m = Mat::Zero(4 * NDOMAIN, 1);
-        for (int i = 0; i < 4 * NDOMAIN; i++) m(i, 0) = X_[(size_t)i];
+        Mat m = Mat::Zero(4 * N_, 1);
+        for (int i = 0; i < 4 * N_; i++) m(i, 0) = X_[(size_t)i];
         return m;
     }
     int getDomain() const { return domain_; }
@@ -228,6 +236,7 @@ public:
     const std::vector<double> &Pr_refined() const { return pr_; }
     const std::vector<double> &Prd_refined() const { return prd_; }
     size_t gaitDomain() const { return gaitDomain_; }
+    int horizon() const { return N_; }
 
 private:
     template <class M> static void copy_obs(const M &P, std::vector<double> &out)
@@ -238,11 +247,11 @@ private:
 
     srb_ctx *context(int C, int use_nlp)
     {
-        const int key = C * 2 + use_nlp;
+        const int key = C * 2 + use_nlp;            /* one horizon per object */
         auto it = ctx_.find(key);
         if (it != ctx_.end()) return it->second;
         srb_params p;
-        srb_params_default(&p, NDOMAIN, C);   /* K_obs = 1 (closest obstacle), K_nbr = 0 */
+        srb_params_default(&p, N_, C);        /* K_obs = 1 (closest obstacle), K_nbr = 0 */
         p.use_nlp = use_nlp;
         srb_ctx *c = nullptr;
         if (srb_ctx_create(&p, 1, device_, &c) != SRB_OK)
@@ -251,13 +260,13 @@ private:
         return c;
     }
 
-    /* MPC_dist.cpp:702-782: 4 x N window of the HL path at columns N*gaitDomain_, flattened
+    /* MPC_dist.cpp:702-782: 4 x N window of the HL path from column NDOMAIN*gaitDomain_, flattened
      * column-major (x, xdot, y, ydot per grid). */
     void copPlanner_eventbase(double *ref) const
     {
         if (pr_.empty()) throw std::runtime_error("MPC_dist: setReferenceTrajectory() not called");
-        const int N = NDOMAIN;
-        const long c0 = (long)N * (long)gaitDomain_;
+        const int N = N_;
+        const long c0 = (long)NDOMAIN * (long)gaitDomain_;
         if (c0 + N > ref_cols_) throw std::runtime_error("MPC_dist: reference trajectory exhausted");
         const long r0 = 2 * (long)agent_id_;
         auto at = [&](const std::vector<double> &M, long r, long c) { return M[(size_t)(c * ref_rows_ + r)]; };
@@ -290,6 +299,7 @@ private:
     }
 
     int device_;
+    int N_;                                      /* horizon (grids) */
     size_t agent_id_ = 0, gaitDomain_ = 0;
     int domain_ = 0;
     bool is_success_ = true;
@@ -304,8 +314,7 @@ private:
     double state_other_[4] = {0};
     std::map<int, srb_ctx *> ctx_;
     std::vector<double> x_, x_qp_;
-    std::array<double, 4 * NDOMAIN> X_{};
-    std::array<double, NDOMAIN> U0_{};
+    std::vector<double> X_;
     std::array<double, 20> alpha_{};
     int status_[2] = {0, 0}, iters_[2] = {0, 0};
 };

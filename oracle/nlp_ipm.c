@@ -393,6 +393,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     int npassed = 0;                                        /* near-optimal iterates so far */
     int saved = 0, restore = 0;                             /* best near-optimal iterate */
     double best_rx = 1e300;
+    int provisional = 0;
     double *xsave = malloc(sizeof(double) * n), *ssave = malloc(sizeof(double) * m), *zsave = malloc(sizeof(double) * m);
     int nearwait = ORC_NLP_NEARWAIT;
     if (getenv("ORC_NLP_NEARWAIT")) nearwait = atoi(getenv("ORC_NLP_NEARWAIT"));
@@ -410,12 +411,22 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         double nrx = sqrt(dotv(rx, rx, n)), nrz = sqrt(dotv(rz, rz, m)), nry = sqrt(dotv(ry, ry, p));
         double sz = dotv(s, z, m);
         if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
+        {                                          /* divergence: ORC_Z_DIV (qp_ipm.c) */
+            double zm = 0.0;
+            for (int r = 0; r < m; r++) zm = fmax(zm, z[r]);
+            if (!(zm <= ORC_Z_DIV)) { flag = 3; break; }
+        }
         /* dual residual scaled by the objective gradient (the NLP's own criterion; the
          * QP stage keeps iSWIFT's absolute test): max(1, ||Q x + f||_inf) */
         double gmax = 1.0;
         for (int j = 0; j < n; j++) { double gj = fabs(Pd[j] * x[j] + c[j]); if (gj > gmax) gmax = gj; }
         const int pass = nrx < fx * th * gmax && nrz < th && nry < th && sz / m < fmu * tol;
-        if (pass && dxlast < fdx) { flag = 0; break; }
+        if (pass && dxlast < fdx) {
+            /* the loosened tests (ORC_NLP_EXITF) rely on the polish: met only by them, the result is
+             * provisional -- ACCEPTABLE unless the polish is accepted (the kernel, same rule) */
+            provisional = !(nrx < th * gmax && nrz < th && nry < th && sz / m < tol);
+            flag = 0; break;
+        }
         /* exploration: one early polish attempt once the complementarity gap is below early_mu */
         if (early_mu > 0 && !early_tried && sz / m < early_mu && nrz < early_rz) {
             early_tried = 1;
@@ -533,7 +544,8 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         for (int r = 0; r < m; r++) { s[r] += ap * dsv[r]; z[r] += ad * dz[r]; }
         it++;
     }
-    if (saved && (restore || flag == 2 || flag == 4)) {   /* ACCEPTABLE / MAXIT: the best saved iterate */
+    if (flag == 0 && provisional) flag = 4;
+    if (saved && !provisional && (restore || flag == 2 || flag == 4)) {   /* ACCEPTABLE / MAXIT: the best saved iterate */
         memcpy(x, xsave, sizeof(double) * n); memcpy(s, ssave, sizeof(double) * m); memcpy(z, zsave, sizeof(double) * m);
         flag = 4;
     }

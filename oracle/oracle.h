@@ -78,6 +78,10 @@ void orc_select_obstacles(const orc_params *p, const double x0[4],
                           double *obs_out, double *eps_out);
 
 /* iSWIFT algorithm restated (Prime.c:127-230, Auxilary.c); returns 0..3 exit code. */
+/* the NMPC's divergence rule (both stages): a dual beyond this ends the solve FATAL at its finite
+ * iterate (infeasible rows; converging solves keep their duals below ~1e4) -- srb_kernels.hip,
+ * srb12_kernels.hip and oracle/srb12.c apply the same threshold */
+#define ORC_Z_DIV 1e10
 /* qp_init: 0 = iSWIFT's kkt_initialize (Auxilary.c:680-755), 1 = scaled start (qp_ipm.c) */
 int orc_qp_solve_init(int n, int m, int p, const double *Pd, const double *c, const double *A, const double *b,
                       const double *G, const double *h, int maxit, double tol, int qp_init, double *x_out, double *q_out,
@@ -180,10 +184,13 @@ typedef struct orc12_params {
     double eps_obs, eps_nbr, tol;
     int qp_maxit, nlp_maxit, use_nlp;
     double z0;                          /* NLP initial duals z0 / max(s, 1) */
+    double tol_final;                   /* complementarity tolerance of the last stage (srb12_params) */
+    int polish;                         /* 1: active-set polish of the last stage's result */
 } orc12_params;
 
 void orc12_params_default(orc12_params *p, int N);
-int orc12_nv(const orc12_params *p);   /* 24N + 1: X (12N) | U (12N) | s */
+int orc12_nv(const orc12_params *p);
+extern int orc12_polish_stats[4];      /* polishes rejected, accepted, Newton steps, most steps of one solve */   /* 24N + 1: X (12N) | U (12N) | s */
 void orc12_dynamics(const orc12_params *p, const double x0[12], const double *xref, const double *foot,
                     const int *contact, double *A, double *B, double *c);
 int orc12_solve_agent(const orc12_params *p, const double x0[12], const double *xref, const double *foot,

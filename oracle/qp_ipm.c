@@ -139,7 +139,7 @@ static double steplen(const double *v, const double *dv, int m)
 static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf, const double *c,
                          const double *A, const double *b, const double *G, const double *h,
                          int maxit, double tol, double *x_out, double *q_out, int *iters_out, int no_trap,
-                         int *trapped, int qp_init)
+                         int *trapped, int qp_init, double zdiv)
 {
     kktws w;
     ws_init(&w, n, m, p, Pd, A, G);
@@ -199,6 +199,15 @@ static int qp_solve_impl(int n, int m, int p, const double *Pd, const double *Pf
         gmul(&w, x, rz);
         for (int r = 0; r < m; r++) rz[r] = h[r] - s[r] - rz[r];
         const double th = tol / sqrt(3.0);
+        /* divergence (zdiv > 0: the NMPC's QP stage, ORC_Z_DIV): a dual beyond zdiv means the rows
+         * are infeasible -- the duals of converging solves stay below ~1e4 on every workload, those of
+         * infeasible ones pass 1e10 within a few iterations and then overflow.  FATAL at this
+         * (finite) iterate, as the kernel (srb_kernels.hip, the same rule and threshold) */
+        if (zdiv > 0) {
+            double zm = 0.0;
+            for (int r = 0; r < m; r++) zm = fmax(zm, z[r]);
+            if (!(zm <= zdiv)) { flag = 3; break; }
+        }
         if (norm2(rx, n) < th && norm2(rz, m) < th && (p == 0 || norm2(ry, p) < th) && dot(s, z, m) / m < tol) {
             flag = 0; break;
         }
@@ -255,14 +264,14 @@ int orc_qp_solve_init(int n, int m, int p, const double *Pd, const double *c, co
                       const double *G, const double *h, int maxit, double tol, int qp_init, double *x_out, double *q_out,
                       int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, qp_init);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, qp_init, ORC_Z_DIV);
 }
 
 int orc_qp_solve(int n, int m, int p, const double *Pd, const double *c,
                  const double *A, const double *b, const double *G, const double *h,
                  int maxit, double tol, double *x_out, double *q_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, 0);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, q_out, iters_out, 0, NULL, 0, 0.0);
 }
 
 /* iSWIFT with the sigma <= sigma_d branch (Prime.c:193-196) disabled.  The step-length rule keeps
@@ -274,7 +283,7 @@ int orc_qp_solve_nt(int n, int m, int p, const double *Pd, const double *c,
                     const double *A, const double *b, const double *G, const double *h,
                     int maxit, double tol, double *x_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 1, NULL, 0);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 1, NULL, 0, 0.0);
 }
 
 /* iSWIFT semantics, reporting whether the sigma <= sigma_d branch was taken */
@@ -283,7 +292,7 @@ int orc_qp_solve_trap(int n, int m, int p, const double *Pd, const double *c,
                       int maxit, double tol, double *x_out, int *iters_out, int *trapped)
 {
     *trapped = 0;
-    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, trapped, 0);
+    return qp_solve_impl(n, m, p, Pd, NULL, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, trapped, 0, 0.0);
 }
 
 /* general (full, symmetric) P -- used for iSWIFT's own test QP (Matrices_small.h) */
@@ -291,5 +300,5 @@ int orc_qp_solve_full(int n, int m, int p, const double *P, const double *c,
                       const double *A, const double *b, const double *G, const double *h,
                       int maxit, double tol, double *x_out, int *iters_out)
 {
-    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, NULL, 0);
+    return qp_solve_impl(n, m, p, NULL, P, c, A, b, G, h, maxit, tol, x_out, NULL, iters_out, 0, NULL, 0, 0.0);
 }

@@ -59,6 +59,8 @@ void orc12_params_default(orc12_params *p, int N)
     p->eps_obs = (double)1.9f; p->eps_nbr = (double)2.2f;              /* dec_vars_constr_cost.h:401-402 */
     p->tol = 1e-6; p->qp_maxit = 25; p->nlp_maxit = 50; p->use_nlp = 1;
     p->z0 = 100.0;                       /* the LIP mode's SRB_NLP_Z0: 6.9 NLP iterations on average at 64 trot agents, against 9.8 (z0 = 1) and 8.6 (10) */
+    p->tol_final = 1e-9;                 /* last stage: forces within 1e-5 N of the exact optimum (3e-2 N at 1e-6) */
+    p->polish = 1;
 }
 
 int orc12_nv(const orc12_params *p) { return 24 * p->N + 1; }
@@ -179,12 +181,137 @@ static int reduced_pd(const p12_t *P, const double *Hf)
     return ok;
 }
 
+/* ---------------------------------------------------------------------------- active-set polish
+ * The last stage's OPTIMAL iterate is polished to the exact KKT point of its active set (the LIP
+ * mode's rule, oracle/nlp_ipm.c `polish`, restated for this problem; the kernel does the same steps
+ * with its Riccati recursion).  Rows with s KAPPA < z form the active set A; min f s.t. dynamics,
+ * g_A(x) = h_A is solved by Newton steps on the augmented Lagrangian
+ *   (H_L + RHO J_A'J_A) dx = -(grad f + J_A'(z_A + RHO c_A)),
+ *   z_A += RHO (c_A + J_A dx)
+ * (H_L: the cost Hessian and -2 y on (p_x, p_y) of active obstacle rows, y = z_A + RHO c_A the current
+ * multiplier estimate).  At most IT steps per
+ * pass (fewer once |dx| <= DXTOL); accepted when every row holds to PTOL, the active rows to PTOL,
+ * z_A >= -1e-9 max|z_A| and the last step is <= DXTOL; otherwise the most negative multiplier
+ * leaves A, violated rows join and the next pass starts again from the interior-point point (at most
+ * PASSES).  The steps after a pass's first reuse its factor (the kernel's rule: one Riccati factor per
+ * pass; measured no different in acceptance or accuracy from refactoring every step).  Unlike the LIP
+ * polish there is no proximal term on the inactive rows: the cost alone (q, r > 0) makes the matrix
+ * definite, and a proximal weight the size of r = 1e-2 slowed the Newton iteration to a crawl.  Why: the forces are pinned by the friction rows and the r = 1e-2 weight alone along the
+ * legs' internal-force directions, so an interior-point iterate at s'z/m ~ 1e-9 still sits up to
+ * 1e-3 N from the optimum there; the active set's KKT point is exact. */
+#define ORC12_POL_RHO 1e9
+#define ORC12_POL_KAPPA 1e4
+#define ORC12_POL_IT 3
+#define ORC12_POL_PASSES 2
+#define ORC12_POL_PTOL 1e-9
+#define ORC12_POL_DXTOL 1e-7
+
+/* diagnostics for the tests: polishes rejected, accepted, Newton steps in all, most steps of one solve */
+int orc12_polish_stats[4];
+
+/* returns 1 (accepted: x replaced by the polished point) or 0; *steps: Newton steps taken */
+static int polish12(const p12_t *P, int nl, double *x, const double *s, const double *zd, int *steps)
+{
+    const int n = P->n, p = P->p, m = P->mlin + (nl ? P->mc : 0), nk = n + p;
+    double *xt = malloc(sizeof(double) * n), *g = malloc(sizeof(double) * (m ? m : 1));
+    double *J = malloc(sizeof(double) * (size_t)(m ? m : 1) * n), *za = malloc(sizeof(double) * (m ? m : 1));
+    double *Hf = malloc(sizeof(double) * (size_t)n * n), *KK = malloc(sizeof(double) * (size_t)nk * nk);
+    double *rhs = malloc(sizeof(double) * nk);
+    int *act = malloc(sizeof(int) * (m ? m : 1)), *piv = malloc(sizeof(int) * nk);
+    int accepted = 0;
+    *steps = 0;
+    for (int r = 0; r < m; r++) { act[r] = s[r] * ORC12_POL_KAPPA < zd[r]; za[r] = act[r] ? zd[r] : 0.0; }
+    for (int pass = 0; pass < ORC12_POL_PASSES && !accepted; pass++) {
+        memcpy(xt, x, sizeof(double) * n);
+        double lastdx = 1e300;
+        int bad = 0;
+        for (int it = 0; it < ORC12_POL_IT; it++) {
+            rows_eval(P, xt, nl, g, J);
+            memset(Hf, 0, sizeof(double) * (size_t)n * n);
+            for (int i = 0; i < n; i++) { Hf[(size_t)i * n + i] = P->Pd[i]; rhs[i] = -(P->Pd[i] * xt[i] + P->cv[i]); }
+            for (int r = 0; r < m; r++) {
+                const double *Jr = J + (size_t)r * n;
+                const double c = g[r] - h_of(P, r);
+                const double w = act[r] ? ORC12_POL_RHO : 0.0;
+                const double y = act[r] ? za[r] + ORC12_POL_RHO * c : 0.0;
+                if (act[r] && r >= P->mlin) {           /* -2 y on (p_x, p_y) of the row's grid, y = z_A + RHO c_A */
+                    const int k = (r - P->mlin) / P->K;
+                    Hf[(size_t)(12 * k) * n + 12 * k] -= 2.0 * y; Hf[(size_t)(12 * k + 1) * n + 12 * k + 1] -= 2.0 * y;
+                }
+                for (int i = 0; i < n; i++) {
+                    if (Jr[i] == 0.0) continue;
+                    rhs[i] -= Jr[i] * y;
+                    for (int j = 0; j < n; j++) if (Jr[j] != 0.0) Hf[(size_t)i * n + j] += w * Jr[i] * Jr[j];
+                }
+            }
+            const int frz = it > 0;          /* later steps of a pass reuse the first step's factor */
+            if (!frz && !reduced_pd(P, Hf)) { bad = 1; break; }          /* the kernel's Riccati pivots fail there */
+            if (!frz) memset(KK, 0, sizeof(double) * (size_t)nk * nk);
+            if (!frz) for (int i = 0; i < n; i++) memcpy(KK + (size_t)i * nk, Hf + (size_t)i * n, sizeof(double) * n);
+            for (int r = 0; r < p; r++) {
+                double v = -P->beq[r];
+                for (int j = 0; j < n; j++) {
+                    if (!frz) { KK[(size_t)(n + r) * nk + j] = P->Aeq[(size_t)r * n + j]; KK[(size_t)j * nk + n + r] = P->Aeq[(size_t)r * n + j]; }
+                    v += P->Aeq[(size_t)r * n + j] * xt[j];
+                }
+                rhs[n + r] = -v;
+            }
+            if (!frz && orc_lu(nk, KK, piv) != 0) { bad = 1; break; }
+            orc_lu_solve(nk, KK, piv, rhs);
+            double mdx = 0.0;
+            for (int r = 0; r < m; r++)
+                if (act[r]) {
+                    const double *Jr = J + (size_t)r * n;
+                    double jd = 0.0;
+                    for (int i = 0; i < n; i++) if (Jr[i] != 0.0) jd += Jr[i] * rhs[i];
+                    za[r] += ORC12_POL_RHO * (g[r] - h_of(P, r) + jd);
+                }
+            for (int i = 0; i < n; i++) { xt[i] += rhs[i]; mdx = fmax(mdx, fabs(rhs[i])); }
+            (*steps)++;
+            lastdx = mdx;
+            if (getenv("ORC12_TRACE")) fprintf(stderr, "        polish step %d |dx| %.3e\n", it, mdx);
+            if (mdx <= ORC12_POL_DXTOL) break;
+        }
+        if (bad) break;
+        /* acceptance at the polished point */
+        rows_eval(P, xt, nl, g, NULL);
+        double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0;
+        for (int r = 0; r < m; r++) {
+            const double v = g[r] - h_of(P, r);
+            pv = fmax(pv, v);
+            if (act[r]) { cv = fmax(cv, fabs(v)); nzmin = fmax(nzmin, -za[r]); zm = fmax(zm, fabs(za[r])); }
+        }
+        if (getenv("ORC12_TRACE"))
+            fprintf(stderr, "      polish pass %d: primal %.2e |c_A| %.2e -min z_A %.2e last dx %.2e\n", pass, pv, cv, nzmin, lastdx);
+        if (pv <= ORC12_POL_PTOL && cv <= ORC12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= ORC12_POL_DXTOL) {
+            memcpy(x, xt, sizeof(double) * n);
+            accepted = 1;
+            break;
+        }
+        /* next pass: the most negative multiplier leaves, violated rows join (multiplier 0) */
+        int wk = -1;
+        double wd = -1e-9 * zm;
+        for (int r = 0; r < m; r++) if (act[r] && za[r] < wd) { wd = za[r]; wk = r; }
+        int changed = 0;
+        for (int r = 0; r < m; r++) {
+            if (r == wk) { act[r] = 0; changed = 1; }
+            else if (!act[r] && g[r] - h_of(P, r) > ORC12_POL_PTOL) { act[r] = 1; changed = 1; }
+            za[r] = act[r] ? fmax(za[r], 0.0) : 0.0;
+        }
+        if (!changed) break;
+    }
+    free(xt); free(g); free(J); free(za); free(Hf); free(KK); free(rhs); free(act); free(piv);
+    return accepted;
+}
+
 /* one interior-point stage; z (n), lam (p) in/out; returns 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL */
 static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
 {
     const orc12_params *prm = P->prm;
     const int n = P->n, p = P->p, m = P->mlin + (nl ? P->mc : 0), nk = n + p;
     const double tol = prm->tol, th = tol / sqrt(3.0);
+    /* the last stage (the NLP, or the QP alone) ends at s'z/m < tol_final: the forces' accuracy */
+    const double mtol = (nl || !prm->use_nlp) ? prm->tol_final : tol;
     double *g = malloc(sizeof(double) * m), *J = malloc(sizeof(double) * (size_t)m * n);
     double *s = malloc(sizeof(double) * m), *zd = malloc(sizeof(double) * m);
     double *rd = malloc(sizeof(double) * n), *rp = malloc(sizeof(double) * m), *req = malloc(sizeof(double) * p);
@@ -246,10 +373,14 @@ static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
         }
         nrd = sqrt(nrd); nrp = sqrt(nrp);
         const double mu = sz / (m > 0 ? m : 1);
-        if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz)) { flag = 3; break; }
+        {                                          /* divergence: ORC_Z_DIV (the LIP mode's rule) */
+            double zm = 0.0;
+            for (int r = 0; r < m; r++) zm = fmax(zm, zd[r]);
+            if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz) || !(zm <= ORC_Z_DIV)) { flag = 3; break; }
+        }
         if (getenv("ORC12_TRACE"))
             fprintf(stderr, "  %s it %2d |rd| %.3e (th %.3e) |rp| %.3e mu %.3e sigma %.3e\n", nl ? "nlp" : "qp ", it, nrd, th * gm, nrp, mu, sigma);
-        if (nrd < th * gm && nrp < th && mu < tol) { flag = 0; break; }
+        if (nrd < th * gm && nrp < th && mu < mtol) { flag = 0; break; }
         /* Hessian of the Lagrangian + J' W J */
         memset(Hf, 0, sizeof(double) * (size_t)n * n);
         for (int i = 0; i < n; i++) Hf[(size_t)i * n + i] = P->Pd[i];
@@ -328,6 +459,14 @@ static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
         for (int r = 0; r < m; r++) { s[r] += ap * ds[r]; zd[r] += ad * dzd[r]; }
     }
     *iters = it;
+    if (flag == 0 && (nl || !prm->use_nlp) && prm->polish) {         /* the last stage: exact active-set point */
+        int steps = 0;
+        const int acc = polish12(P, nl, z, s, zd, &steps);
+        __atomic_fetch_add(&orc12_polish_stats[acc], 1, __ATOMIC_RELAXED);
+        __atomic_fetch_add(&orc12_polish_stats[2], steps, __ATOMIC_RELAXED);
+        int old = orc12_polish_stats[3];
+        while (steps > old && !__atomic_compare_exchange_n(&orc12_polish_stats[3], &old, steps, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+    }
     free(g); free(J); free(s); free(zd); free(rd); free(rp); free(req); free(Hf); free(KK); free(rhs); free(om); free(r3);
     free(dz); free(dl); free(ds); free(dzd); free(dsa); free(dza); free(piv);
     return flag;
@@ -431,7 +570,8 @@ int orc12_solve_agent(const orc12_params *p_in, const double x0[12], const doubl
     }
     status[0] = ipm(&P, 0, z, lam, &iters[0]);
     if (x_qp) memcpy(x_qp, z, sizeof(double) * n);
-    status[1] = 0; iters[1] = 0;
+    status[1] = (prm->use_nlp && status[0] == 3) ? 3 : 0;      /* FATAL QP: the NLP stage is not run (kernel, same rule) */
+    iters[1] = 0;
     double *obs = NULL, *eps = NULL;
     if (prm->use_nlp && K > 0 && status[0] != 3) {
         /* the selection and prediction of the LIP mode, on the CoM position / velocity */

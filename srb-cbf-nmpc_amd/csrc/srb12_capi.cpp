@@ -15,6 +15,7 @@ int srb_internal_fail(int code, const char *msg);
 int srb_internal_select(srb_ctx *c, int n_agents, const double *x0, const double *obstacles, int n_obs,
                         const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
                         int obstacles_version, int *sel, hipStream_t s);
+int srb_internal_mark_done(srb_ctx *c, hipStream_t s);
 
 typedef void (*srb12_fn)(Srb12KParams, int, const double *, const double *, const double *, const int *,
                          const double *, const double *, const int *, double *, double *, double *, int *, int *);
@@ -69,6 +70,8 @@ extern "C" void srb12_params_default(srb12_params *p, int N)
     p->eps_obs = (double)1.9f; p->eps_nbr = (double)2.2f;
     p->tol = 1e-6; p->qp_maxit = 25; p->nlp_maxit = 50; p->use_nlp = 1;
     p->z0 = 100.0;
+    p->tol_final = 1e-9;
+    p->polish = 1;
 }
 
 extern "C" int srb12_nv(const srb12_params *p) { return 24 * p->N + 1; }
@@ -87,8 +90,8 @@ static int validate12(const srb12_params *p)
     if (p->N < 1 || p->N > SRB12_MAX_N) return srb_internal_fail(SRB_ERR_SIZE, "SRB-12 mode: need 1 <= N <= 24");
     if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs > SRB_KNN_MAX || p->K_nbr > SRB_KNN_MAX)
         return srb_internal_fail(SRB_ERR_ARG, "K_obs, K_nbr out of range (each <= 16)");
-    if (!(p->mass > 0) || !(p->Ts > 0) || !(p->tol > 0) || !(p->mu >= 0) || !(p->fmax > 0) || !(p->Sw > 0))
-        return srb_internal_fail(SRB_ERR_ARG, "srb12_params out of range (mass, Ts, tol, fmax, Sw > 0)");
+    if (!(p->mass > 0) || !(p->Ts > 0) || !(p->tol > 0) || !(p->tol_final > 0) || !(p->mu >= 0) || !(p->fmax > 0) || !(p->Sw > 0))
+        return srb_internal_fail(SRB_ERR_ARG, "srb12_params out of range (mass, Ts, tol, tol_final, fmax, Sw > 0)");
     for (int i = 0; i < 12; i++)
         if (!(p->q[i] >= 0) || !(p->qN[i] >= 0)) return srb_internal_fail(SRB_ERR_ARG, "state weights must be >= 0");
     for (int i = 0; i < 3; i++)
@@ -111,7 +114,7 @@ static Srb12KParams make_k12(const srb12_params *p, int K_obs, int K_nbr)
     k.N = p->N; k.K_obs = K_obs; k.K_nbr = K_nbr; k.use_nlp = p->use_nlp ? 1 : 0;
     k.qp_maxit = p->qp_maxit; k.nlp_maxit = p->nlp_maxit;
     k.Ts = p->Ts; k.mass = p->mass; k.grav = p->grav; k.mus = p->mu / std::sqrt(2.0); k.fmax = p->fmax;
-    k.Sw = p->Sw; k.eps_obs = p->eps_obs; k.eps_nbr = p->eps_nbr; k.tol = p->tol; k.z0 = p->z0;
+    k.Sw = p->Sw; k.eps_obs = p->eps_obs; k.eps_nbr = p->eps_nbr; k.tol = p->tol; k.z0 = p->z0; k.tol_final = p->tol_final; k.polish = p->polish ? 1 : 0;
     std::memcpy(k.Ib, p->Ib, sizeof k.Ib);
     std::memcpy(k.q, p->q, sizeof k.q); std::memcpy(k.qN, p->qN, sizeof k.qN); std::memcpy(k.r, p->r, sizeof k.r);
     return k;
@@ -133,24 +136,36 @@ extern "C" int srb12_ctx_create(const srb12_params *p, int max_agents, int devic
     if ((rc = srb_ctx_create(&sp, max_agents, device, &sc))) return rc;
     srb12_ctx *c = new srb12_ctx();
     std::memset(c, 0, sizeof *c);
+    // a failure after this point unwinds through srb12_ctx_destroy (it null-checks every buffer and
+    // destroys the selection context); *out stays untouched
+#define CREATE_CHK(expr)                                                                                \
+    do {                                                                                                \
+        hipError_t e_ = (expr);                                                                         \
+        if (e_ != hipSuccess) {                                                                         \
+            const int rc_ = srb_internal_fail(SRB_ERR_HIP, (std::string(#expr ": ") + hipGetErrorString(e_)).c_str()); \
+            srb12_ctx_destroy(c);   /* sets no error: the message above stays */                      \
+            return rc_;                                                                                 \
+        }                                                                                               \
+    } while (0)
     c->p = *p; c->max_agents = max_agents; c->device = device; c->sel_ctx = sc;
     const size_t A = (size_t)max_agents, N = (size_t)p->N, nv = 24 * N + 1;
-    H12CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int i = 0; i < 3; i++) H12CHK(hipEventCreate(&c->ev[i]));
-    H12CHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
-    H12CHK(hipMalloc(&c->pos, A * 4 * sizeof(double)));
-    H12CHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
-    H12CHK(hipMalloc(&c->x0, A * 12 * sizeof(double)));
-    H12CHK(hipMalloc(&c->xref, A * 12 * N * sizeof(double)));
-    H12CHK(hipMalloc(&c->foot, A * 12 * N * sizeof(double)));
-    H12CHK(hipMalloc(&c->contact, A * 4 * N * sizeof(int)));
-    H12CHK(hipMalloc(&c->x_qp, A * nv * sizeof(double)));
-    H12CHK(hipMalloc(&c->x, A * nv * sizeof(double)));
-    H12CHK(hipMalloc(&c->obj, A * sizeof(double)));
-    H12CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
-    H12CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
-    H12CHK(hipMalloc(&c->dbg, (2 * 64 * 8 + 16) * sizeof(double)));
+    CREATE_CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 3; i++) CREATE_CHK(hipEventCreate(&c->ev[i]));
+    CREATE_CHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    CREATE_CHK(hipMalloc(&c->pos, A * 4 * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->x0, A * 12 * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->xref, A * 12 * N * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->foot, A * 12 * N * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->contact, A * 4 * N * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->x_qp, A * nv * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->x, A * nv * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->obj, A * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->dbg, (2 * 64 * 8 + 16) * sizeof(double)));
     c->dbg_agent = -1;
+#undef CREATE_CHK
     *out = c;
     return SRB_OK;
 }
@@ -159,15 +174,16 @@ extern "C" int srb12_ctx_destroy(srb12_ctx *c)
 {
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->any) (void)hipEventSynchronize(c->done);
     void *bufs[] = {c->dbg, c->pos, c->sel, c->x0, c->xref, c->foot, c->contact, c->obstacles, c->nbr, c->x_qp, c->x, c->obj,
                     c->status, c->iters};
     for (void *b : bufs)
         if (b) (void)hipFree(b);
-    for (int i = 0; i < 3; i++) (void)hipEventDestroy(c->ev[i]);
-    (void)hipEventDestroy(c->done);
-    (void)hipStreamDestroy(c->stream);
+    for (int i = 0; i < 3; i++)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     srb_ctx_destroy(c->sel_ctx);
     delete c;
     return SRB_OK;
@@ -177,6 +193,18 @@ static int order12(srb12_ctx *c, hipStream_t s)
 {
     if (c->any && s != c->last) H12CHK(hipStreamWaitEvent(s, c->done, 0));
     return SRB_OK;
+}
+
+// "up to K nearest": the rows selected per agent, clamped to what the tables hold (batch-uniform, as
+// the LIP mode) and 0 without the NLP stage -- the launch and the host copy-back of sel use this one rule
+static void clamp_rows(const srb12_params *p, const srb12_batch *d, int *Ko, int *Kn)
+{
+    int ko = p->K_obs, kn = p->K_nbr;
+    if (ko > d->n_obs) ko = d->n_obs > 0 ? d->n_obs : 0;
+    const int others = d->nbr_state ? d->n_all - 1 : 0;
+    if (kn > others) kn = others > 0 ? others : 0;
+    if (!p->use_nlp) ko = kn = 0;
+    *Ko = ko; *Kn = kn;
 }
 
 static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_t s)
@@ -190,12 +218,8 @@ static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_
         return srb_internal_fail(SRB_ERR_ARG, "obstacles missing");
     if (p->use_nlp && p->K_nbr > 0 && d->nbr_state && (d->agent_offset < 0 || d->agent_offset + n_agents > d->n_all))
         return srb_internal_fail(SRB_ERR_ARG, "agent_offset out of range of the neighbour table");
-    // "up to K nearest": clamp to what exists (batch-uniform), as the LIP mode
-    int Ko = p->K_obs, Kn = p->K_nbr;
-    if (Ko > d->n_obs) Ko = d->n_obs > 0 ? d->n_obs : 0;
-    const int others = d->nbr_state ? d->n_all - 1 : 0;
-    if (Kn > others) Kn = others > 0 ? others : 0;
-    if (!p->use_nlp) Ko = Kn = 0;
+    int Ko = 0, Kn = 0;
+    clamp_rows(p, d, &Ko, &Kn);
     Srb12KParams k = make_k12(p, Ko, Kn);
     k.dbg_agent = c->dbg_agent; k.dbg = c->dbg;
     const srb12_inst *in = pick12(p);
@@ -209,6 +233,9 @@ static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_
         int rc = srb_internal_select(c->sel_ctx, n_agents, c->pos, d->obstacles, Ko > 0 ? d->n_obs : 0, d->nbr_state,
                                      Kn > 0 ? d->n_all : 0, d->agent_offset, Ko, Kn, d->obstacles_version, sel, s);
         if (rc) return rc;
+        // the selection context's own ordering event: its grid buffers are reallocated only after
+        // this launch (grid_reserve waits on it)
+        if ((rc = srb_internal_mark_done(c->sel_ctx, s))) return rc;
     }
     H12CHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->xref, d->foot, d->contact,
@@ -292,8 +319,9 @@ extern "C" int srb12_solve_batch(srb12_ctx *c, int n_agents, const srb12_batch *
     H12CHK(hipMemcpyAsync(h->status, c->status, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     H12CHK(hipMemcpyAsync(h->iters, c->iters, A * 2 * sizeof(int), hipMemcpyDeviceToHost, s));
     if (h->sel) {
-        const int Kt = (c->p.K_obs < h->n_obs ? c->p.K_obs : (h->n_obs > 0 ? h->n_obs : 0)) +
-                       (c->p.K_nbr < (h->nbr_state ? h->n_all - 1 : 0) ? c->p.K_nbr : (h->nbr_state && h->n_all > 1 ? h->n_all - 1 : 0));
+        int Ko = 0, Kn = 0;
+        clamp_rows(&c->p, h, &Ko, &Kn);
+        const int Kt = Ko + Kn;
         if (Kt > 0) H12CHK(hipMemcpyAsync(h->sel, c->sel, A * Kt * sizeof(int), hipMemcpyDeviceToHost, s));
     }
     H12CHK(hipStreamSynchronize(s));

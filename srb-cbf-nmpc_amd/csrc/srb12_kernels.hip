@@ -40,7 +40,7 @@ namespace {
 
 struct Srb12Lds {
     double *Wl, *cs, *ct, *Lm, *Hx, *V0, *Gt, *Ft, *Mt, *Q3, *Rh, *Z, *xr, *gX, *gU;
-    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *obs, *eps;
+    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *obs, *eps, *xsv;
     int *sel;
 };
 
@@ -59,6 +59,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     L.gX = L.rX + 13 * N; L.gU = L.rU + 12 * N;              // gradients: column 1 (free until the refinement)
     L.gus = p; p += 12 * N; L.vv = p; p += 16; L.sc = p; p += 16;
     L.obs = p; p += 2 * N * K; L.eps = p; p += K;
+    L.xsv = p; p += 24 * N + 1;                             // the interior-point result (polish)
     L.sel = (int *)p;
     return L;
 }
@@ -226,33 +227,353 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     double ss[TS], zz[TS], dsa[TS], dza[TS];
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
+    int nrow = nf;                                      // rows of the current stage (row_g)
+    auto row_g = [&](int id, double &g, double &h, double &c0, double &c1, double &c2, int &kind) {
+        g = 0.0; h = 0.0; c0 = c1 = c2 = 0.0; kind = 0;
+        if (id < nf) {
+            const int k = id / 24, l = (id / 6) & 3, q = id % 6;
+            if (L.ct[4 * k + l] != 0.0) {
+                kind = 1;
+                fric_coef(q, mus, c0, c1, c2);
+                const double *u = U + 12 * k + 3 * l;
+                g = c0 * u[0] + c1 * u[1] + c2 * u[2];
+                h = (q == 5) ? prm.fmax : 0.0;
+            }
+        } else if (id < nrow) {
+            const int e = id - nf, k = e / K, j = e - k * K;
+            kind = 2;
+            const double dx = X[12 * k] - L.obs[2 * e], dy = X[12 * k + 1] - L.obs[2 * e + 1];
+            c0 = -2.0 * dx; c1 = -2.0 * dy;
+            g = -(dx * dx + dy * dy) - L.Z[24 * N];
+            h = -L.eps[j];
+        }
+    };
+    // Q^_k (state block k, 13 x 13): diag(q) + delta on the 12 states, the obstacle rows' (p_x, p_y, s)
+    // block; the slack's own weight Sw + delta enters once, at s_0
+    auto qhat = [&](int k, int i, int j, double delta) {
+        double v = (i == j && i < 12) ? ((k == N - 1) ? prm.qN[i] : prm.q[i]) + delta : 0.0;
+        const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
+        if (pi && pj) {
+            const double *q3 = L.Q3 + 6 * k;
+            const int a = (i == 12) ? 2 : i, b = (j == 12) ? 2 : j;
+            const int lo = a < b ? a : b, hi = a < b ? b : a;
+            v += (lo == 0) ? (hi == 0 ? q3[0] : hi == 1 ? q3[1] : q3[3]) : (lo == 1) ? (hi == 1 ? q3[2] : q3[4]) : q3[5];
+        }
+        return v;
+    };
+    // backward Riccati factor over the 13-state with the shift delta; false when a pivot (the inertia
+    // test) or the initial slack's Schur complement is not positive.  Reads the per-grid Hessian blocks
+    // (Q3, Rh), writes Z = D^-1/2 L^-1 and Hux per grid and sets `schur`
+    double schur = 0.0;
+    auto factor = [&](double delta) -> bool {
+        int fail = 0;
+        for (int e = tid; e < 169; e += 64) L.V0[e] = qhat(N - 1, e / 13, e % 13, delta);
+        SYNC();
+        for (int k = N - 1; k >= 0; k--) {
+            const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = L.V0;
+            // G = V A~_k (13 x 13), F = V B~_k (13 x 12)
+            for (int e = tid; e < 169; e += 64) {
+                const int i = e / 13, j = e - 13 * i;
+                const double *Vi = V + 13 * i;
+                double g = Vi[j];
+                if (j >= 6 && j < 9) g = fma(Ts, Vi[j - 6], g);
+                else if (j >= 9 && j < 12) g = fma(Ts, Vi[3] * rzab(j - 9, 0, c, s) + Vi[4] * rzab(j - 9, 1, c, s) + Vi[5] * rzab(j - 9, 2, c, s), g);
+                L.Gt[e] = g;
+            }
+            for (int e = tid; e < 156; e += 64) {
+                const int i = e / 12, j = e - 12 * i, l = j / 3, jj = j - 3 * l;
+                const double *Vi = V + 13 * i;
+                double f = ct[l] * tsm * Vi[6 + jj];
+                for (int a = 0; a < 3; a++) f = fma(Vi[9 + a], W[9 * l + 3 * a + jj], f);
+                L.Ft[e] = f;
+            }
+            SYNC();
+            // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
+            // V_0[12][12] is used (the initial slack's Schur complement)
+            double *Hx = L.Hx + 156 * k, *Vn = L.V0;
+            for (int e = tid; e < 156; e += 64) {
+                const int i = e / 13, j = e - 13 * i;
+                const int li = i / 3, ai = i - 3 * li;
+                double hx = ct[li] * tsm * L.Gt[13 * (6 + ai) + j];
+                for (int a = 0; a < 3; a++) hx = fma(W[9 * li + 3 * a + ai], L.Gt[13 * (9 + a) + j], hx);
+                Hx[e] = hx;
+            }
+            for (int e = tid; e < 169; e += 64) {
+                const int i = e / 13, j = e - 13 * i;
+                double w = L.Gt[e];
+                if (i >= 6 && i < 9) w = fma(Ts, L.Gt[13 * (i - 6) + j], w);
+                else if (i >= 9 && i < 12)
+                    w = fma(Ts, rzab(i - 9, 0, c, s) * L.Gt[39 + j] + rzab(i - 9, 1, c, s) * L.Gt[52 + j] +
+                                    rzab(i - 9, 2, c, s) * L.Gt[65 + j], w);
+                if (k > 0) w += qhat(k - 1, i, j, delta);
+                Vn[e] = w;
+            }
+            SYNC();
+            // Hu = R^ + B'F = L D L' by a forward elimination of [Hu | Hux | I] in registers (row i16
+            // per lane, replicated in every 16-lane row): its pivots are the inertia test, Z = D^-1/2 L^-1
+            // (stored: the solves apply Hu^-1 = Z'Z) and Y = Z Hux, so the Schur update
+            // S = Hux' Hu^-1 Hux = Y'Y is one 16x16x16 product on the matrix cores.  The product with
+            // an explicit inverse, Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on
+            // active rows; Y'Y is positive semi-definite by construction.
+            {
+                const int i16 = lane & 15, q = lane >> 4;
+                double Ag[37];
+                {
+                    const int li = (i16 < 12) ? i16 / 3 : 0, ai = (i16 < 12) ? i16 - 3 * li : 0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) {
+                        double v = 0.0;
+                        if (i16 < 12) {
+                            v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
+                            for (int aa = 0; aa < 3; aa++) v = fma(W[9 * li + 3 * aa + ai], L.Ft[12 * (9 + aa) + j], v);
+                            if (j == i16) v += prm.r[ai] + delta;
+                            if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
+                        }
+                        Ag[j] = v;
+                    }
+#pragma unroll
+                    for (int j = 0; j < 13; j++) Ag[12 + j] = (i16 < 12) ? Hx[13 * i16 + j] : 0.0;
+#pragma unroll
+                    for (int j = 0; j < 12; j++) Ag[25 + j] = (i16 == j) ? 1.0 : 0.0;
+                }
+                double dk = 1.0;
+#pragma unroll
+                for (int kk = 0; kk < 12; kk++) {
+                    const double piv = readlane_d(Ag[kk], kk);
+                    fail |= !(piv > 0.0);
+                    const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
+#pragma unroll
+                    for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, SRB12_PIVROW(Ag[j], kk), Ag[j]);
+#pragma unroll
+                    for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, SRB12_PIVROW(Ag[25 + j], kk), Ag[25 + j]);
+                    dk = (i16 == kk) ? piv : dk;
+                }
+                const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
+                if (lane < 12) {
+#pragma unroll
+                    for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
+#pragma unroll
+                    for (int j = 0; j < 12; j++)
+                        if (j <= lane) L.Lm[78 * k + (lane * (lane + 1)) / 2 + j] = Ag[25 + j] * sc_;
+                }
+                SYNC();
+                d4 acc2 = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+                for (int kk = 0; kk < 4; kk++) {
+                    const int kc = 4 * kk + q;
+                    const double y = (kc < 12 && i16 < 13) ? L.Mt[13 * kc + i16] : 0.0;
+                    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, acc2, 0, 0, 0);
+                }
+#pragma unroll
+                for (int r = 0; r < 4; r++) {
+                    const int row = q + 4 * r;
+                    if (row < 13 && i16 < 13) Vn[13 * row + i16] -= acc2[r];
+                }
+            }
+            SYNC();
+        }
+        if (fail) return false;
+        // the free initial slack closes the recursion: V_0[12][12] + Sw + delta > 0 is the last
+        // pivot of the inertia test
+        schur = L.V0[168] + prm.Sw + delta;
+        return schur > 0.0;
+    };
+    // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
+    // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
+    // Vectors live in registers, component i = lane & 15 (each 16-lane row holds a copy), and move
+    // between lanes by DPP row broadcasts: no LDS round trip or barrier inside the recursion.
+    auto riccati_solve = [&](int c, bool acc) {
+        const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l, tri = (ir * (ir + 1)) / 2;
+        const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
+        double *dX = L.dX, *dU = L.dU, *gus = L.gus;      // acc: the refinement's correction adds in
+        double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
+        for (int k = N - 1; k >= 0; k--) {
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hx = L.Hx + 156 * k;
+            double vb[13];
+#pragma unroll
+            for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
+            double gu = 0.0;
+            if (i < 12) {
+                gu = rU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
+                for (int a = 0; a < 3; a++) gu = fma(W[9 * l + 3 * a + jj], vb[9 + a], gu);
+            }
+            if (lane < 12) gus[12 * k + i] = gu;
+            double w = 0.0, kk = 0.0;                        // kk = -Z'(Z gu)
+#pragma unroll
+            for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(gu, j), w);
+            if (i >= 12) w = 0.0;
+#pragma unroll
+            for (int j = 0; j < 12; j++) kk = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), kk);
+            if (i >= 12) kk = 0.0;
+            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+            double vn = v;                                     // A~' v
+            if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], vn);
+            else if (i >= 9 && i < 12)
+                vn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], vn);
+            if (k > 0 && i < 13) vn += rX[13 * (k - 1) + i];
+            if (i < 13)
+#pragma unroll
+                for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], bc16(kk, j), vn);
+            v = (i < 13) ? vn : 0.0;
+        }
+        const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
+        double prev = (i == 12) ? ds0 : 0.0;
+        for (int k = 0; k < N; k++) {
+            // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hr = L.Hx + 156 * k + 13 * ir;
+            double pb[13];
+#pragma unroll
+            for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
+            double t = gus[12 * k + ir];
+#pragma unroll
+            for (int j = 0; j < 13; j++) t = fma(Hr[j], pb[j], t);
+            if (i >= 12) t = 0.0;
+            double w = 0.0, du = 0.0;                        // du = -Z'(Z t)
+#pragma unroll
+            for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(t, j), w);
+            if (i >= 12) w = 0.0;
+#pragma unroll
+            for (int j = 0; j < 12; j++) du = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), du);
+            if (i >= 12) du = 0.0;
+            if (lane < 12) dU[12 * k + i] = acc ? dU[12 * k + i] + du : du;
+            double db[12];
+#pragma unroll
+            for (int j = 0; j < 12; j++) db[j] = bc16(du, j);
+            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+            double dx = prev;
+            if (i < 3) dx = fma(Ts, i == 0 ? pb[6] : i == 1 ? pb[7] : pb[8], dx);
+            else if (i < 6)
+                dx = fma(Ts, i == 3 ? fma(cc, pb[9], sn * pb[10]) : i == 4 ? fma(-sn, pb[9], cc * pb[10]) : pb[11], dx);
+            else if (i < 9) {
+                for (int ll = 0; ll < 4; ll++) dx = fma(ct[ll] * tsm, i == 6 ? db[3 * ll] : i == 7 ? db[3 * ll + 1] : db[3 * ll + 2], dx);
+            } else if (i < 12) {
+                const int a = i - 9;
+                for (int ll = 0; ll < 4; ll++)
+                    for (int j = 0; j < 3; j++) dx = fma(W[9 * ll + 3 * a + j], db[3 * ll + j], dx);
+            }
+            if (i > 12) dx = 0.0;
+            if (lane < 13) dX[13 * k + i] = acc ? dX[13 * k + i] + dx : dx;
+            prev = dx;
+        }
+        SYNC();
+    };
+    // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
+    // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
+    // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s).
+    // Explicit Gauss-Jordan inverses lose digits once z / s reaches 1e7 on active rows.
+    auto refine = [&](double delta) {
+        const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
+        const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
+        double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N;
+        auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
+            double v = 0.0;
+            for (int j = 0; j < 13; j++) {
+                const bool nz = (j == i) || ((i < 2 || i == 12) && (j < 2 || j == 12));
+                if (nz) v = fma(qhat(k, i, j, delta), dx[j], v);
+            }
+            return v;
+        };
+        for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
+        double m = (i < 13) ? qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i] : 0.0;
+        for (int k = N - 1; k >= 0; k--) {
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+            double vb[13];
+#pragma unroll
+            for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
+            if (lane < 12) {
+                const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+                double t = fma(prm.r[a3] + delta, du[a3], rU[12 * k + i]);
+                for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
+                t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
+                for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
+                tU[12 * k + i] = t;
+            }
+            if (k > 0) {
+                const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                double mn = m;
+                if (i >= 6 && i < 9) mn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], mn);
+                else if (i >= 9 && i < 12)
+                    mn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], mn);
+                m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] : 0.0;
+            }
+        }
+        const double m12 = bc16(m, 12);
+        if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + m12;
+        SYNC();
+        riccati_solve(1, true);
+    };
+    // right-hand side of pass (0 predictor, 1 corrector) into column 0:
+    // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
+    auto build_rhs = [&](int pass, double smu) {
+        for (int e = tid; e < 12 * N; e += 64) {
+            const int k = e / 12, i = e - 12 * k;
+            const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+            L.rX[13 * k + i] = w * (X[e] - L.xr[e]);
+            L.rU[e] = prm.r[i % 3] * U[e];
+        }
+        for (int k = tid; k < N; k += 64) L.rX[13 * k + 12] = 0.0;
+        if (tid == 0) L.sc[2] = prm.Sw * L.Z[24 * N];
+        SYNC();
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            const int id = lane + 64 * t;
+            double g, h, c0, c1, c2; int kind;
+            row_g(id, g, h, c0, c1, c2, kind);
+            if (!kind) continue;
+            const double rp = g + ss[t] - h, om = zz[t] / ss[t];
+            const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
+            const double w = zz[t] + r3 / ss[t] + om * rp;
+            if (kind == 1) {
+                const int k = id / 24, l = (id / 6) & 3;
+                double *ru = L.rU + 12 * k + 3 * l;
+                const double cc[3] = {c0, c1, c2};
+                for (int a = 0; a < 3; a++)
+                    if (cc[a] != 0.0) __hip_atomic_fetch_add(&ru[a], w * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            } else {
+                double *rx = L.rX + 13 * ((id - nf) / K);
+                __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            }
+        }
+        SYNC();
+    };
+    // the rows' steps of the solved column: J dz, ds = -r_p - J dz, dz = (r3 - z ds) / s; step maxima
+    auto row_step = [&](int pass, double smu, double (&dsl)[TS], double (&dzl)[TS]) {
+        double ms = 0.0, mz = 0.0;
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            const int id = lane + 64 * t;
+            double g, h, c0, c1, c2; int kind;
+            row_g(id, g, h, c0, c1, c2, kind);
+            dsl[t] = dzl[t] = 0.0;
+            if (!kind) continue;
+            double jd;
+            if (kind == 1) {
+                const int k = id / 24, l = (id / 6) & 3;
+                const double *du = L.dU + 12 * k + 3 * l;
+                jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
+            } else {
+                const double *dx = L.dX + 13 * ((id - nf) / K);
+                jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+            }
+            const double rp = g + ss[t] - h;
+            const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
+            dsl[t] = -rp - jd; dzl[t] = (r3 - zz[t] * dsl[t]) / ss[t];
+            ms = fmax(ms, -dsl[t] / ss[t]); mz = fmax(mz, -dzl[t] / zz[t]);
+        }
+        double rv[2] = {ms, mz};
+        wred<2, 3u>(rv);
+        return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
+    };
     S12ST(0);   // inputs, model, rollout
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
-        const int nrow = nl ? nf + NK : nf;
+        nrow = nl ? nf + NK : nf;
         // active row count m and the starting slacks / duals (oracle ipm(): QP s = h - g, z = 1 /
         // max(s, 1); NLP shifted so min s = 1 when a row is violated, z = z0 / max(s, 1))
-        auto row_g = [&](int id, double &g, double &h, double &c0, double &c1, double &c2, int &kind) {
-            g = 0.0; h = 0.0; c0 = c1 = c2 = 0.0; kind = 0;
-            if (id < nf) {
-                const int k = id / 24, l = (id / 6) & 3, q = id % 6;
-                if (L.ct[4 * k + l] != 0.0) {
-                    kind = 1;
-                    fric_coef(q, mus, c0, c1, c2);
-                    const double *u = U + 12 * k + 3 * l;
-                    g = c0 * u[0] + c1 * u[1] + c2 * u[2];
-                    h = (q == 5) ? prm.fmax : 0.0;
-                }
-            } else if (id < nrow) {
-                const int e = id - nf, k = e / K, j = e - k * K;
-                kind = 2;
-                const double dx = X[12 * k] - L.obs[2 * e], dy = X[12 * k + 1] - L.obs[2 * e + 1];
-                c0 = -2.0 * dx; c1 = -2.0 * dy;
-                g = -(dx * dx + dy * dy) - L.Z[24 * N];
-                h = -L.eps[j];
-            }
-        };
         double mcount = 0.0, mn = 1e300;
 #pragma unroll
         for (int t = 0; t < TS; t++) {
@@ -279,6 +600,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         }
         const double inv_m = 1.0 / fmax(mcount, 1.0);
         const int maxit = nl ? prm.nlp_maxit : prm.qp_maxit;
+        // the last stage's complementarity test is tol_final (the forces' accuracy: DESIGN.md 11)
+        const double mtol = (stage == nstage - 1) ? prm.tol_final : tol;
         int flag = 2, it = 0;
         double sigma = 0.0;
 #pragma clang loop unroll(disable)
@@ -296,7 +619,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             if (tid == 0) { L.sc[0] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }    // grad_s f, H_ss (inertia scale)
             SYNC();
             // ---- rows: residuals, weights, scatter of J'z and J'WJ into the per-grid blocks
-            double nrp = 0.0, sz = 0.0;
+            double nrp = 0.0, sz = 0.0, zmx = 0.0;
 #pragma unroll
             for (int t = 0; t < TS; t++) {
                 const int id = lane + 64 * t;
@@ -306,6 +629,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double rp = g + ss[t] - h, om = zz[t] / ss[t];
                 nrp = fma(rp, rp, nrp);
                 sz = fma(ss[t], zz[t], sz);
+                zmx = fmax(zmx, zz[t]);
                 if (kind == 1) {
                     const int k = id / 24, l = (id / 6) & 3;
                     double *gu = L.gU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
@@ -370,16 +694,18 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 if (tid == 0) { const double rs = L.sc[0] + l12; nrd = fma(rs, rs, nrd); }
             }
             {
-                double rv[4] = {nrd, nrp, sz, gm};
-                wred<4, 8u>(rv);
-                nrd = sqrt(rv[0]); nrp = sqrt(rv[1]); sz = rv[2]; gm = rv[3];
+                double rv[5] = {nrd, nrp, sz, gm, zmx};
+                wred<5, 24u>(rv);
+                nrd = sqrt(rv[0]); nrp = sqrt(rv[1]); sz = rv[2]; gm = rv[3]; zmx = rv[4];
             }
             const double mu = sz * inv_m;
             double *dbgrow = (agent == prm.dbg_agent && prm.dbg && it < 64) ? prm.dbg + 8 * (64 * stage + it) : nullptr;
             if (dbgrow && tid == 0) { dbgrow[0] = nrd; dbgrow[1] = th * gm; dbgrow[2] = nrp; dbgrow[3] = mu; }
-            if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz)) { flag = 3; break; }
+            // divergence (the LIP mode's rule, SRB_Z_DIV; oracle/srb12.c the same): a dual beyond 1e10 means
+            // infeasible rows -- FATAL at this finite iterate
+            if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz) || !(zmx <= SRB_Z_DIV)) { flag = 3; break; }
             S12ST(1);   // residuals, weights, scatter, costates
-            if (nrd < th * gm && nrp < th && mu < tol) { flag = 0; break; }
+            if (nrd < th * gm && nrp < th && mu < mtol) { flag = 0; break; }
 
             // ---- factorisation (backward Riccati over the 13-state) with the inertia shift delta (NLP)
             double dmax = 1.0;
@@ -393,328 +719,14 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             dmax = wmax(dmax);
             dmax = fmax(dmax, L.sc[1]);
             const double dstart = 1e-10 * dmax;
-            // Q^_k (state block k, 13 x 13): diag(q) + delta on the 12 states, the obstacle rows' (p_x, p_y, s)
-            // block; the slack's own weight Sw + delta enters once, at s_0
-            auto qhat = [&](int k, int i, int j, double delta) {
-                double v = (i == j && i < 12) ? ((k == N - 1) ? prm.qN[i] : prm.q[i]) + delta : 0.0;
-                const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
-                if (pi && pj) {
-                    const double *q3 = L.Q3 + 6 * k;
-                    const int a = (i == 12) ? 2 : i, b = (j == 12) ? 2 : j;
-                    const int lo = a < b ? a : b, hi = a < b ? b : a;
-                    v += (lo == 0) ? (hi == 0 ? q3[0] : hi == 1 ? q3[1] : q3[3]) : (lo == 1) ? (hi == 1 ? q3[2] : q3[4]) : q3[5];
-                }
-                return v;
-            };
-            double delta = 0.0, schur = 0.0;
+            double delta = 0.0;
             int ok = 0;
             for (int tries = 0; tries < (nl ? 14 : 1); tries++) {
                 if (tries > 0) delta = (delta == 0.0) ? dstart : delta * 10.0;
-                int fail = 0;
-                for (int e = tid; e < 169; e += 64) L.V0[e] = qhat(N - 1, e / 13, e % 13, delta);
-                SYNC();
-                for (int k = N - 1; k >= 0; k--) {
-                    const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = L.V0;
-                    // G = V A~_k (13 x 13), F = V B~_k (13 x 12)
-                    for (int e = tid; e < 169; e += 64) {
-                        const int i = e / 13, j = e - 13 * i;
-                        const double *Vi = V + 13 * i;
-                        double g = Vi[j];
-                        if (j >= 6 && j < 9) g = fma(Ts, Vi[j - 6], g);
-                        else if (j >= 9 && j < 12) g = fma(Ts, Vi[3] * rzab(j - 9, 0, c, s) + Vi[4] * rzab(j - 9, 1, c, s) + Vi[5] * rzab(j - 9, 2, c, s), g);
-                        L.Gt[e] = g;
-                    }
-                    for (int e = tid; e < 156; e += 64) {
-                        const int i = e / 12, j = e - 12 * i, l = j / 3, jj = j - 3 * l;
-                        const double *Vi = V + 13 * i;
-                        double f = ct[l] * tsm * Vi[6 + jj];
-                        for (int a = 0; a < 3; a++) f = fma(Vi[9 + a], W[9 * l + 3 * a + jj], f);
-                        L.Ft[e] = f;
-                    }
-                    SYNC();
-                    // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
-                    // V_0[12][12] is used (the initial slack's Schur complement)
-                    double *Hx = L.Hx + 156 * k, *Vn = L.V0;
-                    for (int e = tid; e < 156; e += 64) {
-                        const int i = e / 13, j = e - 13 * i;
-                        const int li = i / 3, ai = i - 3 * li;
-                        double hx = ct[li] * tsm * L.Gt[13 * (6 + ai) + j];
-                        for (int a = 0; a < 3; a++) hx = fma(W[9 * li + 3 * a + ai], L.Gt[13 * (9 + a) + j], hx);
-                        Hx[e] = hx;
-                    }
-                    for (int e = tid; e < 169; e += 64) {
-                        const int i = e / 13, j = e - 13 * i;
-                        double w = L.Gt[e];
-                        if (i >= 6 && i < 9) w = fma(Ts, L.Gt[13 * (i - 6) + j], w);
-                        else if (i >= 9 && i < 12)
-                            w = fma(Ts, rzab(i - 9, 0, c, s) * L.Gt[39 + j] + rzab(i - 9, 1, c, s) * L.Gt[52 + j] +
-                                            rzab(i - 9, 2, c, s) * L.Gt[65 + j], w);
-                        if (k > 0) w += qhat(k - 1, i, j, delta);
-                        Vn[e] = w;
-                    }
-                    SYNC();
-                    // Hu = R^ + B'F = L D L' by a forward elimination of [Hu | Hux | I] in registers (row i16
-                    // per lane, replicated in every 16-lane row): its pivots are the inertia test, Z = D^-1/2 L^-1
-                    // (stored: the solves apply Hu^-1 = Z'Z) and Y = Z Hux, so the Schur update
-                    // S = Hux' Hu^-1 Hux = Y'Y is one 16x16x16 product on the matrix cores.  The product with
-                    // an explicit inverse, Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on
-                    // active rows; Y'Y is positive semi-definite by construction.
-                    {
-                        const int i16 = lane & 15, q = lane >> 4;
-                        double Ag[37];
-                        {
-                            const int li = (i16 < 12) ? i16 / 3 : 0, ai = (i16 < 12) ? i16 - 3 * li : 0;
-#pragma unroll
-                            for (int j = 0; j < 12; j++) {
-                                double v = 0.0;
-                                if (i16 < 12) {
-                                    v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
-                                    for (int aa = 0; aa < 3; aa++) v = fma(W[9 * li + 3 * aa + ai], L.Ft[12 * (9 + aa) + j], v);
-                                    if (j == i16) v += prm.r[ai] + delta;
-                                    if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
-                                }
-                                Ag[j] = v;
-                            }
-#pragma unroll
-                            for (int j = 0; j < 13; j++) Ag[12 + j] = (i16 < 12) ? Hx[13 * i16 + j] : 0.0;
-#pragma unroll
-                            for (int j = 0; j < 12; j++) Ag[25 + j] = (i16 == j) ? 1.0 : 0.0;
-                        }
-                        double dk = 1.0;
-#pragma unroll
-                        for (int kk = 0; kk < 12; kk++) {
-                            const double piv = readlane_d(Ag[kk], kk);
-                            fail |= !(piv > 0.0);
-                            const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
-#pragma unroll
-                            for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, SRB12_PIVROW(Ag[j], kk), Ag[j]);
-#pragma unroll
-                            for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, SRB12_PIVROW(Ag[25 + j], kk), Ag[25 + j]);
-                            dk = (i16 == kk) ? piv : dk;
-                        }
-                        const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
-                        if (lane < 12) {
-#pragma unroll
-                            for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
-#pragma unroll
-                            for (int j = 0; j < 12; j++)
-                                if (j <= lane) L.Lm[78 * k + (lane * (lane + 1)) / 2 + j] = Ag[25 + j] * sc_;
-                        }
-                        SYNC();
-                        d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                        for (int kk = 0; kk < 4; kk++) {
-                            const int kc = 4 * kk + q;
-                            const double y = (kc < 12 && i16 < 13) ? L.Mt[13 * kc + i16] : 0.0;
-                            acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, acc2, 0, 0, 0);
-                        }
-#pragma unroll
-                        for (int r = 0; r < 4; r++) {
-                            const int row = q + 4 * r;
-                            if (row < 13 && i16 < 13) Vn[13 * row + i16] -= acc2[r];
-                        }
-                    }
-                    SYNC();
-                }
-                if (fail) continue;
-                // the free initial slack closes the recursion: V_0[12][12] + Sw + delta > 0 is the last
-                // pivot of the inertia test
-                schur = L.V0[168] + prm.Sw + delta;
-                if (!(schur > 0.0)) continue;
-                ok = 1;
-                break;
+                if (factor(delta)) { ok = 1; break; }
             }
             S12ST(2);   // Riccati factor (all tries)
             if (!ok) { flag = 1; break; }
-            // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
-            // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
-            // Vectors live in registers, component i = lane & 15 (each 16-lane row holds a copy), and move
-            // between lanes by DPP row broadcasts: no LDS round trip or barrier inside the recursion.
-            auto riccati_solve = [&](int c, bool acc) {
-                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l, tri = (ir * (ir + 1)) / 2;
-                const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
-                double *dX = L.dX, *dU = L.dU, *gus = L.gus;      // acc: the refinement's correction adds in
-                double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
-                for (int k = N - 1; k >= 0; k--) {
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hx = L.Hx + 156 * k;
-                    double vb[13];
-#pragma unroll
-                    for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
-                    double gu = 0.0;
-                    if (i < 12) {
-                        gu = rU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
-                        for (int a = 0; a < 3; a++) gu = fma(W[9 * l + 3 * a + jj], vb[9 + a], gu);
-                    }
-                    if (lane < 12) gus[12 * k + i] = gu;
-                    double w = 0.0, kk = 0.0;                        // kk = -Z'(Z gu)
-#pragma unroll
-                    for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(gu, j), w);
-                    if (i >= 12) w = 0.0;
-#pragma unroll
-                    for (int j = 0; j < 12; j++) kk = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), kk);
-                    if (i >= 12) kk = 0.0;
-                    const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                    double vn = v;                                     // A~' v
-                    if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], vn);
-                    else if (i >= 9 && i < 12)
-                        vn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], vn);
-                    if (k > 0 && i < 13) vn += rX[13 * (k - 1) + i];
-                    if (i < 13)
-#pragma unroll
-                        for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], bc16(kk, j), vn);
-                    v = (i < 13) ? vn : 0.0;
-                }
-                const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
-                double prev = (i == 12) ? ds0 : 0.0;
-                for (int k = 0; k < N; k++) {
-                    // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hr = L.Hx + 156 * k + 13 * ir;
-                    double pb[13];
-#pragma unroll
-                    for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
-                    double t = gus[12 * k + ir];
-#pragma unroll
-                    for (int j = 0; j < 13; j++) t = fma(Hr[j], pb[j], t);
-                    if (i >= 12) t = 0.0;
-                    double w = 0.0, du = 0.0;                        // du = -Z'(Z t)
-#pragma unroll
-                    for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(t, j), w);
-                    if (i >= 12) w = 0.0;
-#pragma unroll
-                    for (int j = 0; j < 12; j++) du = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), du);
-                    if (i >= 12) du = 0.0;
-                    if (lane < 12) dU[12 * k + i] = acc ? dU[12 * k + i] + du : du;
-                    double db[12];
-#pragma unroll
-                    for (int j = 0; j < 12; j++) db[j] = bc16(du, j);
-                    const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                    double dx = prev;
-                    if (i < 3) dx = fma(Ts, i == 0 ? pb[6] : i == 1 ? pb[7] : pb[8], dx);
-                    else if (i < 6)
-                        dx = fma(Ts, i == 3 ? fma(cc, pb[9], sn * pb[10]) : i == 4 ? fma(-sn, pb[9], cc * pb[10]) : pb[11], dx);
-                    else if (i < 9) {
-                        for (int ll = 0; ll < 4; ll++) dx = fma(ct[ll] * tsm, i == 6 ? db[3 * ll] : i == 7 ? db[3 * ll + 1] : db[3 * ll + 2], dx);
-                    } else if (i < 12) {
-                        const int a = i - 9;
-                        for (int ll = 0; ll < 4; ll++)
-                            for (int j = 0; j < 3; j++) dx = fma(W[9 * ll + 3 * a + j], db[3 * ll + j], dx);
-                    }
-                    if (i > 12) dx = 0.0;
-                    if (lane < 13) dX[13 * k + i] = acc ? dX[13 * k + i] + dx : dx;
-                    prev = dx;
-                }
-                SYNC();
-            };
-            // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
-            // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
-            // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s).
-            // Explicit Gauss-Jordan inverses lose digits once z / s reaches 1e7 on active rows.
-            auto refine = [&](double delta) {
-                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
-                const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
-                double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N;
-                auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
-                    double v = 0.0;
-                    for (int j = 0; j < 13; j++) {
-                        const bool nz = (j == i) || ((i < 2 || i == 12) && (j < 2 || j == 12));
-                        if (nz) v = fma(qhat(k, i, j, delta), dx[j], v);
-                    }
-                    return v;
-                };
-                for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
-                double m = (i < 13) ? qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i] : 0.0;
-                for (int k = N - 1; k >= 0; k--) {
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
-                    double vb[13];
-#pragma unroll
-                    for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
-                    if (lane < 12) {
-                        const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                        double t = fma(prm.r[a3] + delta, du[a3], rU[12 * k + i]);
-                        for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
-                        t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
-                        for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
-                        tU[12 * k + i] = t;
-                    }
-                    if (k > 0) {
-                        const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                        double mn = m;
-                        if (i >= 6 && i < 9) mn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], mn);
-                        else if (i >= 9 && i < 12)
-                            mn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], mn);
-                        m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] : 0.0;
-                    }
-                }
-                const double m12 = bc16(m, 12);
-                if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + m12;
-                SYNC();
-                riccati_solve(1, true);
-            };
-            // right-hand side of pass (0 predictor, 1 corrector) into column 0:
-            // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
-            auto build_rhs = [&](int pass, double smu) {
-                for (int e = tid; e < 12 * N; e += 64) {
-                    const int k = e / 12, i = e - 12 * k;
-                    const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
-                    L.rX[13 * k + i] = w * (X[e] - L.xr[e]);
-                    L.rU[e] = prm.r[i % 3] * U[e];
-                }
-                for (int k = tid; k < N; k += 64) L.rX[13 * k + 12] = 0.0;
-                if (tid == 0) L.sc[2] = prm.Sw * L.Z[24 * N];
-                SYNC();
-#pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    const int id = lane + 64 * t;
-                    double g, h, c0, c1, c2; int kind;
-                    row_g(id, g, h, c0, c1, c2, kind);
-                    if (!kind) continue;
-                    const double rp = g + ss[t] - h, om = zz[t] / ss[t];
-                    const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
-                    const double w = zz[t] + r3 / ss[t] + om * rp;
-                    if (kind == 1) {
-                        const int k = id / 24, l = (id / 6) & 3;
-                        double *ru = L.rU + 12 * k + 3 * l;
-                        const double cc[3] = {c0, c1, c2};
-                        for (int a = 0; a < 3; a++)
-                            if (cc[a] != 0.0) __hip_atomic_fetch_add(&ru[a], w * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        double *rx = L.rX + 13 * ((id - nf) / K);
-                        __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                }
-                SYNC();
-            };
-            // the rows' steps of the solved column: J dz, ds = -r_p - J dz, dz = (r3 - z ds) / s; step maxima
-            auto row_step = [&](int pass, double smu, double (&dsl)[TS], double (&dzl)[TS]) {
-                double ms = 0.0, mz = 0.0;
-#pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    const int id = lane + 64 * t;
-                    double g, h, c0, c1, c2; int kind;
-                    row_g(id, g, h, c0, c1, c2, kind);
-                    dsl[t] = dzl[t] = 0.0;
-                    if (!kind) continue;
-                    double jd;
-                    if (kind == 1) {
-                        const int k = id / 24, l = (id / 6) & 3;
-                        const double *du = L.dU + 12 * k + 3 * l;
-                        jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
-                    } else {
-                        const double *dx = L.dX + 13 * ((id - nf) / K);
-                        jd = c0 * dx[0] + c1 * dx[1] - dx[12];
-                    }
-                    const double rp = g + ss[t] - h;
-                    const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
-                    dsl[t] = -rp - jd; dzl[t] = (r3 - zz[t] * dsl[t]) / ss[t];
-                    ms = fmax(ms, -dsl[t] / ss[t]); mz = fmax(mz, -dzl[t] / zz[t]);
-                }
-                double rv[2] = {ms, mz};
-                wred<2, 3u>(rv);
-                return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
-            };
             S12ST(3);   // between factor and predictor
             // ---- predictor
             // (the refinement only near the optimum, mu < 1e-3: far from it the step's accuracy is not
@@ -767,10 +779,180 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             qp_flag = flag; qp_it = it;
             if (x_qp_out)
                 for (int v = tid; v < nv; v += 64) x_qp_out[(size_t)agent * nv + v] = L.Z[v];
-            if (flag == 3) break;
+            // a FATAL QP stage ends the solve: the NLP stage does not run and reports FATAL too (a
+            // consumer reading the NLP status alone must not see OPTIMAL; oracle/srb12.c, same rule)
+            if (flag == 3) { if (prm.use_nlp) nlp_flag = 3; break; }
         } else {
             nlp_flag = flag; nlp_it = it;
         }
+    }
+    // ---- active-set polish of the last stage's OPTIMAL result (oracle/srb12.c polish12, the same steps):
+    // rows with s KAPPA < z form the active set A; Newton steps on the augmented Lagrangian
+    //   (H_L + RHO J_A'J_A) d = -(grad f + J_A'(z_A + RHO c_A)),  z_A += RHO (c_A + J_A d)
+    // through the same Riccati factor / solve (the weights RHO on the active rows, 0 on the others,
+    // -2 y on (p_x, p_y) of active obstacle rows, y = z_A + RHO c_A), one factor per pass and at most IT
+    // steps (fewer once |d| <= DXTOL); accepted when every row holds to PTOL, the active rows to PTOL,
+    // z_A >= -1e-9 max |z_A| and the last step <= DXTOL; else the most negative multiplier leaves, the
+    // violated rows join and a second pass starts from the interior-point result.  Rejected: that result
+    // stands (it met tol_final).  Why: along the legs' internal-force directions only r = 1e-2 pins the
+    // forces, so an interior-point iterate at s'z/m ~ 1e-9 is still up to 1e-3 N off; the active set's
+    // KKT point is exact.
+    const int fin_flag = prm.use_nlp ? nlp_flag : qp_flag;
+    if (prm.polish && fin_flag == 0) {
+        S12ST(8);
+        bool pact[TS];
+        double za[TS], cr[TS];
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            double g, h, c0, c1, c2; int kind;
+            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
+            pact[t] = kind && ss[t] * SRB12_POL_KAPPA < zz[t];
+            za[t] = pact[t] ? zz[t] : 0.0;
+        }
+        for (int v = tid; v < nv; v += 64) L.xsv[v] = L.Z[v];
+        bool accepted = false;
+#pragma clang loop unroll(disable)
+        for (int pass = 0; pass < SRB12_POL_PASSES; pass++) {
+            if (pass > 0) {
+                SYNC();
+                for (int v = tid; v < nv; v += 64) L.Z[v] = L.xsv[v];
+            }
+            double lastdx = 1e300;
+            bool bad = false;
+#pragma clang loop unroll(disable)
+            for (int pit = 0; pit < SRB12_POL_IT; pit++) {
+                // gradient (column 1 of the right-hand side) and, for the pass's factor, the Hessian blocks
+                SYNC();
+                for (int e = tid; e < 12 * N; e += 64) {
+                    const int k = e / 12, i = e - 12 * k;
+                    const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+                    L.gX[13 * k + i] = w * (X[e] - L.xr[e]);
+                    L.gU[e] = prm.r[i % 3] * U[e];
+                }
+                for (int k = tid; k < N; k += 64) L.gX[13 * k + 12] = 0.0;
+                if (pit == 0) {
+                    for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
+                    for (int e = tid; e < 24 * N; e += 64) L.Rh[e] = 0.0;
+                }
+                if (tid == 0) { L.sc[3] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }
+                SYNC();
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    const int id = lane + 64 * t;
+                    double g, h, c0, c1, c2; int kind;
+                    row_g(id, g, h, c0, c1, c2, kind);
+                    cr[t] = g - h;
+                    if (!pact[t]) continue;
+                    const double y = fma(SRB12_POL_RHO, cr[t], za[t]), om = SRB12_POL_RHO;
+                    if (kind == 1) {
+                        const int k = id / 24, l = (id / 6) & 3;
+                        double *gu = L.gU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+                        const double cc[3] = {c0, c1, c2};
+                        for (int a = 0; a < 3; a++)
+                            if (cc[a] != 0.0) __hip_atomic_fetch_add(&gu[a], y * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (pit == 0)
+                            for (int a = 0; a < 3; a++)
+                                for (int b = a; b < 3; b++)
+                                    if (cc[a] != 0.0 && cc[b] != 0.0)
+                                        __hip_atomic_fetch_add(&rh[sym3(a, b)], om * cc[a] * cc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    } else {
+                        const int k = (id - nf) / K;
+                        double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
+                        __hip_atomic_fetch_add(&gx[0], y * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&gx[1], y * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&gx[12], -y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        if (pit == 0) {
+                            __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                            __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        }
+                    }
+                }
+                SYNC();
+                if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
+                riccati_solve(1, false);                                    // d = -H^-1 grad (column 1)
+                // multipliers z_A += RHO (c_A + J_A d) at the linearisation point; then x += d
+                double mdx = 0.0;
+#pragma unroll
+                for (int t = 0; t < TS; t++) {
+                    const int id = lane + 64 * t;
+                    double g, h, c0, c1, c2; int kind;
+                    row_g(id, g, h, c0, c1, c2, kind);
+                    if (!pact[t]) continue;
+                    double jd;
+                    if (kind == 1) {
+                        const int k = id / 24, l = (id / 6) & 3;
+                        const double *du = L.dU + 12 * k + 3 * l;
+                        jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
+                    } else {
+                        const double *dx = L.dX + 13 * ((id - nf) / K);
+                        jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+                    }
+                    za[t] = fma(SRB12_POL_RHO, cr[t] + jd, za[t]);
+                }
+                const double dsv = L.dX[12];
+                SYNC();
+                for (int e = tid; e < 12 * N; e += 64) {
+                    const int k = e / 12, i = e - 12 * k;
+                    const double dxe = L.dX[13 * k + i], due = L.dU[e];
+                    X[e] += dxe; U[e] += due;
+                    mdx = fmax(mdx, fmax(fabs(dxe), fabs(due)));
+                }
+                if (tid == 0) { L.Z[24 * N] += dsv; mdx = fmax(mdx, fabs(dsv)); }
+                lastdx = wmax(mdx);
+                if (lastdx <= SRB12_POL_DXTOL) break;
+            }
+            if (bad) break;
+            SYNC();
+            // acceptance at the polished point
+            double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0;
+#pragma unroll
+            for (int t = 0; t < TS; t++) {
+                double g, h, c0, c1, c2; int kind;
+                row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
+                cr[t] = g - h;
+                if (!kind) continue;
+                pv = fmax(pv, cr[t]);
+                if (pact[t]) { cv = fmax(cv, fabs(cr[t])); nzmin = fmax(nzmin, -za[t]); zm = fmax(zm, fabs(za[t])); }
+            }
+            {
+                double rv[4] = {pv, cv, nzmin, zm};
+                wred<4, 15u>(rv);
+                pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3];
+            }
+            if (pv <= SRB12_POL_PTOL && cv <= SRB12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB12_POL_DXTOL) {
+                accepted = true;
+                break;
+            }
+            // next pass: the most negative multiplier leaves (lowest row on ties, the oracle's row order),
+            // violated rows join (multiplier 0), the others keep max(z_A, 0)
+            double wd = -1e-9 * zm;
+            int wk = 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < TS; t++)
+                if (pact[t] && za[t] < wd) lexmin(wd, wk, za[t], lane + 64 * t);
+            if (wk == 0x7fffffff) wd = 1e300;
+            wargmin(wd, wk);
+            bool changed = wk != 0x7fffffff;
+#pragma unroll
+            for (int t = 0; t < TS; t++) {
+                const int id = lane + 64 * t;
+                double g, h, c0, c1, c2; int kind;
+                row_g(id, g, h, c0, c1, c2, kind);
+                if (id == wk) pact[t] = false;
+                else if (kind && !pact[t] && cr[t] > SRB12_POL_PTOL) { pact[t] = true; changed = true; }
+                za[t] = pact[t] ? fmax(za[t], 0.0) : 0.0;
+            }
+            if (!__builtin_amdgcn_ballot_w64(changed)) break;
+        }
+        SYNC();
+        if (!accepted)
+            for (int v = tid; v < nv; v += 64) L.Z[v] = L.xsv[v];
+        SYNC();
+        S12ST(9);
     }
     // ---- outputs: x and 0.5 x'Px + c'x
     double f = 0.0;

@@ -56,12 +56,11 @@ static size_t g_lds_max = 160 * 1024;   // gfx950 LDS per CU; the device's share
 // SIMDs of a CU (NW = 4) for latency; larger batches run one wave per agent so that agents,
 // not waves of one agent, fill the SIMDs -- except large problems (more than five row slots per
 // lane with one wave, e.g. N = 20), where one wave spills its registers and two waves per agent
-// are 1.8x faster (profiles/r01_nw_tuning.txt).  SRB_NMPC_NW = 1 | 2 | 4 overrides (tuning).
+// are 1.8x faster (profiles/r01_nw_tuning.txt).  srb_ctx_set_waves overrides.  (No environment
+// variable changes what the product library computes: every knob is a context setting.)
 static int wanted_waves(int n_agents, int slots, int ctx_nw)
 {
-    static const int forced = [] { const char *e = std::getenv("SRB_NMPC_NW"); return e ? std::atoi(e) : 0; }();
     if (ctx_nw == 1 || ctx_nw == 2 || ctx_nw == 4) return ctx_nw;
-    if (forced == 1 || forced == 2 || forced == 4) return forced;
     if (g_cu_count > 0 && n_agents <= g_cu_count) return 4;
     return (slots > 5 * 64) ? 2 : 1;
 }
@@ -114,6 +113,10 @@ struct srb_ctx {
     int last_nw;
     int nw;                        // waves per agent forced by srb_ctx_set_waves (0: automatic)
     int qp_init;                   // QP starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT
+    // srb_ctx_set_option (SRB_OPT_*): the polish of the NLP result on/off, its penalty and waves per
+    // agent, the selection-grid thresholds
+    int polish, polish_waves, grid_min_rows, grid_min_rows_static;
+    double polish_rho;
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
     float polish_ms;
@@ -285,31 +288,44 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     }
     rc = validate(p);                     // again against this device's LDS per workgroup
     if (rc) return rc;
-    srb_ctx *c = new srb_ctx();
+    srb_ctx *c = new srb_ctx();           // value-initialised: every buffer null until allocated
+    // a failure after this point unwinds through srb_ctx_destroy; *out stays untouched
+#define CREATE_CHK(expr)                                                                               \
+    do {                                                                                               \
+        hipError_t e_ = (expr);                                                                        \
+        if (e_ != hipSuccess) {                                                                        \
+            const int rc_ = fail(SRB_ERR_HIP, std::string(#expr ": ") + hipGetErrorString(e_));          \
+            srb_ctx_destroy(c);                                                                        \
+            return rc_;                                                                                \
+        }                                                                                              \
+    } while (0)
     c->p = *p; c->max_agents = max_agents; c->device = device;
     c->cap_obs = 0; c->cap_nbr = 0; c->obstacles = nullptr; c->nbr = nullptr; c->timed = false; c->nw = 0; c->last_nw = 0;
     for (auto &g : c->grid) g = srb_ctx::grid_buf{nullptr, nullptr, nullptr, nullptr, 0};
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0;
+    c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
     const size_t A = (size_t)max_agents;
-    HIPCHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
-    for (int i = 0; i < 4; i++) HIPCHK(hipEventCreate(&c->ev[i]));
-    HIPCHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
-    HIPCHK(hipMalloc(&c->x0, A * 4 * sizeof(double)));
-    HIPCHK(hipMalloc(&c->ref, A * 4 * N * sizeof(double)));
-    HIPCHK(hipMalloc(&c->foot, A * 2 * C * N * sizeof(double)));
-    HIPCHK(hipMalloc(&c->x_qp, A * nv * sizeof(double)));
-    HIPCHK(hipMalloc(&c->x, A * nv * sizeof(double)));
-    HIPCHK(hipMalloc(&c->obj, A * sizeof(double)));
-    HIPCHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
-    HIPCHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
-    HIPCHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
-    HIPCHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
-    HIPCHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
-    HIPCHK(hipMalloc(&c->zpol, A * (size_t)c->zstride * sizeof(float)));
+    CREATE_CHK(hipStreamCreateWithFlags(&c->stream, hipStreamNonBlocking));
+    for (int i = 0; i < 4; i++) CREATE_CHK(hipEventCreate(&c->ev[i]));
+    CREATE_CHK(hipEventCreateWithFlags(&c->done, hipEventDisableTiming));
+    CREATE_CHK(hipMalloc(&c->x0, A * 4 * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->ref, A * 4 * N * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->foot, A * 2 * C * N * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->x_qp, A * nv * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->x, A * nv * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->obj, A * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->abuf, A * 4 * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->alpha, A * 20 * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->sel, A * 2 * SRB_KNN_MAX * sizeof(int)));
+    CREATE_CHK(hipMalloc(&c->zpol, A * (size_t)c->zstride * sizeof(float)));
+#undef CREATE_CHK
     *out = c;
     return SRB_OK;
 }
@@ -318,7 +334,7 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
 {
     if (!c) return SRB_OK;
     (void)hipSetDevice(c->device);
-    (void)hipStreamSynchronize(c->stream);
+    if (c->stream) (void)hipStreamSynchronize(c->stream);
     if (c->any) (void)hipEventSynchronize(c->done);     // the last launch may be on another stream
     void *bufs[] = {c->x0, c->ref, c->foot, c->x_qp, c->x, c->obj, c->status, c->iters, c->obstacles, c->nbr,
                     c->abuf, c->alpha, c->sel, c->zpol};
@@ -327,9 +343,10 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
     for (auto &g : c->grid)
         for (void *b : {g.g, (void *)g.off, (void *)g.spos, (void *)g.sidx})
             if (b) (void)hipFree(b);
-    for (int i = 0; i < 4; i++) (void)hipEventDestroy(c->ev[i]);
-    (void)hipEventDestroy(c->done);
-    (void)hipStreamDestroy(c->stream);
+    for (int i = 0; i < 4; i++)
+        if (c->ev[i]) (void)hipEventDestroy(c->ev[i]);
+    if (c->done) (void)hipEventDestroy(c->done);
+    if (c->stream) (void)hipStreamDestroy(c->stream);
     delete c;
     return SRB_OK;
 }
@@ -344,10 +361,8 @@ static int launch_select(srb_ctx *c, int n_agents, const double *x0, const doubl
     // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
     // with the arena) get a uniform grid so each agent scans only the cells around it
     // (a versioned static obstacle table builds its grid once, so it pays off at fewer rows;
-    // SRB_GRID_MIN_ROWS overrides both thresholds)
-    static const char *env_rows = std::getenv("SRB_GRID_MIN_ROWS");
-    static const int min_rows = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS;
-    static const int min_rows_static = env_rows ? std::atoi(env_rows) : SRB_GRID_MIN_ROWS_STATIC;
+    // SRB_OPT_GRID_MIN_ROWS / _STATIC set the thresholds)
+    const int min_rows = c->grid_min_rows, min_rows_static = c->grid_min_rows_static;
     const bool go = K_obs > 0 && n_obs >= (obstacles_version != 0 ? min_rows_static : min_rows);
     const bool gn = K_nbr > 0 && n_all >= min_rows;
     if (go) { int rc = grid_reserve(c, 0, n_obs); if (rc) return rc; }
@@ -379,6 +394,8 @@ int srb_internal_select(srb_ctx *c, int n_agents, const double *x0, const double
                          obstacles_version, sel, s);
 }
 
+int srb_internal_mark_done(srb_ctx *c, hipStream_t s) { return mark_done(c, s); }
+
 static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, int use_nlp)
 {
     if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
@@ -395,8 +412,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
         return fail(SRB_ERR_ARG, "agent_offset out of range of the neighbour table");
     SrbKParams k = make_kparams(p, use_nlp);
     k.qp_init = c->qp_init;
-    static const double rho_env = [] { const char *e = std::getenv("SRB_POLISH_RHO"); return e ? std::atof(e) : 0.0; }();
-    k.polish_rho = rho_env > 0.0 ? rho_env : SRB_POLISH_RHO;
+    k.polish_rho = c->polish_rho;
     // "up to K nearest": clamp to what exists (batch-uniform), so no row is ever a dummy
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
@@ -419,7 +435,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     HIPCHK(hipEventRecord(c->ev[2], s));
     // the solve kernel, then (NLP stage) the active-set polish of its result (srb_polish_kernel,
     // same instance geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
-    const bool polish = use_nlp && SRB_POLISH_ON;
+    const bool polish = use_nlp && c->polish;
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
@@ -431,9 +447,8 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
         // index), so it runs at its own waves per agent: at least two (its registers fit two
         // waves per SIMD, and a polish step's latency halves): configs[2] polish 0.067 -> 0.053 ms,
         // configs[1] (solve at 4 waves) and N = 20 (2 waves) unchanged, one wave slower everywhere
-        // (profiles/r03_polish_nw_ab.txt).  SRB_POLISH_NW = 1 | 2 | 4 overrides (tuning).
-        static const int pnw_env = [] { const char *e = std::getenv("SRB_POLISH_NW"); return e ? std::atoi(e) : 0; }();
-        const int pnw = (pnw_env == 1 || pnw_env == 2 || pnw_env == 4) ? pnw_env : (in->nw < 2 ? 2 : in->nw);
+        // (profiles/r03_polish_nw_ab.txt).  SRB_OPT_POLISH_WAVES = 1 | 2 | 4 overrides.
+        const int pnw = c->polish_waves ? c->polish_waves : (in->nw < 2 ? 2 : in->nw);
         const srb_instance *pin = pnw == in->nw ? in : pick_instance(k, pnw);
         if (!pin || pin->nzl != in->nzl) pin = in;
         const size_t plds = (size_t)srb_lds_doubles(k, pin->nzl, pin->nw) * sizeof(double);
@@ -455,6 +470,43 @@ extern "C" int srb_ctx_set_waves(srb_ctx *c, int nw)
 }
 
 extern "C" int srb_ctx_waves(srb_ctx *c) { return c ? c->last_nw : 0; }
+
+extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
+{
+    if (!c) return fail(SRB_ERR_ARG, "null ctx");
+    const bool whole = v == (double)(long long)v;
+    switch (opt) {
+    case SRB_OPT_POLISH:
+        if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH: 0 or 1");
+        c->polish = (int)v; return SRB_OK;
+    case SRB_OPT_POLISH_RHO:
+        if (!(v >= 1e3 && v <= 1e12)) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH_RHO: 1e3 .. 1e12");
+        c->polish_rho = v; return SRB_OK;
+    case SRB_OPT_POLISH_WAVES:
+        if (v != 0.0 && v != 1.0 && v != 2.0 && v != 4.0) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH_WAVES: 0 (automatic), 1, 2 or 4");
+        c->polish_waves = (int)v; return SRB_OK;
+    case SRB_OPT_GRID_MIN_ROWS:
+    case SRB_OPT_GRID_MIN_ROWS_STATIC:
+        if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
+        (opt == SRB_OPT_GRID_MIN_ROWS ? c->grid_min_rows : c->grid_min_rows_static) = (int)v;
+        return SRB_OK;
+    default:
+        return fail(SRB_ERR_ARG, "unknown option");
+    }
+}
+
+extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
+{
+    if (!c || !v) return fail(SRB_ERR_ARG, "null argument");
+    switch (opt) {
+    case SRB_OPT_POLISH: *v = c->polish; return SRB_OK;
+    case SRB_OPT_POLISH_RHO: *v = c->polish_rho; return SRB_OK;
+    case SRB_OPT_POLISH_WAVES: *v = c->polish_waves; return SRB_OK;
+    case SRB_OPT_GRID_MIN_ROWS: *v = c->grid_min_rows; return SRB_OK;
+    case SRB_OPT_GRID_MIN_ROWS_STATIC: *v = c->grid_min_rows_static; return SRB_OK;
+    default: return fail(SRB_ERR_ARG, "unknown option");
+    }
+}
 
 extern "C" int srb_ctx_set_qp_init(srb_ctx *c, int mode)
 {
@@ -513,7 +565,7 @@ extern "C" __global__ void srb_hlplan_step_kernel(int NA, int i, int loop, const
                                                   double *Prd);
 
 // swarms up to this many agents run as one persistent workgroup (srb_hlplan_kernel); larger ones
-// one launch per step over NA / 64 workgroups (srb_hlplan_step_kernel); SRB_HL_STEP=1 forces the latter
+// one launch per step over NA / 64 workgroups (srb_hlplan_step_kernel)
 #define SRB_HL_ONE_WG 1024
 
 extern "C" int srb_hl_plan(int device, int NA, const double *Pstart, const double *Pobs, int n_obs, int loop, double *Pr,
@@ -541,8 +593,7 @@ extern "C" int srb_hl_plan(int device, int NA, const double *Pstart, const doubl
         chk(hipMemcpy(dPs, Pstart, 2 * NA * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
         if (n_obs > 0) chk(hipMemcpy(dOb, Pobs, n_obs * 2 * sizeof(double), hipMemcpyHostToDevice), "hipMemcpy");
     }
-    static const bool force_step = [] { const char *e = std::getenv("SRB_HL_STEP"); return e && std::atoi(e) == 1; }();
-    if (rc == SRB_OK && NA <= SRB_HL_ONE_WG && !force_step) {
+    if (rc == SRB_OK && NA <= SRB_HL_ONE_WG) {
         const int threads = ((NA + 63) / 64) * 64;
         const size_t lds = (4 * (size_t)NA + 2 * (size_t)n_obs) * sizeof(double);
         hipLaunchKernelGGL(srb_hlplan_kernel, dim3(1), dim3(threads), lds, 0, NA, dPs, dOb, n_obs, loop, dPr, dPrd);

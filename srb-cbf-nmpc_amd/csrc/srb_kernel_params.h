@@ -56,6 +56,9 @@
 // pass as converged without the verifying step (oracle ORC_POLISH_DX1 / ORC_POLISH_CTOL)
 #define SRB_POLISH_DX1 1e-4
 #define SRB_POLISH_CTOL 1e-10
+// divergence: a dual beyond this ends a stage FATAL at its finite iterate (infeasible rows; converging
+// solves keep their duals below ~1e4 on every workload; oracle ORC_Z_DIV)
+#define SRB_Z_DIV 1e10
 // cross-wave reduction scratch: sites of up to 8 doubles per wave (srb_kernels.hip)
 #define SRB_RED_SITES 10
 
@@ -119,7 +122,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 3 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
+    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
            (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part
 #ifdef SRB_STAMPS
            + 64
@@ -154,14 +157,21 @@ struct SrbLLKParams {
 // declared but never implemented by the reference, include/fast_MPC.hpp:98-103)
 struct Srb12KParams {
     int N, K_obs, K_nbr, use_nlp;
-    int qp_maxit, nlp_maxit;
-    double Ts, mass, grav, mus, fmax, Sw, eps_obs, eps_nbr, tol, z0;
+    int qp_maxit, nlp_maxit, polish;
+    double Ts, mass, grav, mus, fmax, Sw, eps_obs, eps_nbr, tol, z0, tol_final;
     double Ib[9];                     // body inertia (fast_MPC.cpp:41-43)
     double q[12], qN[12], r[3];       // stage / terminal state weights, force weights
     int dbg_agent;                    // >= 0: that agent records a per-iteration trace into dbg
     double *dbg;                      // [2 stages][64 iterations][8] (srb12_debug_trace)
 };
 #define SRB12_MAX_N 24
+// active-set polish of the last stage's result (oracle/srb12.c ORC12_POL_*, the same constants)
+#define SRB12_POL_RHO 1e9
+#define SRB12_POL_KAPPA 1e4
+#define SRB12_POL_IT 3
+#define SRB12_POL_PASSES 2
+#define SRB12_POL_PTOL 1e-9
+#define SRB12_POL_DXTOL 1e-7
 // row slots: 6 friction rows per (grid, leg) -- masked for swing legs -- then N K obstacle rows
 static inline int srb12_slots(int N, int K) { return 24 * N + N * K; }
 // doubles of LDS one agent needs (the carve in srb12_kernels.hip)
@@ -173,5 +183,6 @@ static inline int srb12_lds_doubles(int N, int K)
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
            + 2 * 13 * N + 2 * 12 * N + 13 * N + 12 * N + 12 * N   // rhs columns (solve, refinement / gradients), solution, gu
            + 16 + 16                                    // vector, scalars
-           + 2 * N * K + 2 * K + 2;                     // obstacle positions, eps, sel (as ints)
+           + 2 * N * K + K + (24 * N + 1)               // obstacle positions, eps, the saved iterate (polish)
+           + K + 2;                                     // sel (as ints)
 }

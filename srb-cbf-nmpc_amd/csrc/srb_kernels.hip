@@ -657,6 +657,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     double *xs = p; p += n4; \
     double *xb = p; p += n4; \
     double *xsv = p; p += n4;                     /* NLP: saved iterate (round-off floor / polish) */ \
+    double *xprev = p; p += n4;                   /* the iterate before the last update (non-finite fallback) */ \
     double *ref = p; p += 4 * N; \
     double *foot = p; p += 2 * C * N; \
     double *obs = p; p += 2 * NK + 2; \
@@ -1003,6 +1004,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         double dxl = 1e300;              // this lane's max |ap dx| over its variable slots, last update
         int npassed = 0;                 // NLP: near-optimal iterates so far
         bool saved = false, restore = false;   // NLP: xsv holds the best near-optimal iterate
+        bool prov = false;                     // NLP: OPTIMAL by the loosened tests only (-> 4 until polished)
         double best_rx = 1e300;                // its dual residual / max(1, ||Q x + f||_inf)
         // the polish kernel (srb_polish_kernel, launched next) starts from the NLP result: its active
         // set and multipliers -- rows with s * KAPPA < z keep z (as float: the Newton iteration's
@@ -1020,11 +1022,12 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0f
                             : (float)(Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? Q[t].z[r] : -fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP));
         };
+        for (int v = tid; v < n; v += NTH) xprev[v] = xs[v];
         for (int iter = 0; iter < maxit; iter++) {
             STAMP_BEGIN();
             // ---- residuals (computeresiduals, Auxilary.c:524-553), norms, reciprocals
             const double s_var = xs[n - 1];
-            double nrx = 0.0, nrz = 0.0, sz = 0.0, gm = 1.0;
+            double nrx = 0.0, nrz = 0.0, sz = 0.0, gm = 1.0, zmx = 0.0;
             double fv[TS];
 #pragma unroll
             for (int t = 0; t < TS; t++) {
@@ -1040,6 +1043,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     const double rz0 = q.h[0] - q.s[0] - f, rz1 = q.h[1] - q.s[1] + f;
                     nrz = fma(q.m[0] * rz0, rz0, fma(q.m[1] * rz1, rz1, nrz));
                     sz = fma(q.m[0] * q.s[0], q.z[0], fma(q.m[1] * q.s[1], q.z[1], sz));
+                    zmx = fmax(zmx, fmax(q.m[0] * q.z[0], q.m[1] * q.z[1]));
 #pragma unroll
                     for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
                     if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z (gram_rhs)
@@ -1052,19 +1056,37 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             STAMP_END(18);                                    // stamps build: residual loop | reduction
             double dxm;
             {
-                double rv[5] = {nrx, nrz, sz, gm, dxl};
-                wred_x<5, 24u, NW>(rv, red + 2 * 8 * NW, tid);
-                nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3]; dxm = rv[4];
+                double rv[6] = {nrx, nrz, sz, gm, dxl, zmx};
+                wred_x<6, 56u, NW>(rv, red + 2 * 8 * NW, tid);
+                nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3]; dxm = rv[4]; zmx = rv[5];
             }
             const double mu = sz * inv_m;
             STAMP_END(3);
-            if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) { flag = 3; break; }
+            // divergence: a dual beyond SRB_Z_DIV means infeasible rows (converging solves keep their duals
+            // below ~1e4; infeasible ones pass 1e10 within a few iterations and then overflow): FATAL at
+            // this finite iterate (oracle/qp_ipm.c, nlp_ipm.c: the same rule).  A non-finite iterate
+            // (nothing else should produce one) returns the previous iterate, so no FATAL solve hands the
+            // caller NaN or inf
+            if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz) || !(zmx <= SRB_Z_DIV)) {
+                flag = 3;
+                if (!isfinite(nrx) || !isfinite(nrz) || !isfinite(sz)) {
+                    SYNC();
+                    for (int v = tid; v < n; v += NTH) xs[v] = xprev[v];
+                    SYNC();
+                }
+                break;
+            }
             // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
             const double thx = nl ? SRB_NLP_EXITF * th * gm : th;
             const double mtol = nl ? SRB_NLP_EXITF * tol : tol;
             NLPDBG(iter, 0, nrx); NLPDBG(iter, 1, thx); NLPDBG(iter, 2, nrz); NLPDBG(iter, 3, sz * inv_m);
             const bool pass = nrx < thx && nrz < th && sz * inv_m < mtol;
-            if (pass && (!nl || dxm < SRB_NLP_DXTOL)) { flag = 0; break; }
+            if (pass && (!nl || dxm < SRB_NLP_DXTOL)) {
+                // NLP: met only by the loosened tests (SRB_NLP_EXITF, which rely on the polish), the result
+                // is provisional -- ACCEPTABLE (4) unless the polish kernel accepts its polish (oracle, same rule)
+                prov = nl && !(nrx < th * gm && sz * inv_m < tol);
+                flag = 0; break;
+            }
             // NLP near the optimum (primal and complementarity met, dual residual within 100x):
             // an inertia shift or a blocked step from here is round-off of the condensed
             // system (W = z/s ~ 1e14 swamps the soft curvature in Z'HZ), not progress -> exit
@@ -1269,6 +1291,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             dxl = fmax(dxl, fabs(ap * q.jd));
                             q.rx = (1.0 - ad) * q.rx + ((ad - ap) * q.a0) * q.jd;
                             if (nl) q.rx = fma(ad * (delta - 2.0 * hso[t]), q.jd, q.rx);
+                            xprev[q.i0] = fv[t];                 // the iterate a non-finite step falls back to
                             xs[q.i0] = fma(ap, q.jd, fv[t]);
                         }
                     }
@@ -1291,7 +1314,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             if (acc) { flag = 4; break; }
             it++;
         }
-        if (nl && saved && (restore || flag == 2 || flag == 4)) {      // ACCEPTABLE / MAXIT: the best saved iterate
+        if (flag == 0 && prov) flag = 4;
+        if (nl && saved && !prov && (restore || flag == 2 || flag == 4)) {      // ACCEPTABLE / MAXIT: the best saved iterate
             for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];     // owner threads, as saved
             flag = 4;                                               // (zpol_g: exported at the save)
         } else if (zpol_g && nl) {

@@ -26,7 +26,9 @@ _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 
 OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
-ABI_VERSION = 3                                               # SRB_ABI_VERSION of include/srbnmpc.h
+# srb_ctx_set_option codes (SRB_OPT_* of include/srbnmpc.h)
+OPTIONS = {"polish": 1, "polish_rho": 2, "polish_waves": 3, "grid_min_rows": 4, "grid_min_rows_static": 5}
+ABI_VERSION = 4                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 
 class Params(ctypes.Structure):
@@ -90,6 +92,8 @@ def lib():
         L.srb_ctx_set_waves.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.srb_ctx_waves.argtypes = [ctypes.c_void_p]
         L.srb_ctx_set_qp_init.argtypes = [ctypes.c_void_p, ctypes.c_int]
+        L.srb_ctx_set_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.c_double]
+        L.srb_ctx_get_option.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
         L.srb_last_polish_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float)]
         L.srb_hl_plan.argtypes = [ctypes.c_int, ctypes.c_int, _dp, _dp, ctypes.c_int, ctypes.c_int, _dp, _dp]
         L.srb_prepare_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Prep), ctypes.c_void_p]
@@ -258,6 +262,16 @@ class BatchSolver:
     def set_waves(self, nw: int = 0):
         """Waves per agent (0 automatic, 1, 2, 4; srb_ctx_set_waves)."""
         _check(lib().srb_ctx_set_waves(self._h, int(nw)))
+
+    def set_option(self, name: str, value: float):
+        """Context option (srb_ctx_set_option): name one of OPTIONS ("polish", "polish_rho",
+        "polish_waves", "grid_min_rows", "grid_min_rows_static")."""
+        _check(lib().srb_ctx_set_option(self._h, OPTIONS[name], float(value)))
+
+    def get_option(self, name: str) -> float:
+        v = ctypes.c_double()
+        _check(lib().srb_ctx_get_option(self._h, OPTIONS[name], ctypes.byref(v)))
+        return v.value
 
     def set_qp_init(self, mode: int = 1):
         """QP-stage starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT's kkt_initialize."""

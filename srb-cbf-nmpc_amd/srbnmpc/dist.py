@@ -28,10 +28,12 @@ class NeighbourExchange:
     shards (n_total % world == 0) the receive buffer IS the table; otherwise the padding is
     squeezed out by one index_select into a preallocated table."""
 
-    def __init__(self, n_total: int, world: int, rank: int, device, dtype=None):
+    def __init__(self, n_total: int, world: int, rank: int, device, dtype=None, force_collective: bool = False):
+        """force_collective: run the all-gather even with one rank (tests: the RCCL path on one GPU)."""
         import torch as _t
         dtype = dtype or _t.float64
         self.n_total, self.world, self.rank = n_total, world, rank
+        self.force = bool(force_collective)
         self.counts = [shard_range(n_total, world, r)[1] - shard_range(n_total, world, r)[0] for r in range(world)]
         self.cmax = max(self.counts)
         self.send = _t.zeros((self.cmax, 4), dtype=dtype, device=device)
@@ -45,8 +47,10 @@ class NeighbourExchange:
         self.flat = dist.is_initialized() and dist.get_backend() != "gloo"
 
     def __call__(self, local_state: torch.Tensor) -> torch.Tensor:
-        if self.world == 1:
+        if self.world == 1 and not self.force:
             return local_state
+        if local_state.shape[0] != self.counts[self.rank]:
+            raise ValueError(f"rank {self.rank} holds {self.counts[self.rank]} agents, got {local_state.shape[0]} rows")
         self.send[:local_state.shape[0]].copy_(local_state)
         if self.flat:
             dist.all_gather_into_tensor(self.recv, self.send)

@@ -11,6 +11,13 @@ reads the same:
 
 run_NMPC keeps the reference's host-side planners (copPlanner_eventbase, footholdsPlanner)
 and sends the solve (with the fused Bezier fit) to the GPU as a batch of one.
+
+Horizon: the reference hard-codes N = NDOMAIN = 4 grids (MPC_dist.cpp:92, :104).  MPCDist(horizon=N)
+generalises it as SURVEY.md 5 asks (BASELINE configs[0]: horizon 10): the window still starts at
+column NDOMAIN * gaitDomain_ (a gait domain is NDOMAIN grids) and spans N columns, every grid gets
+the domain's footholds, get_MPCsol() is 4N x 1, and the Bezier fit keeps using X_0..X_3 (the
+domain); horizon=NDOMAIN (default) is the reference exactly.
+
 generateReferenceTrajectory (the offline HL planner, MPC_dist.cpp:930-1104) runs on the
 GPU through srb_hl_plan; callers that already hold its output use setReferenceTrajectory.
 """
@@ -28,9 +35,12 @@ INIT_FOOTPRINT = np.array([[0.2188, -0.1320],   # FR   (MPC_dist.cpp:1206-1209)
 class MPCDist:
     _solvers = {}
 
-    def __init__(self, device: int = 0):
+    def __init__(self, device: int = 0, horizon: int = NDOMAIN):
+        if horizon < NDOMAIN:
+            raise ValueError(f"horizon {horizon} < NDOMAIN = {NDOMAIN} (the Bezier fit reads X_0..X_3)")
         self.use_snopt = False            # MPC_dist.hpp:139: False -> QP only
         self.device = device
+        self.N = int(horizon)
         self.agent_id_ = 0
         self.gaitDomain_ = 0
         self.domain_ = 0
@@ -48,7 +58,7 @@ class MPCDist:
         self.toePos_ = np.zeros((3, 4))
         self.state_other = np.zeros(4)
         self.alpha_COM_traj_e_ = np.zeros((4, 5))
-        self.mpc_state_e_x_eventbased_ = np.zeros(4 * NDOMAIN)
+        self.mpc_state_e_x_eventbased_ = np.zeros(4 * self.N)
         self.qp_solution_eventbased_ = None
         self.last_status = None
         self.last_iters = None
@@ -90,10 +100,14 @@ class MPCDist:
         self.state_other = np.asarray(state_other, dtype=np.float64).ravel()[:4].copy()
 
     # ------------------------------------------------------------------ planners (host)
-    def copPlanner_eventbase(self, N: int = NDOMAIN):
-        """MPC_dist.cpp:702-782: 4 x N window of the HL path, flattened column-major."""
+    def copPlanner_eventbase(self, N: int | None = None):
+        """MPC_dist.cpp:702-782: 4 x N window of the HL path from column NDOMAIN * gaitDomain_,
+        flattened column-major (N = the horizon)."""
+        N = self.N if N is None else N
         a = self.agent_id_
-        c0 = N * self.gaitDomain_
+        c0 = NDOMAIN * self.gaitDomain_
+        if c0 + N > self.Pr_refined_.shape[1]:
+            raise RuntimeError("MPC_dist: reference trajectory exhausted")
         qref = np.zeros((4, N))
         qref[0] = self.Pr_refined_[2 * a, c0:c0 + N]
         qref[1] = self.Prd_refined_[2 * a, c0:c0 + N]
@@ -122,15 +136,15 @@ class MPCDist:
     # ------------------------------------------------------------------ solve
     def _solver(self, C: int, use_nlp: bool):
         from . import BatchSolver, default_params
-        key = (self.device, C, use_nlp)
+        key = (self.device, self.N, C, use_nlp)
         if key not in MPCDist._solvers:
-            p = default_params(NDOMAIN, C, K_obs=1, K_nbr=0, use_nlp=int(use_nlp))
+            p = default_params(self.N, C, K_obs=1, K_nbr=0, use_nlp=int(use_nlp))
             MPCDist._solvers[key] = BatchSolver(p, 1, self.device)
         return MPCDist._solvers[key]
 
     def run_NMPC(self):
         """MPC_dist.cpp:81-454 with the QP/NLP solve on the GPU."""
-        N = NDOMAIN
+        N = self.N
         ref = self.copPlanner_eventbase(N)
         F = self.footholdsPlanner()
         C = F.shape[1]
@@ -147,7 +161,7 @@ class MPCDist:
         self.last_iters = out["iters"][0]
         X = self.mpc_state_e_x_eventbased_.reshape(N, 4)
         self.alpha_COM_traj_e_ = out["alpha"][0]
-        self.mpc_state_alpha_buffer_ = X[3].copy()              # buffer update (:798)
+        self.mpc_state_alpha_buffer_ = X[NDOMAIN - 1].copy()    # buffer update (:798): the domain's end
         self.gaitDomain_ += 1
         return x
 

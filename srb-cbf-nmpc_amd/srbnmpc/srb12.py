@@ -20,7 +20,8 @@ _p12_fields = [("N", ctypes.c_int), ("K_obs", ctypes.c_int), ("K_nbr", ctypes.c_
                ("q", ctypes.c_double * 12), ("qN", ctypes.c_double * 12), ("r", ctypes.c_double * 3),
                ("Sw", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
                ("tol", ctypes.c_double), ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int),
-               ("use_nlp", ctypes.c_int), ("z0", ctypes.c_double)]
+               ("use_nlp", ctypes.c_int), ("z0", ctypes.c_double),
+               ("tol_final", ctypes.c_double), ("polish", ctypes.c_int)]
 
 
 class Params12(ctypes.Structure):
@@ -133,8 +134,16 @@ class Solver12:
         def iptr(t):
             return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _ip)
         A = x0.shape[0]
+        import torch
+        Ko, Kn = n_selected(self.params, 0 if obstacles is None else obstacles.shape[0],
+                            0 if nbr_state is None else nbr_state.shape[0])
+        sel = out.get("sel")
+        # the kernel writes rows of stride Ko + Kn (clamped to the tables, 0 without the NLP stage):
+        # anything else would be overrun or read misaligned (BatchSolver.solve_device, same check)
+        if sel is not None and (sel.dtype != torch.int32 or tuple(sel.shape) != (A, Ko + Kn) or not sel.is_contiguous()):
+            raise ValueError(f"out['sel'] must be a contiguous int32 tensor of shape ({A}, {Ko + Kn}) "
+                             f"(n_selected(params, n_obs, n_all)), got {tuple(sel.shape)} {sel.dtype}")
         if stream is None:
-            import torch
             stream = torch.cuda.current_stream(self.device).cuda_stream
         b = Batch12(dptr(x0), dptr(xref), dptr(foot), iptr(contact), dptr(obstacles), dptr(nbr_state),
                     0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],

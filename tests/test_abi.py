@@ -176,3 +176,27 @@ def test_abi_version_and_struct_size_checks():
         assert f(*args(b)) == -1 and b"null argument" in lib.srb_last_error()   # passes the layout check
     # the mirrors match the C layout: struct_size first, then the pointers 8-byte aligned
     assert srbnmpc.Batch.x0.offset == 8 and srbnmpc.Prep.Pr.offset == 8 and lowlevel.LLIO.ind.offset == 8
+
+
+def test_no_environment_variable_changes_the_numerics():
+    """every numeric knob is a context setting (srb_ctx_set_waves,
+    srb_ctx_set_option: polish on/off, its rho and waves, the selection-grid thresholds); the
+    product library reads no environment variable at all, so a stray variable on a robot cannot
+    change a solution.  Checked on the built library's dynamic symbols and strings."""
+    path = srbnmpc.LIB_PATH
+    if os.path.basename(path) != "libsrbnmpc.so":
+        pytest.skip("a diagnostic build is selected (SRBNMPC_LIB)")
+    blob = open(path, "rb").read()
+    for name in (b"SRB_POLISH_RHO", b"SRB_NMPC_NW", b"SRB_POLISH_NW", b"SRB_GRID_MIN_ROWS", b"SRB_HL_STEP"):
+        assert name not in blob, name
+    import subprocess
+    syms = subprocess.run(["nm", "-D", "--undefined-only", path], capture_output=True, text=True, check=True).stdout
+    assert not re.search(r"\b(secure_)?getenv\b", syms), [l for l in syms.splitlines() if "getenv" in l]
+    # the option entry points validate without a context or GPU
+    lib = srbnmpc.lib()
+    assert lib.srb_ctx_set_option(None, srbnmpc.OPTIONS["polish"], 0.0) == -1
+    v = ctypes.c_double()
+    assert lib.srb_ctx_get_option(None, srbnmpc.OPTIONS["polish_rho"], ctypes.byref(v)) == -1
+    hdr = open(os.path.join(ROOT, "include", "srbnmpc.h")).read()
+    for k, code in srbnmpc.OPTIONS.items():
+        assert re.search(rf"#define SRB_OPT_{k.upper()} {code}\b", hdr), k

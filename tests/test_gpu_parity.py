@@ -156,23 +156,25 @@ def test_gpu_matches_oracle(N, C, Ko, Kn, A, nlp):
 def test_free_velocity_workload_statuses_and_solutions_vs_oracle():
     """The hard workload (workload.make_batch velocity="free": U[-0.3, 0.3] per axis, uncorrelated
     with the goal and the trot support): a few percent of the instances have infeasible CoM-CoP
-    rows, so both stages also end MAXIT / KKTFAIL.  GPU and oracle must agree on the exit codes
-    (rare round-off flips of a non-converging instance allowed), and wherever both are OPTIMAL the
-    solutions agree as on the easy workload."""
+    rows.  Their duals diverge; both the kernel and the oracle end such a stage FATAL once a dual
+    passes SRB_Z_DIV = 1e10 (converging solves stay below ~1e4), at a finite iterate.  So every
+    output is finite, the status arrays equal the oracle's, and wherever both are OPTIMAL the
+    solutions agree as on the easy workload.  (The reference returns a finite last iterate on a
+    non-optimal exit: iswift_qp.cpp:126-151.)"""
     N, C, Ko, Kn, A = 10, 2, 3, 8, 512
     b = workload.make_batch(A, N, C, seed=5, velocity="free")
-    out = solver(N, C, Ko, Kn, 1).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    s = solver(N, C, Ko, Kn, 1)
+    buf = np.zeros((A, 4)); buf[:, 0] = b["x0"][:, 0]; buf[:, 2] = b["x0"][:, 2]
+    out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], alpha_buf=buf)
     r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"], b["obstacles"],
                            b["nbr_state"], nthreads=8)
     assert np.isin(out["status"], [0, 1, 2, 3, 4]).all()
-    fatal = (out["status"] == 3).any(1)                          # FATAL: the iterate left the finite range
-    assert np.isfinite(out["x"][~fatal]).all()
+    for k in ("x", "x_qp", "obj", "alpha"):                      # every agent, FATAL ones included
+        assert np.isfinite(out[k]).all(), (k, np.where(~np.isfinite(out[k]).reshape(A, -1).all(1))[0])
     nonopt = (r["status"] != 0).any(1)
     assert nonopt.sum() >= 5, nonopt.sum()                       # the workload is hard: some fail in both
-    # converged or not, stage by stage: the same verdict.  The failure CODE of a non-converging
-    # instance differs: measured 28 GPU FATAL (non-finite residuals: the condensed iterate
-    # overflows on the infeasible rows) against 5 FATAL + 23 MAXIT in the oracle's full-space LU
-    # (DESIGN.md section 10)
+    diff = np.where((out["status"] != r["status"]).any(1))[0]
+    assert diff.size == 0, [(int(a), out["status"][a].tolist(), r["status"][a].tolist()) for a in diff]
     ok_g, ok_o = out["status"] == 0, r["status"] == 0
     assert (ok_g[:, 0] == ok_o[:, 0]).mean() >= 0.99
     assert (ok_g.all(1) == ok_o.all(1)).mean() >= 0.98, (ok_g.all(1) != ok_o.all(1)).sum()
@@ -180,6 +182,33 @@ def test_free_velocity_workload_statuses_and_solutions_vs_oracle():
     assert both.mean() >= 0.9
     np.testing.assert_allclose(xus(N, out["x_qp"][both]), xus(N, r["x_qp"][both]), atol=QP_TOL, rtol=0)
     np.testing.assert_allclose(xus(N, out["x"][both]), xus(N, r["x"][both]), atol=NLP_TOL, rtol=0)
+
+
+@pytest.mark.parametrize("N,C", [(4, 4), (4, 2), (10, 2), (10, 4), (20, 2)])
+def test_hip_qp_stage_vs_iswift_min_degree_goldens(N, C):
+    """the HIP QP stage itself on all 64 instances per (N, C) of
+    tests/golden/qp_iswift_md.npz (genuine iSWIFT under a minimum-degree ordering, the stand-in for
+    the reference's Eigen AMD, iswift_qp.cpp:184-210): within 1e-7 of each instance's exact optimum
+    in X, U, s and never worse than iSWIFT-md in the exact l1 merit -- the checks
+    tests/test_oracle.py applies to the oracle, here on the kernel's own output."""
+    import os
+    from kkt import l1_merit, qp_exact_optimum
+    g = np.load(os.path.join(os.path.dirname(__file__), "golden", "qp_iswift_md.npz"), allow_pickle=False)
+    k = f"N{N}_C{C}_"
+    x0, ref, foot = g[k + "x0"], g[k + "ref"], g[k + "foot"]
+    out = solver(N, C, use_nlp=0).solve(x0, ref, foot, qp_only=True)
+    assert (out["status"][:, 0] == 0).all(), out["status"][:, 0]
+    p = oracle.params(N, C)
+    sel = np.r_[0:6 * N, -1]
+    for a in range(x0.shape[0]):
+        Pd, c, A, b, G, h = oracle.build_qp(p, x0[a], ref[a], foot[a])
+        x = out["x_qp"][a]
+        xs, y, z = qp_exact_optimum(Pd, c, A, b, G, h, g[k + "x_orc"][a])
+        fstar = 0.5 * Pd @ (xs * xs) + c @ xs
+        assert np.abs(x[sel] - xs[sel]).max() < 1e-7, (a, np.abs(x[sel] - xs[sel]).max())
+        m_gpu = l1_merit(Pd, c, A, b, G, h, x, y, z)
+        m_md = l1_merit(Pd, c, A, b, G, h, g[k + "x_md"][a], y, z)
+        assert m_gpu <= m_md + 1e-12 * max(1.0, abs(fstar)), (a, m_gpu - fstar, m_md - fstar)
 
 
 # ----------------------------------------------------------------------------- full-size properties
@@ -226,6 +255,40 @@ def test_full_size_properties(A, Kn):
         gJ, hh = nlp_rows(N, C, Pd.size, G, h, obs, eps, p.vsat)
         cert = certify(Pd, c, Aeq, beq, gJ, hh, x[a])
         assert cert["stat_rel"] < 1e-5 and cert["prim"] < 1e-6, (a, cert)
+
+
+def test_unpolished_loosened_exit_is_acceptable_not_optimal():
+    """the NLP stage exits on dual-residual / complementarity tests 10x looser than the
+    QP's (SRB_NLP_EXITF) because the polish makes the result exact.  A result that met only those
+    loosened tests is provisional: with the polish off (SRB_OPT_POLISH = 0) it must read ACCEPTABLE
+    (4), never OPTIMAL, exactly as the oracle (ORC_NO_POLISH) says; with the polish on every such
+    solve is promoted to OPTIMAL at the exact KKT point."""
+    import os
+    N, C, Ko, Kn, A = 10, 2, 3, 8, 256
+    b = workload.make_batch(A, N, C, seed=11)
+    p = srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn)
+    s = srbnmpc.BatchSolver(p, A)
+    try:
+        s.set_option("polish", 0)
+        assert s.get_option("polish") == 0.0
+        off = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+        s.set_option("polish", 1)
+        on = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    finally:
+        s.close()
+    os.environ["ORC_NO_POLISH"] = "1"
+    try:
+        r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"],
+                               b["obstacles"], b["nbr_state"], nthreads=8)
+    finally:
+        del os.environ["ORC_NO_POLISH"]
+    prov = off["status"][:, 1] == 4
+    assert prov.sum() >= A // 10, prov.sum()                    # the loosened exit is the common case
+    assert ((off["status"] == r["status"]).all(1)).mean() >= 0.99
+    assert not ((off["status"][:, 1] == 0) & (r["status"][:, 1] == 4)).any()
+    assert (on["status"] == 0).all()                            # polished: OPTIMAL
+    # the interior-point results themselves are unchanged by the status rule
+    np.testing.assert_allclose(xus(N, off["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
 def test_config5_full_size_vs_oracle_and_acceptable_exit():
@@ -514,6 +577,42 @@ def test_mpcdist_surface_on_reference_instance(kat2):
     np.testing.assert_allclose(alpha, oracle.fit_bezier([0, 0, 0, 0], np.asarray(kat2["x_nlp"])[:16].reshape(4, 4)),
                                atol=1e-6)
     assert m.gaitDomain_ == 1
+
+
+def test_mpcdist_horizon_10_trot_cycles_vs_oracle():
+    """BASELINE configs[0]: one A1 agent, horizon 10, trot, through MPCDist(horizon=10) for three
+    control cycles (the window advances NDOMAIN = 4 columns a cycle, the predicted state seeds the
+    next): statuses, QP point and NLP point against the oracle on the same inputs."""
+    N, C = 10, 2
+    m = srbnmpc.MPCDist(horizon=N)
+    m.setAgentID(0)
+    m.setPstart(np.zeros(2))
+    Pobs = np.array([[0.9, 0.35], [2.0, -1.0], [3.1, 0.6]])
+    m.setPobs_real(Pobs.T)
+    T = 40
+    c = np.arange(T)
+    Pr = np.zeros((2, T)); Prd = np.zeros((2, T))
+    Pr[0] = 0.27 * 0.043 * (c + 1); Prd[0] = 0.27
+    m.setReferenceTrajectory(Pr, Prd)
+    m.use_snopt = True
+    p = oracle.params(N, C, K_obs=1, use_nlp=1)
+    q = np.zeros(18); dq = np.zeros(18)
+    for cyc in range(3):
+        ind = [1, 0, 0, 1] if cyc % 2 == 0 else [0, 1, 1, 0]          # trot: FR + RL, then FL + RR
+        m.updateState(q, dq, ind, m.toePos_, np.zeros(4))
+        ref = m.copPlanner_eventbase()
+        foot = np.repeat(m.footholdsPlanner()[None], N, 0)
+        x0 = np.array([q[0], dq[0], q[1], dq[1]])
+        buf = m.mpc_state_alpha_buffer_.copy()
+        m.run_NMPC()
+        r = oracle.solve_batch(p, x0[None], ref[None], foot[None], Pobs)
+        assert m.last_status.tolist() == r["status"][0].tolist() == [0, 0], (cyc, m.last_status, r["status"])
+        np.testing.assert_allclose(xus(N, m.qp_solution_eventbased_), xus(N, r["x_qp"][0]), atol=QP_TOL, rtol=0)
+        np.testing.assert_allclose(m.get_MPCsol().ravel(), r["x"][0][:4 * N], atol=NLP_TOL, rtol=0)
+        X = m.get_MPCsol().reshape(N, 4)
+        np.testing.assert_allclose(m.get_alphaCOM(), oracle.fit_bezier(buf, X[:4]), atol=1e-9)
+        q[0], dq[0], q[1], dq[1] = X[3]
+    assert m.gaitDomain_ == 3 and m.get_MPCsol().shape == (4 * N, 1)
 
 
 @pytest.mark.parametrize("N,C,Kn", [(4, 4, 0), (10, 2, 8)])

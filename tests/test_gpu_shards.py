@@ -135,9 +135,11 @@ def test_rank_shard_of_8gpu_swarm_vs_oracle(config, rank):
 
 
 def test_rccl_backend_all_gather_round_trip():
-    """The RCCL path of the neighbour exchange on this box's one GPU: a one-rank "nccl" (RCCL)
-    process group, NeighbourExchange's flat mode, and the all_gather_into_tensor call it issues
-    per cycle, in a child process (the group must not outlive the test)."""
+    """The RCCL path of the neighbour exchange on this box's one GPU, in a child process (the group
+    must not outlive the test): a one-rank "nccl" (RCCL) process group and the NeighbourExchange
+    object bench.py calls every step -- its flat all_gather_into_tensor on RCCL over three cycles
+    with the buffers reused, and its unequal-shard path (padded receive buffer + index_select into
+    the table) on GPU tensors, the other ranks' blocks supplied by a stand-in collective."""
     import socket
     import subprocess
     with socket.socket() as sk:
@@ -151,12 +153,35 @@ os.environ.update(MASTER_ADDR="127.0.0.1", MASTER_PORT="{port}")
 dist.init_process_group("nccl", rank=0, world_size=1, device_id=torch.device("cuda", 0))
 assert dist.get_backend() == "nccl"
 x = torch.arange(1024 * 4, dtype=torch.float64, device="cuda").view(1024, 4)
-ex = sd.NeighbourExchange(1024, 1, 0, x.device)
+# the exchange object bench.py calls every step (bench.py main_srb12 / main), its flat RCCL path
+ex = sd.NeighbourExchange(1024, 1, 0, x.device, force_collective=True)
 assert ex.flat
-recv = torch.zeros_like(x)
-dist.all_gather_into_tensor(recv, x)
+for cycle in range(3):                                   # buffers reused across control cycles
+    out = ex(x + cycle)
+    torch.cuda.synchronize()
+    assert torch.equal(out, x + cycle)
+    assert out.data_ptr() == ex.recv.data_ptr()           # equal shards: the receive buffer is the table
+# unequal shards (1000 agents over 3 ranks: 334 / 333 / 333): the padded receive buffer and the
+# index_select into the table, on this GPU; the other two ranks' blocks are supplied by a stand-in for
+# the collective (one process cannot host three RCCL ranks on one device)
+full = torch.randn(1000, 4, dtype=torch.float64, device="cuda")
+ex3 = sd.NeighbourExchange(1000, 3, 1, x.device)
+assert ex3.flat and not ex3.equal and ex3.counts == [334, 333, 333]
+lo, hi = sd.shard_range(1000, 3, 1)
+def fake_all_gather(recv, send):
+    v = recv.view(3, ex3.cmax, 4)
+    v.zero_()
+    for r in range(3):
+        a, b = sd.shard_range(1000, 3, r)
+        v[r, :b - a] = send[:b - a] if r == 1 else full[a:b]
+real = dist.all_gather_into_tensor
+dist.all_gather_into_tensor = fake_all_gather
+try:
+    tab = ex3(full[lo:hi])
+finally:
+    dist.all_gather_into_tensor = real
 torch.cuda.synchronize()
-assert torch.equal(recv, x)
+assert torch.equal(tab, full), (tab - full).abs().max()
 dist.destroy_process_group()
 print("rccl ok")
 """
