@@ -19,15 +19,18 @@ int srb_internal_mark_done(srb_ctx *c, hipStream_t s);
 
 typedef void (*srb12_fn)(Srb12KParams, int, const double *, const double *, const double *, const int *,
                          const double *, const double *, const int *, double *, double *, double *, int *, int *);
-#define DECL12(TS)                                                                                              \
-    extern "C" __global__ void srb12_kernel_##TS(Srb12KParams, int, const double *, const double *,              \
-                                                 const double *, const int *, const double *, const double *,    \
-                                                 const int *, double *, double *, double *, int *, int *);
-DECL12(4) DECL12(6) DECL12(8) DECL12(12)
+#define DECL12(TL, TO)                                                                                          \
+    extern "C" __global__ void srb12_kernel_##TL##_##TO(Srb12KParams, int, const double *, const double *,      \
+                                                        const double *, const int *, const double *,             \
+                                                        const double *, const int *, double *, double *,         \
+                                                        double *, int *, int *);
+SRB12_INSTANCES(DECL12)
 #undef DECL12
 extern "C" __global__ void srb12_pos_kernel(int n_agents, const double *x0g, double *pos);
-struct srb12_inst { int ts; srb12_fn fn; };
-static const srb12_inst g_inst12[] = {{4, srb12_kernel_4}, {6, srb12_kernel_6}, {8, srb12_kernel_8}, {12, srb12_kernel_12}};
+struct srb12_inst { int tl, to; srb12_fn fn; };
+#define ENTRY12(TL, TO) {TL, TO, srb12_kernel_##TL##_##TO},
+static const srb12_inst g_inst12[] = {SRB12_INSTANCES(ENTRY12)};
+#undef ENTRY12
 
 #define H12CHK(expr)                                                                                    \
     do {                                                                                                \
@@ -76,11 +79,12 @@ extern "C" void srb12_params_default(srb12_params *p, int N)
 
 extern "C" int srb12_nv(const srb12_params *p) { return 24 * p->N + 1; }
 
+// the first instance with enough leg-slot and obstacle-slot trips (the list is ordered by cost)
 static const srb12_inst *pick12(const srb12_params *p)
 {
-    const int S = srb12_slots(p->N, p->K_obs + p->K_nbr);
+    const int tl = srb12_leg_trips(p->N), to = srb12_obs_trips(p->N, p->K_obs + p->K_nbr);
     for (const srb12_inst &in : g_inst12)
-        if (64 * in.ts >= S) return &in;
+        if (in.tl >= tl && in.to >= to) return &in;
     return nullptr;
 }
 

@@ -13,22 +13,25 @@
 //         NLP stage the obstacle rows -|p_k - o_kj|^2 - s <= -eps_j (dec_vars_constr_cost.h:262-302).
 //
 // Execution model: one 64-lane wavefront per agent runs both interior-point stages (QP without
-// the obstacle rows, then the NLP warm-started from it), the iteration of oracle/srb12.c step for
-// step.  The Newton system is solved by a Riccati recursion over the horizon instead of the
-// oracle's dense LU -- O(N 12^3) per iteration, the structure the 12-state model has:
-//   * every inequality row is a slot owned by one lane (registers), scattered into per-grid
-//     Hessian blocks (the p_xy 2x2 block and the s border column of the obstacle rows, the 3x3
-//     friction blocks of each leg) by LDS atomics;
-//   * backward pass per grid: G = V A, F = V B (A, B applied through their structure: a few FMAs
-//     per entry), Hu = R^ + B'F = L D L' by a register forward elimination of [Hu | Hux | I] (its
-//     pivots are the reduced Hessian's: the inertia test), Z = D^-1/2 L^-1 kept for the solves
-//     (Hu^-1 = Z'Z), and the Schur update V' = Q^ + A'G - Y'Y, Y = Z Hux, as a 16x16x16 product on
-//     the matrix cores (v_mfma_f64_16x16x4f64), positive semi-definite by construction;
-//   * the obstacle slack s rides along as a 13th state (s_{k+1} = s_k, s_0 free), so the stiff
-//     obstacle rows stay inside one grid's block;
-//   * the dual residual uses the costates of the backward recursion lambda_k = grad_x_k L +
-//     A_k' lambda_{k+1} (the state part of r_d is zero, the input part is the reduced gradient);
-//     the primal-dual step does not depend on them (oracle, same rule).
+// the obstacle rows, then the NLP warm-started from it) and the active-set polish of the last
+// stage -- the iteration of oracle/srb12.c step for step.  The Newton system is solved by a Riccati
+// recursion over the horizon (O(N 13^3) per iteration) instead of the oracle's dense LU.  The
+// obstacle slack s rides along as a 13th state (s_{k+1} = s_k, s_0 free), so the stiff obstacle
+// rows stay inside one grid's block.  Round 4 layout:
+//   * rows: a LEG slot per (grid, leg) holds that leg's six friction rows in the registers of one
+//     lane (its 3 x 3 Hessian block and force gradient are formed in-lane, no atomics); an OBSTACLE
+//     slot per (grid, row) adds its (p_x, p_y, s) block by LDS atomics;
+//   * factor, stage k: the products G = V A~, F = V B~, A~'G, B~'G, B~'F on the matrix cores
+//     (v_mfma_f64_16x16x4f64; V stays in the accumulator layout from stage to stage, whose D
+//     operand is directly the next product's B operand), then Hu = L D L' by a COLUMN-oriented
+//     elimination of [Hu | Hux | I] (lane j holds column j: one readlane of the pivot column's
+//     multipliers per entry, 37 columns over 37 lanes), Y = D^-1/2 L^-1 Hux, Z = D^-1/2 L^-1, and
+//     Y'Y (the Schur update, positive semi-definite by construction), Hu^-1 = Z'Z and the gain
+//     K = -Z'Y as three more MFMA products; per stage K and Hu^-1 go to LDS for the solves;
+//   * solves: vectors in registers, component i = lane & 15 replicated in the four 16-lane rows;
+//     each matrix-vector product is split over the rows (row g takes columns 4g..4g+3, gathered by
+//     ds_bpermute), then summed across rows by two permlane swaps -- 4 LDS reads per lane and
+//     product instead of 13, and a 4-long instead of a 13-long dependent chain.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
 #include "srb_kernel_params.h"
@@ -39,41 +42,30 @@
 namespace {
 
 struct Srb12Lds {
-    double *Wl, *cs, *ct, *Lm, *Hx, *V0, *Gt, *Ft, *Mt, *Q3, *Rh, *Z, *xr, *gX, *gU;
-    double *rX, *rU, *dX, *dU, *gus, *vv, *sc, *obs, *eps, *xsv;
+    double *Wl, *cs, *ct, *Kst, *Hst, *T, *Q3, *Rh, *Z, *xr;
+    double *rX, *rU, *gX, *gU, *dX, *dU, *kff, *vv, *sc, *obs, *eps, *xsv;
     int *sel;
 };
 
-// the carve of srb12_lds_doubles (srb_kernel_params.h), same order.  State vectors carry 13 entries
-// per grid (the 12 states and the slack), input vectors 12; columns 0 (solve) and 1 (its refinement)
+// the carve of srb12_lds_doubles (srb_kernel_params.h), same order.  The right-hand side columns:
+// column 0 (rX | rU: the Newton solves) and column 1 (gX | gU: gradients, the refinement's
+// correction, the polish); the polish keeps the interior-point iterate in column 0's space (xsv)
 __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
 {
     Srb12Lds L;
     L.Wl = p; p += 36 * N;  L.cs = p; p += 2 * N;  L.ct = p; p += 4 * N;
-    L.Lm = p; p += 78 * N; L.Hx = p; p += 156 * N;          // Z = D^-1/2 L^-1 packed lower triangle, Hux
-    L.V0 = p; p += 169;                                     // V (the update is written over it)
-    L.Gt = p; p += 169; L.Ft = p; p += 156; L.Mt = L.Ft;    // Y reuses F's storage (single wave, in order)
+    L.Kst = p; p += 156 * N;                                // K_k = -Hu^-1 Hux, 12 x 13 row-major per grid
+    L.Hst = p; p += 78 * N;                                 // Hu_k^-1, packed lower triangle per grid
+    L.T = p; p += 300;                                      // factor transposes (column-major 12-row blocks)
     L.Q3 = p; p += 6 * N; L.Rh = p; p += 24 * N;
     L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N;
-    L.rX = p; p += 26 * N; L.rU = p; p += 24 * N; L.dX = p; p += 13 * N; L.dU = p; p += 12 * N;
-    L.gX = L.rX + 13 * N; L.gU = L.rU + 12 * N;              // gradients: column 1 (free until the refinement)
-    L.gus = p; p += 12 * N; L.vv = p; p += 16; L.sc = p; p += 16;
+    L.rX = p; L.rU = p + 13 * N; L.gX = p + 25 * N; L.gU = p + 38 * N; L.xsv = p; p += 50 * N;
+    L.dX = p; p += 13 * N; L.dU = p; p += 12 * N; L.kff = p; p += 12 * N;
+    L.vv = p; p += 16; L.sc = p; p += 16;
     L.obs = p; p += 2 * N * K; L.eps = p; p += K;
-    L.xsv = p; p += 24 * N + 1;                             // the interior-point result (polish)
     L.sel = (int *)p;
     return L;
 }
-
-// pivot-row entries of the forward elimination: every 16-lane row holds the whole matrix, so a DPP
-// row broadcast (SRB12_ELIM_DPP=1) or a readlane of lane kk (0) give the same value
-#ifndef SRB12_ELIM_DPP
-#define SRB12_ELIM_DPP 0
-#endif
-#if SRB12_ELIM_DPP
-#define SRB12_PIVROW(v, kk) bc16((v), (kk))
-#else
-#define SRB12_PIVROW(v, kk) readlane_d((v), (kk))
-#endif
 
 // per-phase cycle stamps of the traced agent (diagnostic build -DSRB12_STAMPS, libsrbnmpc_s12st.so):
 // s_memtime deltas accumulated into prm.dbg[SRB12_DBG_TRACE + slot], read by srb12_debug_trace
@@ -133,11 +125,60 @@ __device__ __forceinline__ int sym3(int a, int b)
     const int i = a < b ? a : b, j = a < b ? b : a;
     return (i == 0) ? j : (i == 1) ? 2 + j : 5;
 }
-
+// packed lower-triangle index of (i, j)
+__device__ __forceinline__ int tri(int i, int j)
+{
+    return (i >= j) ? (i * (i + 1)) / 2 + j : (j * (j + 1)) / 2 + i;
+}
+// A~_k[i][j] (13 x 13: the 12 states and the slack; zero beyond)
+__device__ __forceinline__ double atil(int i, int j, double Ts, double c, double s)
+{
+    double v = (i == j && i < 13) ? 1.0 : 0.0;
+    if (i < 3 && j == i + 6) v = Ts;
+    if (i >= 3 && i < 6 && j >= 9 && j < 12) v = Ts * rzab(j - 9, i - 3, c, s);
+    return v;
+}
+// B~_k[i][j] (13 x 12: state row i, input j = 3 leg + axis; zero beyond)
+__device__ __forceinline__ double btil(int i, int j, const double *W, const double *ct, double tsm)
+{
+    if (j >= 12) return 0.0;
+    const int l = j / 3, a = j - 3 * l;
+    if (i >= 6 && i < 9) return (a == i - 6) ? ct[l] * tsm : 0.0;
+    if (i >= 9 && i < 12) return W[9 * l + 3 * (i - 9) + a];
+    return 0.0;
+}
+// value of x held by lane `src` (any 64-bit register): ds_bpermute, no LDS memory traffic
+__device__ __forceinline__ double perm_d(double x, int src)
+{
+    const long long b = __double_as_longlong(x);
+    const int lo = __builtin_amdgcn_ds_bpermute(src << 2, (int)b);
+    const int hi = __builtin_amdgcn_ds_bpermute(src << 2, (int)(b >> 32));
+    return __longlong_as_double(((long long)hi << 32) | (unsigned int)lo);
+}
+// sum over the four 16-lane rows (lanes l, l^16, l^32, l^48), every lane gets the total: two
+// permlane-swap stages, two values interleaved
+__device__ __forceinline__ void rowsum2(double &a, double &b)
+{
+    double a0, a1, b0, b1;
+    swap_d<32>(a, a0, a1); swap_d<32>(b, b0, b1);
+    a = a0 + a1; b = b0 + b1;
+    swap_d<16>(a, a0, a1); swap_d<16>(b, b0, b1);
+    a = a0 + a1; b = b0 + b1;
+}
+__device__ __forceinline__ double rowsum(double a)
+{
+    double a0, a1;
+    swap_d<32>(a, a0, a1); a = a0 + a1;
+    swap_d<16>(a, a0, a1); return a0 + a1;
+}
+__device__ __forceinline__ d4 mfma(double a, double b, d4 c)
+{
+    return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
+}
 
 } // namespace
 
-template <int TS>
+template <int TL, int TO>
 __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, const double *__restrict__ x0g,
         const double *__restrict__ xrefg, const double *__restrict__ footg, const int *__restrict__ contactg,
         const double *__restrict__ obstacles, const double *__restrict__ nbr_state, const int *__restrict__ sel_g,
@@ -145,10 +186,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         int *__restrict__ status_out, int *__restrict__ iters_out, double *lds)
 {
     const int tid = threadIdx.x, lane = tid;
-    const int N = prm.N, K = prm.K_obs + prm.K_nbr, NK = N * K, nv = 24 * N + 1;
-    const int nf = 24 * N;                                  // friction row slots
+    const int N = prm.N, K = prm.K_obs + prm.K_nbr, NK = N * K, nv = 24 * N + 1, NL = 4 * N;
     const double Ts = prm.Ts, tsm = prm.Ts / prm.mass, mus = prm.mus;
     const double tol = prm.tol, th = tol / sqrt(3.0);
+    const int ci = lane & 15, gi = lane >> 4;          // column / component, 16-lane row
     Srb12Lds L = carve12(lds, N, K);
     double *X = L.Z, *U = L.Z + 12 * N;
     const double *x0 = x0g + 12 * (size_t)agent;
@@ -223,33 +264,25 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         SYNC();
     }
 
-    // ---------------- slot state (registers): row t of this lane is slot id = lane + 64 t
-    double ss[TS], zz[TS], dsa[TS], dza[TS];
+    // ---------------- row slots (registers).  Leg slot t of this lane: leg e = lane + 64 t (grid e / 4,
+    // leg e % 4), its six friction rows q (global row 6 e + q, the oracle's stage-major order) when the
+    // leg is in stance.  Obstacle slot t: row e = lane + 64 t (grid e / K, row e % K; global row
+    // 24 N + e), NLP stage only.  s, z and the predictor's ds, dz (kept for the corrector).
+    double ls[TL][6], lz[TL][6], lsa[TL][6], lza[TL][6];
+    double os[TO], oz[TO], osa[TO], oza[TO];
+    bool lon[TL], oon[TO];
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
-    int nrow = nf;                                      // rows of the current stage (row_g)
-    auto row_g = [&](int id, double &g, double &h, double &c0, double &c1, double &c2, int &kind) {
-        g = 0.0; h = 0.0; c0 = c1 = c2 = 0.0; kind = 0;
-        if (id < nf) {
-            const int k = id / 24, l = (id / 6) & 3, q = id % 6;
-            if (L.ct[4 * k + l] != 0.0) {
-                kind = 1;
-                fric_coef(q, mus, c0, c1, c2);
-                const double *u = U + 12 * k + 3 * l;
-                g = c0 * u[0] + c1 * u[1] + c2 * u[2];
-                h = (q == 5) ? prm.fmax : 0.0;
-            }
-        } else if (id < nrow) {
-            const int e = id - nf, k = e / K, j = e - k * K;
-            kind = 2;
-            const double dx = X[12 * k] - L.obs[2 * e], dy = X[12 * k + 1] - L.obs[2 * e + 1];
-            c0 = -2.0 * dx; c1 = -2.0 * dy;
-            g = -(dx * dx + dy * dy) - L.Z[24 * N];
-            h = -L.eps[j];
-        }
+    // obstacle row e at the current iterate: g, h and the Jacobian (c0, c1) on (p_x, p_y) (-1 on s)
+    auto obs_row = [&](int e, double &g, double &h, double &c0, double &c1) {
+        const int k = e / K, j = e - k * K;
+        const double dx = X[12 * k] - L.obs[2 * e], dy = X[12 * k + 1] - L.obs[2 * e + 1];
+        c0 = -2.0 * dx; c1 = -2.0 * dy;
+        g = -(dx * dx + dy * dy) - L.Z[24 * N];
+        h = -L.eps[j];
     };
-    // Q^_k (state block k, 13 x 13): diag(q) + delta on the 12 states, the obstacle rows' (p_x, p_y, s)
-    // block; the slack's own weight Sw + delta enters once, at s_0
+    // Q^_k (state block k, 13 x 13) entry: diag(q) + delta on the 12 states, the obstacle rows' (p_x,
+    // p_y, s) block; the slack's own weight Sw + delta enters once, at s_0 (the factor's last pivot)
     auto qhat = [&](int k, int i, int j, double delta) {
         double v = (i == j && i < 12) ? ((k == N - 1) ? prm.qN[i] : prm.q[i]) + delta : 0.0;
         const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
@@ -261,211 +294,195 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         }
         return v;
     };
-    // backward Riccati factor over the 13-state with the shift delta; false when a pivot (the inertia
-    // test) or the initial slack's Schur complement is not positive.  Reads the per-grid Hessian blocks
-    // (Q3, Rh), writes Z = D^-1/2 L^-1 and Hux per grid and sets `schur`
+    // R^_k entry (12 x 12): r + delta on the diagonal, each stance leg's 3 x 3 row block (Rh)
+    auto rhat = [&](int k, int i, int j, double delta) {
+        if (i >= 12 || j >= 12) return 0.0;
+        double v = (i == j) ? prm.r[i % 3] + delta : 0.0;
+        if (i / 3 == j / 3) v += L.Rh[24 * k + 6 * (i / 3) + sym3(i % 3, j % 3)];
+        return v;
+    };
+
+    // ---------------- backward Riccati factor over the 13-state with the shift delta.  false when a
+    // pivot (the inertia test) or the initial slack's Schur complement is not positive.  Reads the
+    // per-grid blocks (Q3, Rh), writes K_k and Hu_k^-1 per grid, sets `schur`.
     double schur = 0.0;
     auto factor = [&](double delta) -> bool {
         int fail = 0;
-        for (int e = tid; e < 169; e += 64) L.V0[e] = qhat(N - 1, e / 13, e % 13, delta);
-        SYNC();
+        d4 Vd;                                            // V in the MFMA accumulator layout: V[gi + 4 q][ci]
+#pragma unroll
+        for (int q = 0; q < 4; q++) Vd[q] = qhat(N - 1, gi + 4 * q, ci, delta);
         for (int k = N - 1; k >= 0; k--) {
             const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *V = L.V0;
-            // G = V A~_k (13 x 13), F = V B~_k (13 x 12)
-            for (int e = tid; e < 169; e += 64) {
-                const int i = e / 13, j = e - 13 * i;
-                const double *Vi = V + 13 * i;
-                double g = Vi[j];
-                if (j >= 6 && j < 9) g = fma(Ts, Vi[j - 6], g);
-                else if (j >= 9 && j < 12) g = fma(Ts, Vi[3] * rzab(j - 9, 0, c, s) + Vi[4] * rzab(j - 9, 1, c, s) + Vi[5] * rzab(j - 9, 2, c, s), g);
-                L.Gt[e] = g;
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+            // operand values: A~[4 kb + gi][ci] (B operand of A~, A operand of A~'), B~ likewise (rows
+            // 4..11 only: kb = 1, 2)
+            double Ab[4];
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) Ab[kb] = atil(4 * kb + gi, ci, Ts, c, s);
+            const double Bb1 = btil(4 + gi, ci, W, ct, tsm), Bb2 = btil(8 + gi, ci, W, ct, tsm);
+            d4 G = {0.0, 0.0, 0.0, 0.0}, F = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) G = mfma(Vd[kb], Ab[kb], G);           // G = V A~
+            F = mfma(Vd[1], Bb1, F); F = mfma(Vd[2], Bb2, F);                      // F = V B~
+            d4 Vn, Hu, Hux = {0.0, 0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                Vn[q] = (k > 0) ? qhat(k - 1, gi + 4 * q, ci, delta) : 0.0;
+                Hu[q] = rhat(k, gi + 4 * q, ci, delta);
             }
-            for (int e = tid; e < 156; e += 64) {
-                const int i = e / 12, j = e - 12 * i, l = j / 3, jj = j - 3 * l;
-                const double *Vi = V + 13 * i;
-                double f = ct[l] * tsm * Vi[6 + jj];
-                for (int a = 0; a < 3; a++) f = fma(Vi[9 + a], W[9 * l + 3 * a + jj], f);
-                L.Ft[e] = f;
-            }
-            SYNC();
-            // Hux = B'G (12 x 13, stored), V_next = Q^_{k-1} + A~'G (then - Hux' Hu^-1 Hux); at k = 0 only
-            // V_0[12][12] is used (the initial slack's Schur complement)
-            double *Hx = L.Hx + 156 * k, *Vn = L.V0;
-            for (int e = tid; e < 156; e += 64) {
-                const int i = e / 13, j = e - 13 * i;
-                const int li = i / 3, ai = i - 3 * li;
-                double hx = ct[li] * tsm * L.Gt[13 * (6 + ai) + j];
-                for (int a = 0; a < 3; a++) hx = fma(W[9 * li + 3 * a + ai], L.Gt[13 * (9 + a) + j], hx);
-                Hx[e] = hx;
-            }
-            for (int e = tid; e < 169; e += 64) {
-                const int i = e / 13, j = e - 13 * i;
-                double w = L.Gt[e];
-                if (i >= 6 && i < 9) w = fma(Ts, L.Gt[13 * (i - 6) + j], w);
-                else if (i >= 9 && i < 12)
-                    w = fma(Ts, rzab(i - 9, 0, c, s) * L.Gt[39 + j] + rzab(i - 9, 1, c, s) * L.Gt[52 + j] +
-                                    rzab(i - 9, 2, c, s) * L.Gt[65 + j], w);
-                if (k > 0) w += qhat(k - 1, i, j, delta);
-                Vn[e] = w;
+#pragma unroll
+            for (int kb = 0; kb < 4; kb++) Vn = mfma(Ab[kb], G[kb], Vn);          // Q^_{k-1} + A~'G
+            Hux = mfma(Bb1, G[1], Hux); Hux = mfma(Bb2, G[2], Hux);                // B~'G (12 x 13)
+            Hu = mfma(Bb1, F[1], Hu); Hu = mfma(Bb2, F[2], Hu);                    // R^ + B~'F
+            // to the column layout: Hu, Hux column-major in T (12 rows a column)
+#pragma unroll
+            for (int q = 0; q < 3; q++) {
+                const int i = gi + 4 * q;
+                if (ci < 12) L.T[12 * ci + i] = Hu[q];
+                if (ci < 13) L.T[144 + 12 * ci + i] = Hux[q];
             }
             SYNC();
-            // Hu = R^ + B'F = L D L' by a forward elimination of [Hu | Hux | I] in registers (row i16
-            // per lane, replicated in every 16-lane row): its pivots are the inertia test, Z = D^-1/2 L^-1
-            // (stored: the solves apply Hu^-1 = Z'Z) and Y = Z Hux, so the Schur update
-            // S = Hux' Hu^-1 Hux = Y'Y is one 16x16x16 product on the matrix cores.  The product with
-            // an explicit inverse, Hux'(Hu^-1 Hux), loses V's definiteness once z / s reaches ~1e7 on
-            // active rows; Y'Y is positive semi-definite by construction.
+            // lane j < 12: column j of Hu; 12..24: column j - 12 of Hux; 25..36: column j - 25 of I
+            double col[12];
             {
-                const int i16 = lane & 15, q = lane >> 4;
-                double Ag[37];
-                {
-                    const int li = (i16 < 12) ? i16 / 3 : 0, ai = (i16 < 12) ? i16 - 3 * li : 0;
+                const double *src = (lane < 12) ? L.T + 12 * lane : L.T + 144 + 12 * (lane < 25 ? lane - 12 : 0);
 #pragma unroll
-                    for (int j = 0; j < 12; j++) {
-                        double v = 0.0;
-                        if (i16 < 12) {
-                            v = ct[li] * tsm * L.Ft[12 * (6 + ai) + j];
-                            for (int aa = 0; aa < 3; aa++) v = fma(W[9 * li + 3 * aa + ai], L.Ft[12 * (9 + aa) + j], v);
-                            if (j == i16) v += prm.r[ai] + delta;
-                            if (j / 3 == li) v += L.Rh[24 * k + 6 * li + sym3(ai, j - 3 * (j / 3))];
-                        }
-                        Ag[j] = v;
-                    }
+                for (int r = 0; r < 12; r++) col[r] = (lane < 25) ? src[r] : ((lane - 25 == r) ? 1.0 : 0.0);
+            }
+            SYNC();
+            // Hu = L D L': forward elimination, row i -= (Hu[i][kk] / d_kk) row kk for i > kk, on every column.
+            // Lane kk holds column kk, whose entries below the pivot are the multipliers (readlane)
+            double dinv[12];
 #pragma unroll
-                    for (int j = 0; j < 13; j++) Ag[12 + j] = (i16 < 12) ? Hx[13 * i16 + j] : 0.0;
+            for (int kk = 0; kk < 12; kk++) {
+                const double piv = readlane_d(col[kk], kk);
+                fail |= !(piv > 0.0);
+                const double t = col[kk] * rcp_d(piv);
 #pragma unroll
-                    for (int j = 0; j < 12; j++) Ag[25 + j] = (i16 == j) ? 1.0 : 0.0;
-                }
-                double dk = 1.0;
+                for (int i = kk + 1; i < 12; i++) col[i] = fma(-readlane_d(col[i], kk), t, col[i]);
+                dinv[kk] = (piv > 0.0) ? 1.0 / sqrt(piv) : 0.0;
+            }
+            // Y = D^-1/2 L^-1 Hux (lanes 12..24), Z = D^-1/2 L^-1 (lanes 25..36), back to T column-major
+            if (lane >= 12 && lane < 37)
 #pragma unroll
-                for (int kk = 0; kk < 12; kk++) {
-                    const double piv = readlane_d(Ag[kk], kk);
-                    fail |= !(piv > 0.0);
-                    const double f = (i16 > kk && i16 < 12) ? Ag[kk] * rcp_d(piv) : 0.0;
+                for (int r = 0; r < 12; r++) L.T[12 * (lane - 12) + r] = col[r] * dinv[r];
+            SYNC();
+            // Y'Y (13 x 13), Hu^-1 = Z'Z (12 x 12), Z'Y = -K (12 x 13): operands Y[4 kb + gi][ci], Z[..][ci]
+            d4 YY = {0.0, 0.0, 0.0, 0.0}, ZZ = {0.0, 0.0, 0.0, 0.0}, ZY = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
-                    for (int j = kk + 1; j < 25; j++) Ag[j] = fma(-f, SRB12_PIVROW(Ag[j], kk), Ag[j]);
+            for (int kb = 0; kb < 3; kb++) {
+                const int r = 4 * kb + gi;
+                const double ya = (ci < 13) ? L.T[12 * ci + r] : 0.0;
+                const double za = (ci < 12) ? L.T[156 + 12 * ci + r] : 0.0;
+                YY = mfma(ya, ya, YY); ZZ = mfma(za, za, ZZ); ZY = mfma(za, ya, ZY);
+            }
+            Vd = Vn - YY;                                  // V_{k-1} = Q^ + A~'G - Hux' Hu^-1 Hux
+            double *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
 #pragma unroll
-                    for (int j = 0; j <= kk; j++) Ag[25 + j] = fma(-f, SRB12_PIVROW(Ag[25 + j], kk), Ag[25 + j]);
-                    dk = (i16 == kk) ? piv : dk;
-                }
-                const double sc_ = (i16 < 12 && dk > 0.0) ? 1.0 / sqrt(dk) : 0.0;
-                if (lane < 12) {
-#pragma unroll
-                    for (int j = 0; j < 13; j++) L.Mt[13 * lane + j] = Ag[12 + j] * sc_;
-#pragma unroll
-                    for (int j = 0; j < 12; j++)
-                        if (j <= lane) L.Lm[78 * k + (lane * (lane + 1)) / 2 + j] = Ag[25 + j] * sc_;
-                }
-                SYNC();
-                d4 acc2 = {0.0, 0.0, 0.0, 0.0};
-#pragma unroll
-                for (int kk = 0; kk < 4; kk++) {
-                    const int kc = 4 * kk + q;
-                    const double y = (kc < 12 && i16 < 13) ? L.Mt[13 * kc + i16] : 0.0;
-                    acc2 = __builtin_amdgcn_mfma_f64_16x16x4f64(y, y, acc2, 0, 0, 0);
-                }
-#pragma unroll
-                for (int r = 0; r < 4; r++) {
-                    const int row = q + 4 * r;
-                    if (row < 13 && i16 < 13) Vn[13 * row + i16] -= acc2[r];
-                }
+            for (int q = 0; q < 3; q++) {
+                const int i = gi + 4 * q;
+                if (ci < 13) Kk[13 * i + ci] = -ZY[q];
+                if (ci <= i) Hk[tri(i, ci)] = ZZ[q];
             }
             SYNC();
         }
         if (fail) return false;
-        // the free initial slack closes the recursion: V_0[12][12] + Sw + delta > 0 is the last
-        // pivot of the inertia test
-        schur = L.V0[168] + prm.Sw + delta;
+        // the free initial slack closes the recursion: V_-1[12][12] + Sw + delta > 0 is the last
+        // pivot of the inertia test (row 12 = gi 0, q 3; column 12 = lane 12)
+        schur = readlane_d(Vd[3], 12) + prm.Sw + delta;
         return schur > 0.0;
     };
-    // Riccati solve of column c (rX: 13 per grid, rU: 12 per grid, sc[2 + c]: the s_0 entry) into
-    // dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0 free).
-    // Vectors live in registers, component i = lane & 15 (each 16-lane row holds a copy), and move
-    // between lanes by DPP row broadcasts: no LDS round trip or barrier inside the recursion.
+
+    // ---------------- Riccati solve of column c (rX / gX: 13 per grid, rU / gU: 12, sc[2 + c]: the s_0
+    // entry) into dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0
+    // free).  Component i = ci of every vector, replicated in the four rows; row gi takes columns
+    // 4 gi .. 4 gi + 3 of each matrix-vector product (perm_d gathers them), rowsum adds the rows.
     auto riccati_solve = [&](int c, bool acc) {
-        const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l, tri = (ir * (ir + 1)) / 2;
-        const double *rX = L.rX + 13 * N * c, *rU = L.rU + 12 * N * c;
-        double *dX = L.dX, *dU = L.dU, *gus = L.gus;      // acc: the refinement's correction adds in
+        const int i = ci, g = gi, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
+        const double *rX = c ? L.gX : L.rX, *rU = c ? L.gU : L.rU;
+        const int gsrc = 16 * g + 4 * g;                   // lane holding component 4 g (this row's copy)
         double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
         for (int k = N - 1; k >= 0; k--) {
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hx = L.Hx + 156 * k;
-            double vb[13];
-#pragma unroll
-            for (int j = 0; j < 13; j++) vb[j] = bc16(v, j);
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
+            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+            const double v6 = bc16(v, 6), v7 = bc16(v, 7), v8 = bc16(v, 8), v9 = bc16(v, 9), v10 = bc16(v, 10), v11 = bc16(v, 11);
+            // gu = rhs_u + B~'v
             double gu = 0.0;
             if (i < 12) {
-                gu = rU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
-                for (int a = 0; a < 3; a++) gu = fma(W[9 * l + 3 * a + jj], vb[9 + a], gu);
+                gu = fma(ct[l] * tsm, a == 0 ? v6 : a == 1 ? v7 : v8, rU[12 * k + i]);
+                gu = fma(W[9 * l + a], v9, gu); gu = fma(W[9 * l + 3 + a], v10, gu); gu = fma(W[9 * l + 6 + a], v11, gu);
             }
-            if (lane < 12) gus[12 * k + i] = gu;
-            double w = 0.0, kk = 0.0;                        // kk = -Z'(Z gu)
+            // K'gu (state i) and -Hu^-1 gu (input i): this row's four input columns j = 4 g + m
+            double pk = 0.0, ph = 0.0;
 #pragma unroll
-            for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(gu, j), w);
-            if (i >= 12) w = 0.0;
-#pragma unroll
-            for (int j = 0; j < 12; j++) kk = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), kk);
-            if (i >= 12) kk = 0.0;
-            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-            double vn = v;                                     // A~' v
-            if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], vn);
+            for (int m = 0; m < 4; m++) {
+                const int j = 4 * g + m;
+                const double gj = perm_d(gu, gsrc + m);
+                if (j < 12) {
+                    pk = fma((i < 13) ? Kk[13 * j + i] : 0.0, gj, pk);
+                    ph = fma((i < 12) ? Hk[tri(i, j)] : 0.0, gj, ph);
+                }
+            }
+            rowsum2(pk, ph);
+            if (g == 0 && i < 12) L.kff[12 * k + i] = -ph;
+            // v_{k-1} = rhs_x(k-1) + A~'v + K'gu
+            const double v0 = bc16(v, 0), v1 = bc16(v, 1), v2 = bc16(v, 2), v3 = bc16(v, 3), v4 = bc16(v, 4), v5 = bc16(v, 5);
+            double vn = v + pk;
+            if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? v0 : i == 7 ? v1 : v2, vn);
             else if (i >= 9 && i < 12)
-                vn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], vn);
+                vn = fma(Ts, i == 9 ? fma(cc, v3, -sn * v4) : i == 10 ? fma(sn, v3, cc * v4) : v5, vn);
             if (k > 0 && i < 13) vn += rX[13 * (k - 1) + i];
-            if (i < 13)
-#pragma unroll
-                for (int j = 0; j < 12; j++) vn = fma(Hx[13 * j + i], bc16(kk, j), vn);
             v = (i < 13) ? vn : 0.0;
         }
         const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
+        SYNC();                                            // kff
         double prev = (i == 12) ? ds0 : 0.0;
+        const int lsrc = 16 * g + 3 * g;                   // lane holding component 3 g (leg g's first force)
         for (int k = 0; k < N; k++) {
-            // t = Hux dx_k + gu_k ; du_k = -Hu^-1 t ; dx_{k+1} = A~_k dx_k + B~_k du_k
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Zk = L.Lm + 78 * k, *Hr = L.Hx + 156 * k + 13 * ir;
-            double pb[13];
-#pragma unroll
-            for (int j = 0; j < 13; j++) pb[j] = bc16(prev, j);
-            double t = gus[12 * k + ir];
-#pragma unroll
-            for (int j = 0; j < 13; j++) t = fma(Hr[j], pb[j], t);
-            if (i >= 12) t = 0.0;
-            double w = 0.0, du = 0.0;                        // du = -Z'(Z t)
-#pragma unroll
-            for (int j = 0; j < 12; j++) w = fma((j <= ir) ? Zk[tri + j] : 0.0, bc16(t, j), w);
-            if (i >= 12) w = 0.0;
-#pragma unroll
-            for (int j = 0; j < 12; j++) du = fma((ir <= j) ? -Zk[(j * (j + 1)) / 2 + ir] : 0.0, bc16(w, j), du);
-            if (i >= 12) du = 0.0;
-            if (lane < 12) dU[12 * k + i] = acc ? dU[12 * k + i] + du : du;
-            double db[12];
-#pragma unroll
-            for (int j = 0; j < 12; j++) db[j] = bc16(du, j);
+            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k;
             const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-            double dx = prev;
-            if (i < 3) dx = fma(Ts, i == 0 ? pb[6] : i == 1 ? pb[7] : pb[8], dx);
-            else if (i < 6)
-                dx = fma(Ts, i == 3 ? fma(cc, pb[9], sn * pb[10]) : i == 4 ? fma(-sn, pb[9], cc * pb[10]) : pb[11], dx);
-            else if (i < 9) {
-                for (int ll = 0; ll < 4; ll++) dx = fma(ct[ll] * tsm, i == 6 ? db[3 * ll] : i == 7 ? db[3 * ll + 1] : db[3 * ll + 2], dx);
-            } else if (i < 12) {
-                const int a = i - 9;
-                for (int ll = 0; ll < 4; ll++)
-                    for (int j = 0; j < 3; j++) dx = fma(W[9 * ll + 3 * a + j], db[3 * ll + j], dx);
+            // du = kff + K dx: this row's state columns j = 4 g + m
+            double pk = 0.0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const int j = 4 * g + m;
+                const double dj = perm_d(prev, gsrc + m);
+                if (j < 13) pk = fma((i < 12) ? Kk[13 * ir + j] : 0.0, dj, pk);
             }
+            double du = rowsum(pk) + ((i < 12) ? L.kff[12 * k + i] : 0.0);
+            if (i >= 12) du = 0.0;
+            if (g == 0 && i < 12) L.dU[12 * k + i] = acc ? L.dU[12 * k + i] + du : du;
+            // dx_{k+1} = A~ dx + B~ du: row g adds leg g's forces (and row 0 the A~ part)
+            const double d0 = perm_d(du, lsrc), d1 = perm_d(du, lsrc + 1), d2 = perm_d(du, lsrc + 2);
+            double pb = 0.0;
+            if (i >= 6 && i < 9) pb = ct[g] * tsm * (i == 6 ? d0 : i == 7 ? d1 : d2);
+            else if (i >= 9 && i < 12) {
+                const double *w = W + 9 * g + 3 * (i - 9);
+                pb = fma(w[0], d0, fma(w[1], d1, w[2] * d2));
+            }
+            if (g == 0) {
+                const double p6 = bc16(prev, 6), p7 = bc16(prev, 7), p8 = bc16(prev, 8);
+                const double p9 = bc16(prev, 9), p10 = bc16(prev, 10), p11 = bc16(prev, 11);
+                double ax = prev;
+                if (i < 3) ax = fma(Ts, i == 0 ? p6 : i == 1 ? p7 : p8, ax);
+                else if (i < 6)
+                    ax = fma(Ts, i == 3 ? fma(cc, p9, sn * p10) : i == 4 ? fma(-sn, p9, cc * p10) : p11, ax);
+                pb += ax;
+            }
+            double dx = rowsum(pb);
             if (i > 12) dx = 0.0;
-            if (lane < 13) dX[13 * k + i] = acc ? dX[13 * k + i] + dx : dx;
+            if (g == 0 && i < 13) L.dX[13 * k + i] = acc ? L.dX[13 * k + i] + dx : dx;
             prev = dx;
         }
         SYNC();
     };
     // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
     // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
-    // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s).
-    // Explicit Gauss-Jordan inverses lose digits once z / s reaches 1e7 on active rows.
+    // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s)
     auto refine = [&](double delta) {
-        const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
+        const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
         const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
-        double *tX = L.rX + 13 * N, *tU = L.rU + 12 * N;
+        double *tX = L.gX, *tU = L.gU;
         auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
             double v = 0.0;
             for (int j = 0; j < 13; j++) {
@@ -503,100 +520,157 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         SYNC();
         riccati_solve(1, true);
     };
-    // right-hand side of pass (0 predictor, 1 corrector) into column 0:
-    // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
-    auto build_rhs = [&](int pass, double smu) {
+
+    // ---------------- the rows: gradient of f and J'z into column 1, the Hessian blocks (leg blocks Rh
+    // written by their lanes, obstacle blocks Q3 by atomics), residual sums.  y(row): the multiplier
+    // (z, or the polish's z_A + RHO c_A); w(row): the Hessian weight (z / s, or RHO / 0)
+    auto grad_f = [&](double *gx, double *gu) {
         for (int e = tid; e < 12 * N; e += 64) {
             const int k = e / 12, i = e - 12 * k;
             const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
-            L.rX[13 * k + i] = w * (X[e] - L.xr[e]);
-            L.rU[e] = prm.r[i % 3] * U[e];
+            gx[13 * k + i] = w * (X[e] - L.xr[e]);
+            gu[e] = prm.r[i % 3] * U[e];
         }
-        for (int k = tid; k < N; k += 64) L.rX[13 * k + 12] = 0.0;
+        for (int k = tid; k < N; k += 64) gx[13 * k + 12] = 0.0;
+    };
+    // right-hand side of pass (0 predictor, 1 corrector) into column 0:
+    // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
+    auto build_rhs = [&](int pass, double smu) {
+        grad_f(L.rX, L.rU);
         if (tid == 0) L.sc[2] = prm.Sw * L.Z[24 * N];
         SYNC();
 #pragma unroll
-        for (int t = 0; t < TS; t++) {
-            const int id = lane + 64 * t;
-            double g, h, c0, c1, c2; int kind;
-            row_g(id, g, h, c0, c1, c2, kind);
-            if (!kind) continue;
-            const double rp = g + ss[t] - h, om = zz[t] / ss[t];
-            const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
-            const double w = zz[t] + r3 / ss[t] + om * rp;
-            if (kind == 1) {
-                const int k = id / 24, l = (id / 6) & 3;
-                double *ru = L.rU + 12 * k + 3 * l;
-                const double cc[3] = {c0, c1, c2};
-                for (int a = 0; a < 3; a++)
-                    if (cc[a] != 0.0) __hip_atomic_fetch_add(&ru[a], w * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-            } else {
-                double *rx = L.rX + 13 * ((id - nf) / K);
-                __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+        for (int t = 0; t < TL; t++) {
+            if (!lon[t]) continue;
+            const int e = lane + 64 * t;
+            const double *u = U + 3 * e;
+            double r[3] = {0.0, 0.0, 0.0};
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                double c0, c1, c2;
+                fric_coef(q, mus, c0, c1, c2);
+                const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
+                const double s = ls[t][q], z = lz[t][q];
+                const double rp = g + s - h, om = z / s;
+                const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
+                const double w = z + r3 / s + om * rp;
+                r[0] = fma(w, c0, r[0]); r[1] = fma(w, c1, r[1]); r[2] = fma(w, c2, r[2]);
             }
+            double *ru = L.rU + 3 * e;
+            ru[0] += r[0]; ru[1] += r[1]; ru[2] += r[2];
+        }
+#pragma unroll
+        for (int t = 0; t < TO; t++) {
+            if (!oon[t]) continue;
+            const int e = lane + 64 * t;
+            double g, h, c0, c1;
+            obs_row(e, g, h, c0, c1);
+            const double s = os[t], z = oz[t];
+            const double rp = g + s - h, om = z / s;
+            const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
+            const double w = z + r3 / s + om * rp;
+            double *rx = L.rX + 13 * (e / K);
+            __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
         }
         SYNC();
     };
-    // the rows' steps of the solved column: J dz, ds = -r_p - J dz, dz = (r3 - z ds) / s; step maxima
-    auto row_step = [&](int pass, double smu, double (&dsl)[TS], double (&dzl)[TS]) {
+    // the rows' steps of the solved column: J dw, ds = -r_p - J dw, dz = (r3 - z ds) / s; step maxima
+    auto row_step = [&](int pass, double smu, double (&dls)[TL][6], double (&dlz)[TL][6], double (&dos)[TO],
+                        double (&doz)[TO]) {
         double ms = 0.0, mz = 0.0;
 #pragma unroll
-        for (int t = 0; t < TS; t++) {
-            const int id = lane + 64 * t;
-            double g, h, c0, c1, c2; int kind;
-            row_g(id, g, h, c0, c1, c2, kind);
-            dsl[t] = dzl[t] = 0.0;
-            if (!kind) continue;
-            double jd;
-            if (kind == 1) {
-                const int k = id / 24, l = (id / 6) & 3;
-                const double *du = L.dU + 12 * k + 3 * l;
-                jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
-            } else {
-                const double *dx = L.dX + 13 * ((id - nf) / K);
-                jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+        for (int t = 0; t < TL; t++) {
+#pragma unroll
+            for (int q = 0; q < 6; q++) dls[t][q] = dlz[t][q] = 0.0;
+            if (!lon[t]) continue;
+            const int e = lane + 64 * t;
+            const double *u = U + 3 * e, *du = L.dU + 3 * e;
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                double c0, c1, c2;
+                fric_coef(q, mus, c0, c1, c2);
+                const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
+                const double jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
+                const double s = ls[t][q], z = lz[t][q];
+                const double rp = g + s - h;
+                const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
+                dls[t][q] = -rp - jd; dlz[t][q] = (r3 - z * dls[t][q]) / s;
+                ms = fmax(ms, -dls[t][q] / s); mz = fmax(mz, -dlz[t][q] / z);
             }
-            const double rp = g + ss[t] - h;
-            const double r3 = -ss[t] * zz[t] + (pass ? smu - dsa[t] * dza[t] : 0.0);
-            dsl[t] = -rp - jd; dzl[t] = (r3 - zz[t] * dsl[t]) / ss[t];
-            ms = fmax(ms, -dsl[t] / ss[t]); mz = fmax(mz, -dzl[t] / zz[t]);
+        }
+#pragma unroll
+        for (int t = 0; t < TO; t++) {
+            dos[t] = doz[t] = 0.0;
+            if (!oon[t]) continue;
+            const int e = lane + 64 * t;
+            double g, h, c0, c1;
+            obs_row(e, g, h, c0, c1);
+            const double *dx = L.dX + 13 * (e / K);
+            const double jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+            const double s = os[t], z = oz[t];
+            const double rp = g + s - h;
+            const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
+            dos[t] = -rp - jd; doz[t] = (r3 - z * dos[t]) / s;
+            ms = fmax(ms, -dos[t] / s); mz = fmax(mz, -doz[t] / z);
         }
         double rv[2] = {ms, mz};
         wred<2, 3u>(rv);
         return make_double2(rv[0] > 0.0 ? 1.0 / rv[0] : 1.0, rv[1] > 0.0 ? 1.0 / rv[1] : 1.0);
     };
+
     S12ST(0);   // inputs, model, rollout
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
-        nrow = nl ? nf + NK : nf;
-        // active row count m and the starting slacks / duals (oracle ipm(): QP s = h - g, z = 1 /
-        // max(s, 1); NLP shifted so min s = 1 when a row is violated, z = z0 / max(s, 1))
+        // active rows and the starting slacks / duals (oracle ipm(): QP s = h - g, z = 1 / max(s, 1);
+        // NLP shifted so min s = 1 when a row is violated, z = z0 / max(s, 1))
         double mcount = 0.0, mn = 1e300;
 #pragma unroll
-        for (int t = 0; t < TS; t++) {
-            double g, h, c0, c1, c2; int kind;
-            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
-            ss[t] = h - g;
-            if (kind) { mcount += 1.0; mn = fmin(mn, h - g); }
+        for (int t = 0; t < TL; t++) {
+            const int e = lane + 64 * t;
+            lon[t] = e < NL && L.ct[e] != 0.0;
+            const double *u = U + 3 * (lon[t] ? e : 0);
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                double c0, c1, c2;
+                fric_coef(q, mus, c0, c1, c2);
+                ls[t][q] = ((q == 5) ? prm.fmax : 0.0) - (c0 * u[0] + c1 * u[1] + c2 * u[2]);
+                if (lon[t]) { mcount += 1.0; mn = fmin(mn, ls[t][q]); }
+            }
+        }
+#pragma unroll
+        for (int t = 0; t < TO; t++) {
+            const int e = lane + 64 * t;
+            oon[t] = nl && e < NK;
+            double g = 0.0, h = 0.0, c0, c1;
+            if (oon[t]) obs_row(e, g, h, c0, c1);
+            os[t] = h - g;
+            if (oon[t]) { mcount += 1.0; mn = fmin(mn, h - g); }
         }
         {
             double rv[2] = {mcount, -mn};
             wred<2, 2u>(rv);
             mcount = rv[0]; mn = -rv[1];
         }
-        const double ssh = (nl && mn <= 0.0) ? 1.0 - mn : 0.0;
+        const double ssh = (nl && mn <= 0.0) ? 1.0 - mn : 0.0, zs = nl ? prm.z0 : 1.0;
 #pragma unroll
-        for (int t = 0; t < TS; t++) {
-            double g, h, c0, c1, c2; int kind;
-            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
-            double s = ss[t] + ssh;
-            if (!nl && s < 1e-8) s = 1e-8;
-            ss[t] = kind ? s : 1.0;
-            zz[t] = kind ? (nl ? prm.z0 : 1.0) / fmax(s, 1.0) : 0.0;
-            dsa[t] = dza[t] = 0.0;
+        for (int t = 0; t < TL; t++)
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                double s = ls[t][q] + ssh;
+                if (!nl && s < 1e-8) s = 1e-8;
+                ls[t][q] = lon[t] ? s : 1.0;
+                lz[t][q] = lon[t] ? zs / fmax(s, 1.0) : 0.0;
+                lsa[t][q] = lza[t][q] = 0.0;
+            }
+#pragma unroll
+        for (int t = 0; t < TO; t++) {
+            double s = os[t] + ssh;
+            os[t] = oon[t] ? s : 1.0;
+            oz[t] = oon[t] ? zs / fmax(s, 1.0) : 0.0;
+            osa[t] = oza[t] = 0.0;
         }
         const double inv_m = 1.0 / fmax(mcount, 1.0);
         const int maxit = nl ? prm.nlp_maxit : prm.qp_maxit;
@@ -606,55 +680,64 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         double sigma = 0.0;
 #pragma clang loop unroll(disable)
         for (it = 0; it < maxit; it++) {
-            // ---- gradient of f (X, U; Sw s of the slack at s_0), cleared per-grid blocks
-            for (int e = tid; e < 12 * N; e += 64) {
-                const int k = e / 12, i = e - 12 * k;
-                const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
-                L.gX[13 * k + i] = w * (X[e] - L.xr[e]);
-                L.gU[e] = prm.r[i % 3] * U[e];
-            }
-            for (int k = tid; k < N; k += 64) L.gX[13 * k + 12] = 0.0;
+            // ---- gradient of f (X, U; Sw s of the slack at s_0), cleared obstacle blocks
+            grad_f(L.gX, L.gU);
             for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
-            for (int e = tid; e < 24 * N; e += 64) L.Rh[e] = 0.0;
             if (tid == 0) { L.sc[0] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }    // grad_s f, H_ss (inertia scale)
             SYNC();
-            // ---- rows: residuals, weights, scatter of J'z and J'WJ into the per-grid blocks
+            // ---- rows: residuals, weights, J'z and J'WJ into the per-grid blocks
             double nrp = 0.0, sz = 0.0, zmx = 0.0;
 #pragma unroll
-            for (int t = 0; t < TS; t++) {
-                const int id = lane + 64 * t;
-                double g, h, c0, c1, c2; int kind;
-                row_g(id, g, h, c0, c1, c2, kind);
-                if (!kind) continue;
-                const double rp = g + ss[t] - h, om = zz[t] / ss[t];
-                nrp = fma(rp, rp, nrp);
-                sz = fma(ss[t], zz[t], sz);
-                zmx = fmax(zmx, zz[t]);
-                if (kind == 1) {
-                    const int k = id / 24, l = (id / 6) & 3;
-                    double *gu = L.gU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                    const double cc[3] = {c0, c1, c2};
-                    for (int a = 0; a < 3; a++)
-                        if (cc[a] != 0.0) __hip_atomic_fetch_add(&gu[a], zz[t] * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    for (int a = 0; a < 3; a++)
-                        for (int b = a; b < 3; b++)
-                            if (cc[a] != 0.0 && cc[b] != 0.0)
-                                __hip_atomic_fetch_add(&rh[sym3(a, b)], om * cc[a] * cc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                } else {
-                    // obstacle row of grid k on (p_x, p_y, s): J = (c0, c1, -1), Lagrangian Hessian -2z on p_x, p_y
-                    const int k = (id - nf) / K;
-                    double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
-                    __hip_atomic_fetch_add(&gx[0], zz[t] * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&gx[1], zz[t] * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&gx[12], -zz[t], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * zz[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * zz[t]), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    __hip_atomic_fetch_add(&L.sc[1], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+            for (int t = 0; t < TL; t++) {
+                const int e = lane + 64 * t;
+                if (e >= NL) continue;
+                double gz[3] = {0.0, 0.0, 0.0}, rh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                if (lon[t]) {
+                    const double *u = U + 3 * e;
+#pragma unroll
+                    for (int q = 0; q < 6; q++) {
+                        double c0, c1, c2;
+                        fric_coef(q, mus, c0, c1, c2);
+                        const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
+                        const double s = ls[t][q], z = lz[t][q];
+                        const double rp = g + s - h, om = z / s;
+                        nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
+                        const double cc[3] = {c0, c1, c2};
+#pragma unroll
+                        for (int a = 0; a < 3; a++) {
+                            gz[a] = fma(z, cc[a], gz[a]);
+#pragma unroll
+                            for (int b = a; b < 3; b++) rh[sym3(a, b)] = fma(om * cc[a], cc[b], rh[sym3(a, b)]);
+                        }
+                    }
+                    double *gu = L.gU + 3 * e;
+                    gu[0] += gz[0]; gu[1] += gz[1]; gu[2] += gz[2];
                 }
+#pragma unroll
+                for (int m = 0; m < 6; m++) L.Rh[6 * e + m] = rh[m];
+            }
+#pragma unroll
+            for (int t = 0; t < TO; t++) {
+                if (!oon[t]) continue;
+                const int e = lane + 64 * t;
+                double g, h, c0, c1;
+                obs_row(e, g, h, c0, c1);
+                const double s = os[t], z = oz[t];
+                const double rp = g + s - h, om = z / s;
+                nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
+                // obstacle row of grid k on (p_x, p_y, s): J = (c0, c1, -1), Lagrangian Hessian -2z on p_x, p_y
+                const int k = e / K;
+                double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
+                __hip_atomic_fetch_add(&gx[0], z * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&gx[1], z * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&gx[12], -z, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * z), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                __hip_atomic_fetch_add(&L.sc[1], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             SYNC();
             // ---- costates and the dual residual (13-state: the slack rides along as x[12], s_{k+1} = s_k):
@@ -669,24 +752,25 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             gm = fmax(gm, fabs(prm.Sw * L.Z[24 * N]));
             {
-                const int i = lane & 15, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
+                const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
                 double lam = (i < 13) ? L.gX[13 * (N - 1) + i] : 0.0;
                 for (int k = N - 1; k >= 0; k--) {
                     const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
-                    double vb[13];
-#pragma unroll
-                    for (int j = 0; j < 13; j++) vb[j] = bc16(lam, j);
+                    const double v6 = bc16(lam, 6), v7 = bc16(lam, 7), v8 = bc16(lam, 8);
+                    const double v9 = bc16(lam, 9), v10 = bc16(lam, 10), v11 = bc16(lam, 11);
                     if (lane < 12) {
-                        double ru = L.gU[12 * k + i] + ct[l] * tsm * (jj == 0 ? vb[6] : jj == 1 ? vb[7] : vb[8]);
-                        for (int a = 0; a < 3; a++) ru = fma(W[9 * l + 3 * a + jj], vb[9 + a], ru);
+                        double ru = fma(ct[l] * tsm, jj == 0 ? v6 : jj == 1 ? v7 : v8, L.gU[12 * k + i]);
+                        ru = fma(W[9 * l + jj], v9, ru); ru = fma(W[9 * l + 3 + jj], v10, ru); ru = fma(W[9 * l + 6 + jj], v11, ru);
                         nrd = fma(ru, ru, nrd);
                     }
                     if (k > 0) {
                         const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+                        const double v0 = bc16(lam, 0), v1 = bc16(lam, 1), v2 = bc16(lam, 2);
+                        const double v3 = bc16(lam, 3), v4 = bc16(lam, 4), v5 = bc16(lam, 5);
                         double ln = lam;
-                        if (i >= 6 && i < 9) ln = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], ln);
+                        if (i >= 6 && i < 9) ln = fma(Ts, i == 6 ? v0 : i == 7 ? v1 : v2, ln);
                         else if (i >= 9 && i < 12)
-                            ln = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], ln);
+                            ln = fma(Ts, i == 9 ? fma(cc, v3, -sn * v4) : i == 10 ? fma(sn, v3, cc * v4) : v5, ln);
                         lam = (i < 13) ? ln + L.gX[13 * (k - 1) + i] : 0.0;
                     }
                 }
@@ -736,18 +820,24 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             riccati_solve(0, false);
             if (refn) refine(delta);
             S12ST(4);   // predictor rhs + solve (+ refinement)
-            double dsl[TS], dzl[TS];
-            double2 al = row_step(0, 0.0, dsl, dzl);
+            double dls[TL][6], dlz[TL][6], dos[TO], doz[TO];
+            double2 al = row_step(0, 0.0, dls, dlz, dos, doz);
 #pragma unroll
-            for (int t = 0; t < TS; t++) { dsa[t] = dsl[t]; dza[t] = dzl[t]; }
+            for (int t = 0; t < TL; t++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) { lsa[t][q] = dls[t][q]; lza[t][q] = dlz[t][q]; }
+#pragma unroll
+            for (int t = 0; t < TO; t++) { osa[t] = dos[t]; oza[t] = doz[t]; }
             {
                 double num = 0.0;
 #pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    double g, h, c0, c1, c2; int kind;
-                    row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
-                    if (kind) num = fma(fma(al.x, dsa[t], ss[t]), fma(al.y, dza[t], zz[t]), num);
-                }
+                for (int t = 0; t < TL; t++)
+                    if (lon[t])
+#pragma unroll
+                        for (int q = 0; q < 6; q++) num = fma(fma(al.x, lsa[t][q], ls[t][q]), fma(al.y, lza[t][q], lz[t][q]), num);
+#pragma unroll
+                for (int t = 0; t < TO; t++)
+                    if (oon[t]) num = fma(fma(al.x, osa[t], os[t]), fma(al.y, oza[t], oz[t]), num);
                 num = wsum(num);
                 const double rho = num / sz, mr = rho < 1.0 ? rho : 1.0;
                 sigma = mr * mr * mr;
@@ -758,7 +848,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             riccati_solve(0, false);
             if (refn) refine(delta);
             S12ST(6);   // corrector rhs + solve (+ refinement)
-            al = row_step(1, sigma * mu, dsl, dzl);
+            al = row_step(1, sigma * mu, dls, dlz, dos, doz);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);
             if (dbgrow && tid == 0) { dbgrow[4] = ap; dbgrow[5] = ad; dbgrow[6] = delta; dbgrow[7] = sigma; }
             // ---- update: x += ap dx (the slack: ds_0, carried in every grid's x[12]), rows s += ap ds, z += ad dz
@@ -771,7 +861,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             if (tid == 0) L.Z[24 * N] = fma(ap, dsv, L.Z[24 * N]);
 #pragma unroll
-            for (int t = 0; t < TS; t++) { ss[t] = fma(ap, dsl[t], ss[t]); zz[t] = fma(ad, dzl[t], zz[t]); }
+            for (int t = 0; t < TL; t++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) { ls[t][q] = fma(ap, dls[t][q], ls[t][q]); lz[t][q] = fma(ad, dlz[t][q], lz[t][q]); }
+#pragma unroll
+            for (int t = 0; t < TO; t++) { os[t] = fma(ap, dos[t], os[t]); oz[t] = fma(ad, doz[t], oz[t]); }
             SYNC();
             S12ST(7);   // corrector row step + update
         }
@@ -800,15 +894,21 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     const int fin_flag = prm.use_nlp ? nlp_flag : qp_flag;
     if (prm.polish && fin_flag == 0) {
         S12ST(8);
-        bool pact[TS];
-        double za[TS], cr[TS];
+        bool lact[TL][6], oact[TO];
+        double lza_[TL][6], ozz[TO], lcr[TL][6], ocr[TO];
 #pragma unroll
-        for (int t = 0; t < TS; t++) {
-            double g, h, c0, c1, c2; int kind;
-            row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
-            pact[t] = kind && ss[t] * SRB12_POL_KAPPA < zz[t];
-            za[t] = pact[t] ? zz[t] : 0.0;
+        for (int t = 0; t < TL; t++)
+#pragma unroll
+            for (int q = 0; q < 6; q++) {
+                lact[t][q] = lon[t] && ls[t][q] * SRB12_POL_KAPPA < lz[t][q];
+                lza_[t][q] = lact[t][q] ? lz[t][q] : 0.0;
+            }
+#pragma unroll
+        for (int t = 0; t < TO; t++) {
+            oact[t] = oon[t] && os[t] * SRB12_POL_KAPPA < oz[t];
+            ozz[t] = oact[t] ? oz[t] : 0.0;
         }
+        SYNC();
         for (int v = tid; v < nv; v += 64) L.xsv[v] = L.Z[v];
         bool accepted = false;
 #pragma clang loop unroll(disable)
@@ -823,76 +923,85 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             for (int pit = 0; pit < SRB12_POL_IT; pit++) {
                 // gradient (column 1 of the right-hand side) and, for the pass's factor, the Hessian blocks
                 SYNC();
-                for (int e = tid; e < 12 * N; e += 64) {
-                    const int k = e / 12, i = e - 12 * k;
-                    const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
-                    L.gX[13 * k + i] = w * (X[e] - L.xr[e]);
-                    L.gU[e] = prm.r[i % 3] * U[e];
-                }
-                for (int k = tid; k < N; k += 64) L.gX[13 * k + 12] = 0.0;
-                if (pit == 0) {
-                    for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
-                    for (int e = tid; e < 24 * N; e += 64) L.Rh[e] = 0.0;
-                }
+                grad_f(L.gX, L.gU);
+                if (pit == 0) for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
                 if (tid == 0) { L.sc[3] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }
                 SYNC();
 #pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    const int id = lane + 64 * t;
-                    double g, h, c0, c1, c2; int kind;
-                    row_g(id, g, h, c0, c1, c2, kind);
-                    cr[t] = g - h;
-                    if (!pact[t]) continue;
-                    const double y = fma(SRB12_POL_RHO, cr[t], za[t]), om = SRB12_POL_RHO;
-                    if (kind == 1) {
-                        const int k = id / 24, l = (id / 6) & 3;
-                        double *gu = L.gU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+                for (int t = 0; t < TL; t++) {
+                    const int e = lane + 64 * t;
+                    if (e >= NL) continue;
+                    double gz[3] = {0.0, 0.0, 0.0}, rh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
+                    const double *u = U + 3 * (lon[t] ? e : 0);
+#pragma unroll
+                    for (int q = 0; q < 6; q++) {
+                        double c0, c1, c2;
+                        fric_coef(q, mus, c0, c1, c2);
+                        lcr[t][q] = c0 * u[0] + c1 * u[1] + c2 * u[2] - ((q == 5) ? prm.fmax : 0.0);
+                        if (!lact[t][q]) continue;
+                        const double y = fma(SRB12_POL_RHO, lcr[t][q], lza_[t][q]);
                         const double cc[3] = {c0, c1, c2};
-                        for (int a = 0; a < 3; a++)
-                            if (cc[a] != 0.0) __hip_atomic_fetch_add(&gu[a], y * cc[a], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (pit == 0)
-                            for (int a = 0; a < 3; a++)
-                                for (int b = a; b < 3; b++)
-                                    if (cc[a] != 0.0 && cc[b] != 0.0)
-                                        __hip_atomic_fetch_add(&rh[sym3(a, b)], om * cc[a] * cc[b], __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    } else {
-                        const int k = (id - nf) / K;
-                        double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
-                        __hip_atomic_fetch_add(&gx[0], y * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_add(&gx[1], y * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_add(&gx[12], -y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        if (pit == 0) {
-                            __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                            __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+#pragma unroll
+                        for (int a = 0; a < 3; a++) {
+                            gz[a] = fma(y, cc[a], gz[a]);
+#pragma unroll
+                            for (int b = a; b < 3; b++) rh[sym3(a, b)] = fma(SRB12_POL_RHO * cc[a], cc[b], rh[sym3(a, b)]);
                         }
+                    }
+                    if (lon[t]) { double *gu = L.gU + 3 * e; gu[0] += gz[0]; gu[1] += gz[1]; gu[2] += gz[2]; }
+                    if (pit == 0)
+#pragma unroll
+                        for (int m = 0; m < 6; m++) L.Rh[6 * e + m] = rh[m];
+                }
+#pragma unroll
+                for (int t = 0; t < TO; t++) {
+                    if (!oon[t]) continue;
+                    const int e = lane + 64 * t;
+                    double g, h, c0, c1;
+                    obs_row(e, g, h, c0, c1);
+                    ocr[t] = g - h;
+                    if (!oact[t]) continue;
+                    const double y = fma(SRB12_POL_RHO, ocr[t], ozz[t]), om = SRB12_POL_RHO;
+                    const int k = e / K;
+                    double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
+                    __hip_atomic_fetch_add(&gx[0], y * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&gx[1], y * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    __hip_atomic_fetch_add(&gx[12], -y, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                    if (pit == 0) {
+                        __hip_atomic_fetch_add(&q3[0], fma(om * c0, c0, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&q3[1], om * c0 * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&q3[2], fma(om * c1, c1, -2.0 * y), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                        __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
                 SYNC();
                 if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
                 riccati_solve(1, false);                                    // d = -H^-1 grad (column 1)
                 // multipliers z_A += RHO (c_A + J_A d) at the linearisation point; then x += d
-                double mdx = 0.0;
 #pragma unroll
-                for (int t = 0; t < TS; t++) {
-                    const int id = lane + 64 * t;
-                    double g, h, c0, c1, c2; int kind;
-                    row_g(id, g, h, c0, c1, c2, kind);
-                    if (!pact[t]) continue;
-                    double jd;
-                    if (kind == 1) {
-                        const int k = id / 24, l = (id / 6) & 3;
-                        const double *du = L.dU + 12 * k + 3 * l;
-                        jd = c0 * du[0] + c1 * du[1] + c2 * du[2];
-                    } else {
-                        const double *dx = L.dX + 13 * ((id - nf) / K);
-                        jd = c0 * dx[0] + c1 * dx[1] - dx[12];
+                for (int t = 0; t < TL; t++) {
+                    if (!lon[t]) continue;
+                    const double *du = L.dU + 3 * (lane + 64 * t);
+#pragma unroll
+                    for (int q = 0; q < 6; q++) {
+                        if (!lact[t][q]) continue;
+                        double c0, c1, c2;
+                        fric_coef(q, mus, c0, c1, c2);
+                        lza_[t][q] = fma(SRB12_POL_RHO, lcr[t][q] + c0 * du[0] + c1 * du[1] + c2 * du[2], lza_[t][q]);
                     }
-                    za[t] = fma(SRB12_POL_RHO, cr[t] + jd, za[t]);
                 }
+#pragma unroll
+                for (int t = 0; t < TO; t++) {
+                    if (!oact[t]) continue;
+                    const int e = lane + 64 * t;
+                    double g, h, c0, c1;
+                    obs_row(e, g, h, c0, c1);
+                    const double *dx = L.dX + 13 * (e / K);
+                    ozz[t] = fma(SRB12_POL_RHO, ocr[t] + c0 * dx[0] + c1 * dx[1] - dx[12], ozz[t]);
+                }
+                double mdx = 0.0;
                 const double dsv = L.dX[12];
                 SYNC();
                 for (int e = tid; e < 12 * N; e += 64) {
@@ -910,13 +1019,26 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // acceptance at the polished point
             double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0;
 #pragma unroll
-            for (int t = 0; t < TS; t++) {
-                double g, h, c0, c1, c2; int kind;
-                row_g(lane + 64 * t, g, h, c0, c1, c2, kind);
-                cr[t] = g - h;
-                if (!kind) continue;
-                pv = fmax(pv, cr[t]);
-                if (pact[t]) { cv = fmax(cv, fabs(cr[t])); nzmin = fmax(nzmin, -za[t]); zm = fmax(zm, fabs(za[t])); }
+            for (int t = 0; t < TL; t++) {
+                if (!lon[t]) continue;
+                const double *u = U + 3 * (lane + 64 * t);
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    double c0, c1, c2;
+                    fric_coef(q, mus, c0, c1, c2);
+                    lcr[t][q] = c0 * u[0] + c1 * u[1] + c2 * u[2] - ((q == 5) ? prm.fmax : 0.0);
+                    pv = fmax(pv, lcr[t][q]);
+                    if (lact[t][q]) { cv = fmax(cv, fabs(lcr[t][q])); nzmin = fmax(nzmin, -lza_[t][q]); zm = fmax(zm, fabs(lza_[t][q])); }
+                }
+            }
+#pragma unroll
+            for (int t = 0; t < TO; t++) {
+                if (!oon[t]) continue;
+                double g, h, c0, c1;
+                obs_row(lane + 64 * t, g, h, c0, c1);
+                ocr[t] = g - h;
+                pv = fmax(pv, ocr[t]);
+                if (oact[t]) { cv = fmax(cv, fabs(ocr[t])); nzmin = fmax(nzmin, -ozz[t]); zm = fmax(zm, fabs(ozz[t])); }
             }
             {
                 double rv[4] = {pv, cv, nzmin, zm};
@@ -927,24 +1049,35 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 accepted = true;
                 break;
             }
-            // next pass: the most negative multiplier leaves (lowest row on ties, the oracle's row order),
-            // violated rows join (multiplier 0), the others keep max(z_A, 0)
+            // next pass: the most negative multiplier leaves (lowest row on ties, the oracle's row order:
+            // friction 6 leg + q, then obstacles 24 N + e), violated rows join (multiplier 0), the others
+            // keep max(z_A, 0)
             double wd = -1e-9 * zm;
             int wk = 0x7fffffff;
 #pragma unroll
-            for (int t = 0; t < TS; t++)
-                if (pact[t] && za[t] < wd) lexmin(wd, wk, za[t], lane + 64 * t);
+            for (int t = 0; t < TL; t++)
+#pragma unroll
+                for (int q = 0; q < 6; q++)
+                    if (lact[t][q] && lza_[t][q] < wd) lexmin(wd, wk, lza_[t][q], 6 * (lane + 64 * t) + q);
+#pragma unroll
+            for (int t = 0; t < TO; t++)
+                if (oact[t] && ozz[t] < wd) lexmin(wd, wk, ozz[t], 24 * N + lane + 64 * t);
             if (wk == 0x7fffffff) wd = 1e300;
             wargmin(wd, wk);
             bool changed = wk != 0x7fffffff;
 #pragma unroll
-            for (int t = 0; t < TS; t++) {
-                const int id = lane + 64 * t;
-                double g, h, c0, c1, c2; int kind;
-                row_g(id, g, h, c0, c1, c2, kind);
-                if (id == wk) pact[t] = false;
-                else if (kind && !pact[t] && cr[t] > SRB12_POL_PTOL) { pact[t] = true; changed = true; }
-                za[t] = pact[t] ? fmax(za[t], 0.0) : 0.0;
+            for (int t = 0; t < TL; t++)
+#pragma unroll
+                for (int q = 0; q < 6; q++) {
+                    if (6 * (lane + 64 * t) + q == wk) lact[t][q] = false;
+                    else if (lon[t] && !lact[t][q] && lcr[t][q] > SRB12_POL_PTOL) { lact[t][q] = true; changed = true; }
+                    lza_[t][q] = lact[t][q] ? fmax(lza_[t][q], 0.0) : 0.0;
+                }
+#pragma unroll
+            for (int t = 0; t < TO; t++) {
+                if (24 * N + lane + 64 * t == wk) oact[t] = false;
+                else if (oon[t] && !oact[t] && ocr[t] > SRB12_POL_PTOL) { oact[t] = true; changed = true; }
+                ozz[t] = oact[t] ? fmax(ozz[t], 0.0) : 0.0;
             }
             if (!__builtin_amdgcn_ballot_w64(changed)) break;
         }
@@ -973,8 +1106,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     }
 }
 
-#define SRB12_KERNEL(TS)                                                                                        \
-    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TS(                                         \
+#define SRB12_KERNEL(TL, TO)                                                                                    \
+    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TL##_##TO(                                  \
         Srb12KParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ xrefg,        \
         const double *__restrict__ footg, const int *__restrict__ contactg, const double *__restrict__ obstacles, \
         const double *__restrict__ nbr_state, const int *__restrict__ sel_g, double *__restrict__ x_qp_out,      \
@@ -984,13 +1117,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        srb12_agent<TS>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out, x_out, \
-                        obj_out, status_out, iters_out, lds);                                                  \
+        srb12_agent<TL, TO>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out,     \
+                            x_out, obj_out, status_out, iters_out, lds);                                       \
     }
-SRB12_KERNEL(4)
-SRB12_KERNEL(6)
-SRB12_KERNEL(8)
-SRB12_KERNEL(12)
+SRB12_INSTANCES(SRB12_KERNEL)
 
 // CoM rows [x, xdot, y, ydot] of a 12-state batch: the layout the shared selection kernel
 // (srb_knn_kernel) reads its query points from

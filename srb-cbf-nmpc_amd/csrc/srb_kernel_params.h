@@ -172,17 +172,20 @@ struct Srb12KParams {
 #define SRB12_POL_PASSES 2
 #define SRB12_POL_PTOL 1e-9
 #define SRB12_POL_DXTOL 1e-7
-// row slots: 6 friction rows per (grid, leg) -- masked for swing legs -- then N K obstacle rows
-static inline int srb12_slots(int N, int K) { return 24 * N + N * K; }
+// kernel instances (TL, TO): leg-slot trips (4N legs over 64 lanes) and obstacle-slot trips (N K rows)
+#define SRB12_INSTANCES(X) X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(1, 12) X(2, 4) X(2, 8) X(2, 12)
+static inline int srb12_leg_trips(int N) { return (4 * N + 63) / 64; }
+static inline int srb12_obs_trips(int N, int K) { return (N * K + 63) / 64 > 0 ? (N * K + 63) / 64 : 1; }
 // doubles of LDS one agent needs (the carve in srb12_kernels.hip)
 static inline int srb12_lds_doubles(int N, int K)
 {
-    return 36 * N + 2 * N + 4 * N + 78 * N + 156 * N      // W_l, (cos, sin) psi, contact, Z (packed), Hux per grid
-           + 169 + 169 + 156                            // V, G, F (Y reuses F)
+    return 36 * N + 2 * N + 4 * N                        // W_l, (cos, sin) psi, contact
+           + 156 * N + 78 * N                           // K_k, Hu_k^-1 (packed) per grid
+           + 300                                        // factor transposes
            + 6 * N + 24 * N                             // (p_x, p_y, s) blocks, force blocks
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
-           + 2 * 13 * N + 2 * 12 * N + 13 * N + 12 * N + 12 * N   // rhs columns (solve, refinement / gradients), solution, gu
+           + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)
+           + 13 * N + 12 * N + 12 * N                   // solution, feed-forward -Hu^-1 gu
            + 16 + 16                                    // vector, scalars
-           + 2 * N * K + K + (24 * N + 1)               // obstacle positions, eps, the saved iterate (polish)
-           + K + 2;                                     // sel (as ints)
+           + 2 * N * K + K + K + 2;                     // obstacle positions, eps, sel (as ints)
 }
