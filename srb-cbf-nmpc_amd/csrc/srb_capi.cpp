@@ -115,7 +115,7 @@ struct srb_ctx {
     int qp_init;                   // QP starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT
     // srb_ctx_set_option (SRB_OPT_*): the polish of the NLP result on/off, its penalty and waves per
     // agent, the selection-grid thresholds
-    int polish, polish_waves, grid_min_rows, grid_min_rows_static;
+    int polish, polish_waves, grid_min_rows, grid_min_rows_static, polish_fused;
     double polish_rho;
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
@@ -305,7 +305,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
-    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -433,9 +433,12 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
         if (rc) return rc;
     }
     HIPCHK(hipEventRecord(c->ev[2], s));
-    // the solve kernel, then (NLP stage) the active-set polish of its result (srb_polish_kernel,
-    // same instance geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
-    const bool polish = use_nlp && c->polish;
+    // the solve kernel, then (NLP stage) the active-set polish of its result: fused into the solve
+    // kernel's end (SRB_OPT_POLISH_FUSED, instances up to NZL 16), else srb_polish_kernel (same instance
+    // geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
+    const bool fused = use_nlp && c->polish && c->polish_fused && SRB_FUSED_POLISH_OK(in->nzl);
+    const bool polish = use_nlp && c->polish && !fused;
+    k.polish_fused = fused ? 1 : 0;
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
@@ -485,6 +488,9 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
     case SRB_OPT_POLISH_WAVES:
         if (v != 0.0 && v != 1.0 && v != 2.0 && v != 4.0) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH_WAVES: 0 (automatic), 1, 2 or 4");
         c->polish_waves = (int)v; return SRB_OK;
+    case SRB_OPT_POLISH_FUSED:
+        if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH_FUSED: 0 or 1");
+        c->polish_fused = (int)v; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS:
     case SRB_OPT_GRID_MIN_ROWS_STATIC:
         if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
@@ -504,6 +510,7 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_POLISH_WAVES: *v = c->polish_waves; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS: *v = c->grid_min_rows; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS_STATIC: *v = c->grid_min_rows_static; return SRB_OK;
+    case SRB_OPT_POLISH_FUSED: *v = c->polish_fused; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }

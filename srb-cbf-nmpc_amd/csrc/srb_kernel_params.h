@@ -40,6 +40,9 @@
 #ifndef SRB_POLISH_ON
 #define SRB_POLISH_ON 1
 #endif
+// instances whose solve kernel carries the fused polish (srb_kernels.hip; srb_capi.cpp launches the
+// polish kernel for the others)
+#define SRB_FUSED_POLISH_OK(NZL) ((NZL) <= 16)
 
 // diagnostic trace buffer of the nlpdbg build (srb_kernels.hip, srb_capi.cpp)
 #define SRB_NLP_DBG_LEN (8 * 64 + 32 * 32 + 32 + 1024 + 256 + 3 * 256)
@@ -67,7 +70,8 @@ struct SrbKParams {
     int n, nz, mq, use_nlp;
     int qp_maxit, nlp_maxit;
     int qp_init;                           // QP starting point: 1 scaled (s = max(h - Gx, 0.1), z = 1/s), 0 iSWIFT's kkt_initialize
-    double polish_rho;                     // SRB_POLISH_RHO (SRB_POLISH_RHO env override: tuning runs only)
+    int polish_fused;                      // 1: the polish runs at the end of the solve kernel (no polish kernel)
+    double polish_rho;                     // SRB_POLISH_RHO (SRB_OPT_POLISH_RHO)
     double Ad[16], Bd[8];                  // LIP discretisation (MPC_dist.cpp:126-127)
     double Qw, Pw, Rw, Sw, box, fr;        // gains (:172-175), box (:317), mu*h/sqrt(2) (:315)
     double eps_obs, eps_nbr, vsat, tol, Ts;
@@ -123,7 +127,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
     return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
-           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part
+           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + srb_r4(srb_slots(N, C, K))
 #ifdef SRB_STAMPS
            + 64
 #endif

@@ -667,6 +667,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     int *sel = (int *)p; p += (K + 1); \
     double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
     double *part = p; p += (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs (NW = 4) */ \
+    float *zpl = (float *)p; p += rnd4(S);        /* fused polish: the exported active set (2 floats a slot) */ \
     do {} while (0)
 
 #define SRB_AGENT_SETUP \
@@ -773,6 +774,148 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
         for (int i = 1; i < 5; i++) acc = fma(prm.Binv[5 * j + i], xs[4 * (i - 1) + d], acc); \
         alpha_out[(size_t)agent * 20 + 5 * d + j] = acc; \
     } \
+    do {} while (0)
+
+// The passes of the active-set polish (polish_agent, and the fused polish at the end of nmpc_agent):
+// PS[t] holds each slot's active mask (ds), multiplier z_A (dz) and the inactive rows' proximal weight
+// (s); xs the interior-point result, also saved in xsv.  Sets `accepted`.
+#define SRB_POLISH_PASSES_LOOP(PS)                                                                                                            \
+_Pragma("clang loop unroll(disable)")                                                                                                         \
+    for (int pass = 0; pass < SRB_POLISH_PASSES; pass++) {                                                                                    \
+        bool bad = false;                                                                                                                     \
+        double lastdx = 1e300;                                                                                                                \
+_Pragma("clang loop unroll(disable)")                                                                                                         \
+        for (int pit = 0; pit < SRB_POLISH_IT; pit++) {                                                                                       \
+            SYNC(); /* xs of the previous step / pass */                                                                                      \
+            polish_rows<NZL, TS, NW>(PS, nts, xs, OJ, zo, n, rO, R, nz); /* q.jd = g(x), M_o (OJ), zo = z_A */                                \
+            SYNC(); /* R rows, zo */                                                                                                          \
+            if (pit > 0) { /* converged after a small step (oracle, same rule) */                                                             \
+                double cm = 0.0;                                                                                                              \
+_Pragma("unroll")                                                                                                                             \
+                for (int t = 0; t < TS; t++)                                                                                                  \
+                    if (t < nts) {                                                                                                            \
+                        const Slot &q = PS[t];                                                                                                \
+                        cm = fmax(cm, fmax(q.ds[0] * fabs(q.jd - q.h[0]), q.ds[1] * fabs(q.jd + q.h[1])));                                    \
+                    }                                                                                                                         \
+                double rv[1] = {cm};                                                                                                          \
+                wred_x<1, 1u, NW>(rv, red + 6 * 8 * NW, tid);                                                                                 \
+                if (lastdx <= SRB_POLISH_DX1 && rv[0] <= SRB_POLISH_CTOL) { lastdx = 0.0; break; }                                            \
+            }                                                                                                                                 \
+_Pragma("unroll")                                                                                                                             \
+            for (int t = 0; t < TS; t++)                                                                                                      \
+                if (t < nts) {                                                                                                                \
+                    Slot &q = PS[t];                                                                                                          \
+                    q.r3[0] = q.jd - q.h[0]; q.r3[1] = -q.jd - q.h[1];                                                                        \
+                    const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);     \
+                    const double wa = (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]);                \
+                    if (kind_of(q) == K_VAR) {                                                                                                \
+                        double hs = 0.0;                                                                                                      \
+                        if (q.i0 < 4 * N && !(q.i0 & 1)) hs = -2.0 * zo_sum(zo, q.i0 >> 2, K);                                                \
+                        W[q.wr] = q.a0 + hs + wa;                                                                                             \
+                        CF[q.wr] = -(fma(q.a0, q.jd, q.a1) + cfa);                                                                            \
+                    } else {                                                                                                                  \
+                        W[q.wr] = wa; /* COP / OBS rows (VEL: the scratch entry) */                                                           \
+                        CF[q.wr] = -cfa;                                                                                                      \
+                    }                                                                                                                         \
+                }                                                                                                                             \
+            if (NW > 1) SYNC(); /* the VAR rows' plain stores land before the VEL adds */                                                     \
+_Pragma("unroll")                                                                                                                             \
+            for (int t = 0; t < TS; t++)                                                                                                      \
+                if (t < nts && kind_of(PS[t]) == K_VEL) {                                                                                     \
+                    const Slot &q = PS[t];                                                                                                    \
+                    const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);     \
+                    __hip_atomic_fetch_add(&W[q.r], (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]),  \
+                                           __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);                                                   \
+                    __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);                                   \
+                }                                                                                                                             \
+            SYNC();                                                                                                                           \
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);                                                    \
+            SYNC();                                                                                                                           \
+            if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);                                                                           \
+            gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
+            if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; } /* not PD: reject */                                            \
+            la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);                                                                    \
+            double mdx = 0.0;                                                                                                                 \
+_Pragma("unroll")                                                                                                                             \
+            for (int t = 0; t < TS; t++)                                                                                                      \
+                if (t < nts) {                                                                                                                \
+                    Slot &q = PS[t];                                                                                                          \
+                    const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) /* J_o Z dxi, M_o generated (gram_rhs) */                 \
+                        ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),                                                          \
+                              fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))     \
+                        : row_dot<NZL>(R + q.r * LDR, dxi);                                                                                   \
+                    q.dz[0] = fma(q.ds[0] * prm.polish_rho, q.r3[0] + jd, q.dz[0]);                                                           \
+                    q.dz[1] = fma(q.ds[1] * prm.polish_rho, q.r3[1] - jd, q.dz[1]);                                                           \
+                    if (kind_of(q) == K_VAR) {                                                                                                \
+                        xs[q.i0] = q.jd + jd; /* every read of xs this step is behind a barrier */                                            \
+                        mdx = fmax(mdx, fabs(jd));                                                                                            \
+                    }                                                                                                                         \
+                }                                                                                                                             \
+            {                                                                                                                                 \
+                double rv[1] = {mdx};                                                                                                         \
+                wred_x<1, 1u, NW>(rv, red + 8 * 8 * NW, tid);                                                                                 \
+                lastdx = rv[0];                                                                                                               \
+            }                                                                                                                                 \
+            POLDBG(4 + pass, pit, lastdx);                                                                                                    \
+            POLDBG_X(pass, pit, xs, n);                                                                                                       \
+            if (lastdx <= SRB_POLISH_DXTOL) break; /* converged: no further step */                                                           \
+        }                                                                                                                                     \
+        if (bad) break;                                                                                                                       \
+        SYNC();                                                                                                                               \
+ /* ---- acceptance at the polished point */                                                                                                  \
+        double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0, vi = -1e300;                                                                  \
+        {                                                                                                                                     \
+            const double s_var = xs[n - 1];                                                                                                   \
+_Pragma("unroll")                                                                                                                             \
+            for (int t = 0; t < TS; t++)                                                                                                      \
+                if (t < nts) {                                                                                                                \
+                    Slot &q = PS[t];                                                                                                          \
+                    const double fq = slot_f(q, xs, s_var);                                                                                   \
+_Pragma("unroll")                                                                                                                             \
+                    for (int r = 0; r < 2; r++) {                                                                                             \
+                        const double v = r ? -fq - q.h[1] : fq - q.h[0];                                                                      \
+                        q.r3[r] = v;                                                                                                          \
+                        if (q.m[r] != 0.0) pv = fmax(pv, v);                                                                                  \
+                        if (q.ds[r] != 0.0) { cv = fmax(cv, fabs(v)); nzmin = fmax(nzmin, -q.dz[r]); zm = fmax(zm, fabs(q.dz[r])); }          \
+                        else if (q.m[r] != 0.0) vi = fmax(vi, v);                                                                             \
+                    }                                                                                                                         \
+                }                                                                                                                             \
+            double rv[5] = {pv, cv, nzmin, zm, vi};                                                                                           \
+            wred_x<5, 0x1Fu, NW>(rv, red + 7 * 8 * NW, tid);                                                                                  \
+            pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4];                                                                    \
+        }                                                                                                                                     \
+        POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);                           \
+        POLDBG(pass, 5, lastdx);                                                                                                              \
+        if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL) {                             \
+            POLDBG(pass, 6, 1.0);                                                                                                             \
+            accepted = true;                                                                                                                  \
+            break;                                                                                                                            \
+        }                                                                                                                                     \
+ /* next pass: the most negative multiplier leaves A, violated rows join; the rows */                                                         \
+ /* that stay keep their multipliers (>= 0), the new ones start at 0 */                                                                       \
+        double wd = 1e300;                                                                                                                    \
+        int wk = 0x7fffffff;                                                                                                                  \
+_Pragma("unroll")                                                                                                                             \
+        for (int t = 0; t < TS; t++)                                                                                                          \
+            if (t < nts)                                                                                                                      \
+_Pragma("unroll")                                                                                                                             \
+                for (int r = 0; r < 2; r++)                                                                                                   \
+                    if (PS[t].ds[r] != 0.0 && PS[t].dz[r] < -1e-9 * zm) lexmin(wd, wk, PS[t].dz[r], 2 * (tid + NTH * t) + r);                 \
+        wargmin_x<NW>(wd, wk, red + 9 * 8 * NW, tid);                                                                                         \
+        if (wk == 0x7fffffff && !(vi > SRB_POLISH_PTOL)) break; /* nothing to change: rejected */                                             \
+_Pragma("unroll")                                                                                                                             \
+        for (int t = 0; t < TS; t++) {                                                                                                        \
+            Slot &q = PS[t];                                                                                                                  \
+_Pragma("unroll")                                                                                                                             \
+            for (int r = 0; r < 2; r++) {                                                                                                     \
+                if (2 * (tid + NTH * t) + r == wk) q.ds[r] = 0.0;                                                                             \
+                else if (t < nts && q.ds[r] == 0.0 && q.m[r] != 0.0 && q.r3[r] > SRB_POLISH_PTOL) q.ds[r] = 1.0;                              \
+                q.dz[r] = q.ds[r] * fmax(q.dz[r], 0.0);                                                                                       \
+            }                                                                                                                                 \
+        }                                                                                                                                     \
+        SYNC();                                                                                                                               \
+        for (int v = tid; v < n; v += NTH) xs[v] = xsv[v]; /* the next pass starts from the interior-point result */                          \
+    }                                                                                                                                         \
     do {} while (0)
 
 // --------------------------------------------------------------------------- main kernel
@@ -1013,7 +1156,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
         // (the saved one on a restore)
         auto export_zpol = [&]() {
-            float *zp = zpol_g + (size_t)agent * zstride;
+            float *zp = prm.polish_fused ? zpl : zpol_g + (size_t)agent * zstride;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts && tid + NTH * t < S)
@@ -1098,7 +1241,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             if (near && nrx / gm <= best_rx) {     // each thread copies the variables it owns
                 best_rx = nrx / gm;
                 for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
-                if (zpol_g) export_zpol();
+                if (zpol_g || prm.polish_fused) export_zpol();
                 saved = true;
             }
             if (near && ++npassed >= SRB_NLP_NEARWAIT) { flag = 4; break; }
@@ -1318,7 +1461,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         if (nl && saved && !prov && (restore || flag == 2 || flag == 4)) {      // ACCEPTABLE / MAXIT: the best saved iterate
             for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];     // owner threads, as saved
             flag = 4;                                               // (zpol_g: exported at the save)
-        } else if (zpol_g && nl) {
+        } else if ((zpol_g || prm.polish_fused) && nl) {
             export_zpol();
         }
         if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
@@ -1326,6 +1469,35 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     SYNC();
     if (x_qp_out && nstage == 1)
         for (int v = tid; v < n; v += NTH) x_qp_out[(size_t)agent * n + v] = xs[v];
+    // ---- fused active-set polish (prm.polish_fused; otherwise srb_polish_kernel runs next): the same
+    // passes on the LDS state the NLP stage left (term rows, iterate) with the interior-point slots
+    // reused as the polish's (their state is dead here), so an agent that finishes early polishes on
+    // its own SIMD while slower agents still iterate, and nothing goes through HBM.  Compiled for the
+    // instances up to NZL 16 only: in the N = 20 ones (NZL 24) it raised the loop's spills 71 -> 123
+    if constexpr (SRB_FUSED_POLISH_OK(NZL))
+    if (prm.polish_fused && prm.use_nlp && nlp_flag != 1 && nlp_flag != 3) {
+        const int nts = (S + NTH - 1) / NTH;
+        const int cnt = rO, nko = NKP;
+        for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
+#pragma unroll
+        for (int t = 0; t < TS; t++) {
+            const int sl = tid + NTH * t;
+#pragma unroll
+            for (int r = 0; r < 2; r++) {
+                const double v = (t < nts && sl < S) ? (double)zpl[2 * sl + r] : 0.0;
+                Q[t].ds[r] = (v > 0.0) ? 1.0 : 0.0;
+                Q[t].dz[r] = fmax(v, 0.0);
+                Q[t].s[r] = fmax(-v, 0.0);
+            }
+        }
+        bool accepted = false;
+        SRB_POLISH_PASSES_LOOP(Q);
+        SYNC();
+        if (accepted) nlp_flag = 0;
+        else
+            for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];
+        SYNC();
+    }
 
     // ---- outputs: x, objective (ExCost::GetCost, dec_vars_constr_cost.h:423-438), alpha_COM
     SRB_AGENT_OUTPUTS;
@@ -1337,6 +1509,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         iters_out[2 * agent] = qp_it; iters_out[2 * agent + 1] = nlp_it;
     }
 }
+
 
 // --------------------------------------------------------------------------- polish kernel
 // Launched right after the solve kernel on the same stream, same instance geometry.  It rebuilds
@@ -1411,142 +1584,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             }
         }
         bool accepted = false;
-#pragma clang loop unroll(disable)
-        for (int pass = 0; pass < SRB_POLISH_PASSES; pass++) {
-            bool bad = false;
-            double lastdx = 1e300;
-#pragma clang loop unroll(disable)
-            for (int pit = 0; pit < SRB_POLISH_IT; pit++) {
-                SYNC();                                      // xs of the previous step / pass
-                polish_rows<NZL, TS, NW>(P, nts, xs, OJ, zo, n, rO, R, nz);      // q.jd = g(x), M_o (OJ), zo = z_A
-                SYNC();                                      // R rows, zo
-                if (pit > 0) {                               // converged after a small step (oracle, same rule)
-                    double cm = 0.0;
-#pragma unroll
-                    for (int t = 0; t < TS; t++)
-                        if (t < nts) {
-                            const Slot &q = P[t];
-                            cm = fmax(cm, fmax(q.ds[0] * fabs(q.jd - q.h[0]), q.ds[1] * fabs(q.jd + q.h[1])));
-                        }
-                    double rv[1] = {cm};
-                    wred_x<1, 1u, NW>(rv, red + 6 * 8 * NW, tid);
-                    if (lastdx <= SRB_POLISH_DX1 && rv[0] <= SRB_POLISH_CTOL) { lastdx = 0.0; break; }
-                }
-#pragma unroll
-                for (int t = 0; t < TS; t++)
-                    if (t < nts) {
-                        Slot &q = P[t];
-                        q.r3[0] = q.jd - q.h[0]; q.r3[1] = -q.jd - q.h[1];
-                        const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
-                        const double wa = (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]);
-                        if (kind_of(q) == K_VAR) {
-                            double hs = 0.0;
-                            if (q.i0 < 4 * N && !(q.i0 & 1)) hs = -2.0 * zo_sum(zo, q.i0 >> 2, K);
-                            W[q.wr] = q.a0 + hs + wa;
-                            CF[q.wr] = -(fma(q.a0, q.jd, q.a1) + cfa);
-                        } else {
-                            W[q.wr] = wa;                    // COP / OBS rows (VEL: the scratch entry)
-                            CF[q.wr] = -cfa;
-                        }
-                    }
-                if (NW > 1) SYNC();                          // the VAR rows' plain stores land before the VEL adds
-#pragma unroll
-                for (int t = 0; t < TS; t++)
-                    if (t < nts && kind_of(P[t]) == K_VEL) {
-                        const Slot &q = P[t];
-                        const double cfa = q.ds[0] * fma(prm.polish_rho, q.r3[0], q.dz[0]) - q.ds[1] * fma(prm.polish_rho, q.r3[1], q.dz[1]);
-                        __hip_atomic_fetch_add(&W[q.r], (q.ds[0] != 0.0 ? prm.polish_rho : q.s[0]) + (q.ds[1] != 0.0 ? prm.polish_rho : q.s[1]),
-                                               __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                        __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                    }
-                SYNC();
-                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
-                SYNC();
-                if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);
-                gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
-                if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; }      // not PD: reject
-                la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
-                double mdx = 0.0;
-#pragma unroll
-                for (int t = 0; t < TS; t++)
-                    if (t < nts) {
-                        Slot &q = P[t];
-                        const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS)      // J_o Z dxi, M_o generated (gram_rhs)
-                            ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),
-                                  fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))
-                            : row_dot<NZL>(R + q.r * LDR, dxi);
-                        q.dz[0] = fma(q.ds[0] * prm.polish_rho, q.r3[0] + jd, q.dz[0]);
-                        q.dz[1] = fma(q.ds[1] * prm.polish_rho, q.r3[1] - jd, q.dz[1]);
-                        if (kind_of(q) == K_VAR) {
-                            xs[q.i0] = q.jd + jd;            // every read of xs this step is behind a barrier
-                            mdx = fmax(mdx, fabs(jd));
-                        }
-                    }
-                {
-                    double rv[1] = {mdx};
-                    wred_x<1, 1u, NW>(rv, red + 8 * 8 * NW, tid);
-                    lastdx = rv[0];
-                }
-                POLDBG(4 + pass, pit, lastdx);
-                POLDBG_X(pass, pit, xs, n);
-                if (lastdx <= SRB_POLISH_DXTOL) break;       // converged: no further step
-            }
-            if (bad) break;
-            SYNC();
-            // ---- acceptance at the polished point
-            double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0, vi = -1e300;
-            {
-                const double s_var = xs[n - 1];
-#pragma unroll
-                for (int t = 0; t < TS; t++)
-                    if (t < nts) {
-                        Slot &q = P[t];
-                        const double fq = slot_f(q, xs, s_var);
-#pragma unroll
-                        for (int r = 0; r < 2; r++) {
-                            const double v = r ? -fq - q.h[1] : fq - q.h[0];
-                            q.r3[r] = v;
-                            if (q.m[r] != 0.0) pv = fmax(pv, v);
-                            if (q.ds[r] != 0.0) { cv = fmax(cv, fabs(v)); nzmin = fmax(nzmin, -q.dz[r]); zm = fmax(zm, fabs(q.dz[r])); }
-                            else if (q.m[r] != 0.0) vi = fmax(vi, v);
-                        }
-                    }
-                double rv[5] = {pv, cv, nzmin, zm, vi};
-                wred_x<5, 0x1Fu, NW>(rv, red + 7 * 8 * NW, tid);
-                pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4];
-            }
-            POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);
-            POLDBG(pass, 5, lastdx);
-            if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL) {
-                POLDBG(pass, 6, 1.0);
-                accepted = true;
-                break;
-            }
-            // next pass: the most negative multiplier leaves A, violated rows join; the rows
-            // that stay keep their multipliers (>= 0), the new ones start at 0
-            double wd = 1e300;
-            int wk = 0x7fffffff;
-#pragma unroll
-            for (int t = 0; t < TS; t++)
-                if (t < nts)
-#pragma unroll
-                    for (int r = 0; r < 2; r++)
-                        if (P[t].ds[r] != 0.0 && P[t].dz[r] < -1e-9 * zm) lexmin(wd, wk, P[t].dz[r], 2 * (tid + NTH * t) + r);
-            wargmin_x<NW>(wd, wk, red + 9 * 8 * NW, tid);
-            if (wk == 0x7fffffff && !(vi > SRB_POLISH_PTOL)) break;      // nothing to change: rejected
-#pragma unroll
-            for (int t = 0; t < TS; t++) {
-                Slot &q = P[t];
-#pragma unroll
-                for (int r = 0; r < 2; r++) {
-                    if (2 * (tid + NTH * t) + r == wk) q.ds[r] = 0.0;
-                    else if (t < nts && q.ds[r] == 0.0 && q.m[r] != 0.0 && q.r3[r] > SRB_POLISH_PTOL) q.ds[r] = 1.0;
-                    q.dz[r] = q.ds[r] * fmax(q.dz[r], 0.0);
-                }
-            }
-            SYNC();
-            for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];   // the next pass starts from the interior-point result
-        }
+        SRB_POLISH_PASSES_LOOP(P);
         SYNC();
         if (accepted) {
             SRB_AGENT_OUTPUTS;

@@ -291,6 +291,32 @@ def test_unpolished_loosened_exit_is_acceptable_not_optimal():
     np.testing.assert_allclose(xus(N, off["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
+def test_fused_polish_equals_separate_polish_kernel():
+    """the active-set polish runs at the end of the solve kernel
+    (SRB_OPT_POLISH_FUSED = 1, default, instances up to NZL 16) instead of as srb_polish_kernel.
+    Same algorithm from the same float z snapshot, so the results agree to round-off (the two
+    kernels run at different waves per agent, so the reduction orders differ) and every status
+    is identical; both match the oracle at NLP_TOL."""
+    for (N, C, Ko, Kn, A, seed) in [(10, 2, 3, 8, 1024, 5), (10, 4, 1, 0, 256, 6)]:
+        b = workload.make_batch(A, N, C, seed=seed)
+        p = srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn)
+        s = srbnmpc.BatchSolver(p, A)
+        try:
+            assert s.get_option("polish_fused") == 1.0
+            fu = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+            s.set_option("polish_fused", 0)
+            se = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+        finally:
+            s.close()
+        np.testing.assert_array_equal(fu["status"], se["status"])
+        np.testing.assert_allclose(fu["x"], se["x"], atol=1e-8, rtol=0)
+        np.testing.assert_allclose(fu["alpha"], se["alpha"], atol=1e-8, rtol=0)
+        assert (fu["status"][:, 1] == 0).mean() >= 0.99
+        r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"][:128], b["ref"][:128],
+                               b["foot"][:128], b["obstacles"], b["nbr_state"], nthreads=8)
+        np.testing.assert_allclose(xus(N, fu["x"][:128]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+
+
 def test_config5_full_size_vs_oracle_and_acceptable_exit():
     """bench config 5 (2048 agents, N = 20, 3 static + 8 neighbour rows) at full size, EVERY
     agent within NLP_TOL (1e-4) of the oracle in X, U, s.

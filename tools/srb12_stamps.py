@@ -12,7 +12,8 @@ import numpy as np  # noqa: E402
 from srbnmpc import srb12, workload  # noqa: E402
 
 PHASES = ["inputs/model/rollout", "residuals+costates", "Riccati factor", "factor->predictor",
-          "predictor rhs+solve", "predictor step+sigma", "corrector rhs+solve", "corrector step+update"]
+          "predictor rhs+solve", "predictor step+sigma", "corrector rhs+solve", "corrector step+update",
+          "exit test->polish", "active-set polish"]
 A, N = 1024, 10
 b = workload.make_batch12(A, N, "trot", seed=0)
 s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
@@ -24,7 +25,7 @@ for ag in map(int, sys.argv[1:]):
     L.srb12_debug_trace(s._h, ag, None)
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     L.srb12_debug_trace(s._h, -1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
-    st = buf[2 * 64 * 8:2 * 64 * 8 + 8]
+    st = buf[2 * 64 * 8:2 * 64 * 8 + len(PHASES)]
     its = int(out["iters"][ag].sum())
     tot = st.sum()
     print(f"agent {ag}: iters {out['iters'][ag].tolist()}, total {tot:.0f} s_memtime cycles, "
