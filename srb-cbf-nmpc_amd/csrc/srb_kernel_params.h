@@ -127,7 +127,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
     return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
-           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + srb_r4(srb_slots(N, C, K))
+           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + (SRB_FUSED_POLISH_OK(NZL) ? srb_r4(srb_slots(N, C, K)) : 0)
 #ifdef SRB_STAMPS
            + 64
 #endif

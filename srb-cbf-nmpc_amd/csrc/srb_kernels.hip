@@ -667,7 +667,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     int *sel = (int *)p; p += (K + 1); \
     double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
     double *part = p; p += (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs (NW = 4) */ \
-    float *zpl = (float *)p; p += rnd4(S);        /* fused polish: the exported active set (2 floats a slot) */ \
+    float *zpl = (float *)p; p += SRB_FUSED_POLISH_OK(NZL) ? rnd4(S) : 0;   /* fused polish: the exported active set (2 floats a slot) */ \
     do {} while (0)
 
 #define SRB_AGENT_SETUP \
@@ -953,6 +953,12 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     double dxi[NZL];                                         // Newton direction in xi (uniform)
 #pragma unroll
     for (int j = 0; j < NZL; j++) { Mi[j] = (mrow<NZL>(lane) == j) ? 1.0 : 0.0; dxi[j] = 0.0; }
+    // LEAN (the N = 20 instances, NZL 24): 1/z, 1/s, dsT and r3 are recomputed where they are used
+    // instead of held per slot across the Newton solve (16 VGPRs a slot, 64 at TS = 4: the loop's
+    // spills); the same expressions in the same order, so the results are bit-identical
+    constexpr bool LEAN = NZL > 16;
+    auto IZ = [&](const Slot &q, int r) -> double { if constexpr (LEAN) return rcp_d(q.z[r]); else return q.iz[r]; };
+    auto IS = [&](const Slot &q, int r) -> double { if constexpr (LEAN) return rcp_d(q.s[r]); else return q.is[r]; };
     SYNC();
     STAMP_END(0);
 
@@ -1156,7 +1162,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
         // (the saved one on a restore)
         auto export_zpol = [&]() {
-            float *zp = prm.polish_fused ? zpl : zpol_g + (size_t)agent * zstride;
+            float *zp = (SRB_FUSED_POLISH_OK(NZL) && prm.polish_fused) ? zpl : zpol_g + (size_t)agent * zstride;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts && tid + NTH * t < S)
@@ -1187,8 +1193,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     nrz = fma(q.m[0] * rz0, rz0, fma(q.m[1] * rz1, rz1, nrz));
                     sz = fma(q.m[0] * q.s[0], q.z[0], fma(q.m[1] * q.s[1], q.z[1], sz));
                     zmx = fmax(zmx, fmax(q.m[0] * q.z[0], q.m[1] * q.z[1]));
+                    if constexpr (!LEAN)
 #pragma unroll
-                    for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
+                        for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
                     if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z (gram_rhs)
                         const int o = q.r - rO;
                         obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
@@ -1266,10 +1273,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             double dsT = -q.s[r] * q.z[r];
                             if (corr) dsT -= q.ds[r] * q.dz[r];
                             dsT += smu;
-                            q.dsT[r] = dsT;
                             const double rz = r ? (q.h[1] - q.s[1] + f) : (q.h[0] - q.s[0] - f);
-                            q.r3[r] = fma(-dsT, q.iz[r], rz);
-                            cf = fma((r ? -q.m[1] : q.m[0]) * q.z[r] * q.is[r], q.r3[r], cf);
+                            const double r3 = fma(-dsT, IZ(q, r), rz);
+                            if constexpr (!LEAN) { q.dsT[r] = dsT; q.r3[r] = r3; }
+                            cf = fma((r ? -q.m[1] : q.m[0]) * q.z[r] * IS(q, r), r3, cf);
                         }
                         cfs[t] = cf;
                         CF[q.wr] = cf;
@@ -1291,7 +1298,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        const double om = fma(q.m[0] * q.z[0], q.is[0], q.m[1] * q.z[1] * q.is[1]);
+                        const double om = fma(q.m[0] * q.z[0], IS(q, 0), q.m[1] * q.z[1] * IS(q, 1));
                         double hs = 0.0;
                         if (nl && kind_of(q) == K_VAR && q.i0 < 4 * N && !(q.i0 & 1)) {
                             const int k = q.i0 >> 2;
@@ -1305,7 +1312,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 #pragma unroll
                     for (int t = 0; t < TS; t++)
                         if (t < nts && kind_of(Q[t]) == K_VEL)
-                            __hip_atomic_fetch_add(&W[Q[t].r], Q[t].z[0] * Q[t].is[0] + Q[t].z[1] * Q[t].is[1], __ATOMIC_RELAXED,
+                            __hip_atomic_fetch_add(&W[Q[t].r], Q[t].z[0] * IS(Q[t], 0) + Q[t].z[1] * IS(Q[t], 1), __ATOMIC_RELAXED,
                                                    __HIP_MEMORY_SCOPE_WORKGROUP);
                 STAMP_END(16);
                 set_rhs(0);
@@ -1367,9 +1374,20 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         }
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
-                            q.dz[r] = q.m[r] * q.z[r] * q.is[r] * fma(r ? -1.0 : 1.0, q.jd, -q.r3[r]);
-                            q.ds[r] = q.m[r] * fma(-q.s[r], q.dz[r], q.dsT[r]) * q.iz[r];
-                            mxs = fmax(mxs, -q.ds[r] * q.is[r]); mxz = fmax(mxz, -q.dz[r] * q.iz[r]);
+                            const double izr = IZ(q, r), isr = IS(q, r);
+                            double dsT, r3;
+                            if constexpr (LEAN) {                    // set_rhs(pass)'s terms, recomputed
+                                dsT = -q.s[r] * q.z[r];
+                                if (pass == 1 && pc) dsT -= q.ds[r] * q.dz[r];
+                                dsT += (pass == 0) ? 0.0 : (pc ? sigma * mu : sigma_d * mu);
+                                const double rz = r ? (q.h[1] - q.s[1] + fv[t]) : (q.h[0] - q.s[0] - fv[t]);
+                                r3 = fma(-dsT, izr, rz);
+                            } else {
+                                dsT = q.dsT[r]; r3 = q.r3[r];
+                            }
+                            q.dz[r] = q.m[r] * q.z[r] * isr * fma(r ? -1.0 : 1.0, q.jd, -r3);
+                            q.ds[r] = q.m[r] * fma(-q.s[r], q.dz[r], dsT) * izr;
+                            mxs = fmax(mxs, -q.ds[r] * isr); mxz = fmax(mxz, -q.dz[r] * izr);
                         }
                     }
                 STAMP_END(21 + pass);
