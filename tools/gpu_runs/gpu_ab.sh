@@ -1,7 +1,7 @@
 #!/bin/bash
 # A/B timing of alternative builds (srbnmpc/libsrbnmpc*.so named on the command line):
 # quick oracle check, bench configs 2 / 3 / 5 and (if built) stamps, per library.
-#   usage: tools/gpu_ab.sh libsrbnmpc.so libsrbnmpc_b.so ...
+#   usage: tools/gpu_runs/gpu_ab.sh libsrbnmpc.so libsrbnmpc_b.so ...
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -10,7 +10,7 @@ for c in ('c3','c2'):
     a=np.load('gpurun_out/%s_split.npz'%c); b=np.load('gpurun_out/%s_gj0.npz'%c)
     print(c, {k: bool(np.array_equal(a[k],b[k])) for k in a.files})
 " && \
-bash tools/gpu_waves.sh 3 libsrbnmpc.so:1 libsrbnmpc_gj0.so:1 libsrbnmpc.so:1 libsrbnmpc_gj0.so:1 && \
-bash tools/gpu_waves.sh 2 libsrbnmpc.so:4 libsrbnmpc_gj0.so:4 && \
-bash tools/gpu_waves.sh 5 libsrbnmpc.so:2 libsrbnmpc_gj0.so:2 && \
+bash tools/gpu_runs/gpu_waves.sh 3 libsrbnmpc.so:1 libsrbnmpc_gj0.so:1 libsrbnmpc.so:1 libsrbnmpc_gj0.so:1 && \
+bash tools/gpu_runs/gpu_waves.sh 2 libsrbnmpc.so:4 libsrbnmpc_gj0.so:4 && \
+bash tools/gpu_runs/gpu_waves.sh 5 libsrbnmpc.so:2 libsrbnmpc_gj0.so:2 && \
 timeout -k 10 400 python -u -m pytest tests -x -q -m gpu --timeout 120 --timeout-method thread > gpurun_out/pytest_split.log 2>&1; rc=$?; tail -3 gpurun_out/pytest_split.log; exit $rc

@@ -1,6 +1,6 @@
 #!/bin/bash
 # LL CLF-QP: bench line (with CPU baseline), rocprofv3 kernel stats, HBM PMC passes.
-# Every GPU step time-limited; stops at the first failure.   usage: tools/gpu_ll_prof.sh [tag]
+# Every GPU step time-limited; stops at the first failure.   usage: tools/gpu_runs/gpu_ll_prof.sh [tag]
 set -o pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out

@@ -1,6 +1,6 @@
 #!/bin/bash
 # SQ counters of the solve kernel (one rocprofv3 --pmc pass per counter group, kernel trace
-# only): where a wave's cycles go at configs[2].   usage: tools/gpu_pmc_sq.sh [config]
+# only): where a wave's cycles go at configs[2].   usage: tools/gpu_runs/gpu_pmc_sq.sh [config]
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # Round-2 GPU run: gpu test suite, smoke, bench lines (default = configs[2]; configs[1], N=20,
 # LL), rocprofv3 kernel stats + FETCH/WRITE PMC passes for the default config, stamps, and
 # raw GPU outputs of config 5 for offline analysis.  Every GPU step time-limited; stops at
-# the first failure.   usage: tools/gpu_r02.sh [skip_tests]
+# the first failure.   usage: tools/gpu_runs/gpu_r02.sh [skip_tests]
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

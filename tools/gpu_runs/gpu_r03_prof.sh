@@ -3,7 +3,7 @@
 # passes (separate runs) of bench configs 3 (default instance and the spill-free 2-wave instance,
 # for the scratch share of WRITE_SIZE), 5, 2 and the LL path, rocprofv3 kernel-trace stats of the
 # same commands, then the bench lines reading the traffic files.  Every GPU step time-limited and
-# chained: the first failure ends the script.   usage: tools/gpu_r03_prof.sh
+# chained: the first failure ends the script.   usage: tools/gpu_runs/gpu_r03_prof.sh
 set -o pipefail
 mkdir -p gpurun_out
 export TMPDIR=/tmp

@@ -2,7 +2,7 @@
 # Round GPU run: gpu test suite, smoke, bench lines (configs 2/3/5), rocprofv3 kernel-trace
 # stats and HBM PMC passes (FETCH_SIZE, WRITE_SIZE in separate runs) for the default config.
 # Every GPU step has its own time limit; the script stops at the first failure.
-#   usage: tools/gpu_round.sh [tag] [skip_tests]
+#   usage: tools/gpu_runs/gpu_round.sh [tag] [skip_tests]
 set -o pipefail
 TAG=${1:-r01}
 mkdir -p gpurun_out

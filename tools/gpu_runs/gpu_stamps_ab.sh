@@ -1,6 +1,6 @@
 #!/bin/bash
 # Phase stamps (tools/stamps.py) of several stamps builds on one config.
-#   usage: tools/gpu_stamps_ab.sh "N C Ko Kn A" libsrbnmpc_stX.so ...
+#   usage: tools/gpu_runs/gpu_stamps_ab.sh "N C Ko Kn A" libsrbnmpc_stX.so ...
 set -o pipefail
 mkdir -p gpurun_out
 cfg=$1; shift

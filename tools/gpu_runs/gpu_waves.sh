@@ -1,5 +1,5 @@
 #!/bin/bash
-# Bench one config across builds x waves per agent:  tools/gpu_waves.sh <config> lib:nw [lib:nw ...]
+# Bench one config across builds x waves per agent:  tools/gpu_runs/gpu_waves.sh <config> lib:nw [lib:nw ...]
 set -o pipefail
 mkdir -p gpurun_out
 c=$1; shift
