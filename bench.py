@@ -480,11 +480,14 @@ def main():
     ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
     ap.add_argument("--qp-init", type=int, default=1,
                     help="QP-stage start: 1 scaled (default), 0 iSWIFT's kkt_initialize (srb_ctx_set_qp_init)")
+    ap.add_argument("--polish-fused", type=int, default=1,
+                    help="1 (default): the active-set polish runs at the end of the solve kernel where the instance "
+                         "allows (NZL <= 16), 0: as srb_polish_kernel (SRB_OPT_POLISH_FUSED)")
     ap.add_argument("--emulate-shards", type=int, default=1,
                     help="diagnostic: solve rank 0's shard of a swarm this many GPUs wide on one GPU (the whole "
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (tools/pmc_traffic.py); default profiles/r03_pmc_traffic_c<config>.json")
+                    help="PMC summary (tools/pmc_traffic.py); default profiles/r04_pmc_traffic_c<config>.json")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU check of the multi-process launch only (gloo, no GPU, no solve; tests/test_bench_launch.py)")
     args = ap.parse_args()
@@ -537,6 +540,7 @@ def main():
     solver = srbnmpc.BatchSolver(p, n_loc, local_rank)
     solver.set_waves(args.waves)
     solver.set_qp_init(args.qp_init)
+    solver.set_option("polish_fused", args.polish_fused)
     # one explicit stream for the collective, both kernels and the timing events (the C ABI
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)
@@ -590,12 +594,14 @@ def main():
     dense_per_solve = dense_equiv_flops(p, iters) / max(1, iters.shape[0])
     cyc_iter = solve_ms * 1e-3 * SCLK_GHZ * 1e9 / max(1, int(iters.sum(1).max()))
     traffic = traffic_polish = None
+    fused = solver.polish_fused_active()
     if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", f"r03_pmc_traffic_c{args.config}.json")
+        args.traffic_json = os.path.join(ROOT, "profiles", f"r04_pmc_traffic_c{args.config}.json")
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
-            if tj.get("config") == args.config and tj.get("agents") == n_loc:
+            if tj.get("config") == args.config and tj.get("agents") == n_loc and \
+                    tj.get("polish_fused", 0) == int(fused):
                 traffic = tj.get("hbm_bytes_per_launch")
                 traffic_polish = tj.get("kernels", {}).get("srb_polish_kernel", {}).get("hbm_bytes")
         except Exception:
@@ -624,12 +630,13 @@ def main():
                      "cycles_per_iter": cyc_iter,
                      "cycles_per_iter_note": "solve-kernel HIP-event time x 2.4 GHz / IPM iterations (QP + NLP) of "
                                              "the slowest agent: the critical-path cost of one iteration; per-phase "
-                                             "split in profiles/r03_*_stamps.txt",
+                                             "split in profiles/r04_*_stamps.txt",
                      "kernel": "srb_nmpc_kernel", "waves_per_agent": solver.waves(), "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
                      "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
                                    "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
                                    "agent), neither MFMA- nor HBM-throughput-bound",
-                     "polish_ms": float(np.median(pol)), "polish_kernel": "srb_polish_kernel",
+                     "polish_ms": float(np.median(pol)),
+                     "polish_kernel": "fused into srb_nmpc_kernel" if fused else "srb_polish_kernel",
                      "polish_traffic": traffic_polish,
                      "io_bytes_per_launch": io_bytes(p, n_loc, sh["obstacles"].shape[0], A_total if cfg["K_nbr"] else 0)},
         "cpu_baseline": None,

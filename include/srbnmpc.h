@@ -143,13 +143,16 @@ int srb_ctx_waves(srb_ctx *ctx);
  *   SRB_OPT_GRID_MIN_ROWS        tables of this many rows or more get a selection grid (default 8192)
  *   SRB_OPT_GRID_MIN_ROWS_STATIC the same for a versioned static obstacle table (default 4096)
  *   SRB_OPT_POLISH_FUSED         1 (default) the polish runs at the end of the solve kernel (problems with
- *                                N(C-1)+1 <= 16), 0 as a kernel of its own after it; the same results */
+ *                                N(C-1)+1 <= 16), 0 as a kernel of its own after it; the same results
+ *   SRB_OPT_LAST_POLISH          read only: how the last launch polished, 0 not at all, 1 polish kernel,
+ *                                2 fused into the solve kernel */
 #define SRB_OPT_POLISH 1
 #define SRB_OPT_POLISH_RHO 2
 #define SRB_OPT_POLISH_WAVES 3
 #define SRB_OPT_GRID_MIN_ROWS 4
 #define SRB_OPT_GRID_MIN_ROWS_STATIC 5
 #define SRB_OPT_POLISH_FUSED 6
+#define SRB_OPT_LAST_POLISH 7
 int srb_ctx_set_option(srb_ctx *ctx, int opt, double value);
 int srb_ctx_get_option(srb_ctx *ctx, int opt, double *value);
 

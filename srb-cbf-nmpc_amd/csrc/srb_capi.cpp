@@ -116,6 +116,7 @@ struct srb_ctx {
     // srb_ctx_set_option (SRB_OPT_*): the polish of the NLP result on/off, its penalty and waves per
     // agent, the selection-grid thresholds
     int polish, polish_waves, grid_min_rows, grid_min_rows_static, polish_fused;
+    int last_polish;               // how the last launch polished: 0 no, 1 polish kernel, 2 fused
     double polish_rho;
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
@@ -305,7 +306,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
-    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -439,6 +440,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     const bool fused = use_nlp && c->polish && c->polish_fused && SRB_FUSED_POLISH_OK(in->nzl);
     const bool polish = use_nlp && c->polish && !fused;
     k.polish_fused = fused ? 1 : 0;
+    c->last_polish = fused ? 2 : polish ? 1 : 0;
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
@@ -491,6 +493,8 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
     case SRB_OPT_POLISH_FUSED:
         if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_POLISH_FUSED: 0 or 1");
         c->polish_fused = (int)v; return SRB_OK;
+    case SRB_OPT_LAST_POLISH:
+        return fail(SRB_ERR_ARG, "SRB_OPT_LAST_POLISH is read only");
     case SRB_OPT_GRID_MIN_ROWS:
     case SRB_OPT_GRID_MIN_ROWS_STATIC:
         if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
@@ -511,6 +515,7 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_GRID_MIN_ROWS: *v = c->grid_min_rows; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS_STATIC: *v = c->grid_min_rows_static; return SRB_OK;
     case SRB_OPT_POLISH_FUSED: *v = c->polish_fused; return SRB_OK;
+    case SRB_OPT_LAST_POLISH: *v = c->last_polish; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }
@@ -663,8 +668,8 @@ extern "C" int srb_last_polish_ms(srb_ctx *c, float *polish_ms)
     if (!c || !c->timed) return fail(SRB_ERR_ARG, "no timed launch");
     HIPCHK(hipEventSynchronize(c->ev[1]));
     float t = 0;
-    HIPCHK(hipEventElapsedTime(&t, c->ev[3], c->ev[1]));
-    if (polish_ms) *polish_ms = t;      // srb_polish_kernel_* (0 without the NLP stage)
+    if (c->last_polish == 1) HIPCHK(hipEventElapsedTime(&t, c->ev[3], c->ev[1]));
+    if (polish_ms) *polish_ms = t;      // srb_polish_kernel_* (0 without it: no NLP stage, or fused)
     return SRB_OK;
 }
 

@@ -28,7 +28,7 @@ _ip = ctypes.POINTER(ctypes.c_int)
 OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
 # srb_ctx_set_option codes (SRB_OPT_* of include/srbnmpc.h)
 OPTIONS = {"polish": 1, "polish_rho": 2, "polish_waves": 3, "grid_min_rows": 4, "grid_min_rows_static": 5,
-           "polish_fused": 6}
+           "polish_fused": 6, "last_polish": 7}
 ABI_VERSION = 4                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 
@@ -266,13 +266,17 @@ class BatchSolver:
 
     def set_option(self, name: str, value: float):
         """Context option (srb_ctx_set_option): name one of OPTIONS ("polish", "polish_rho",
-        "polish_waves", "grid_min_rows", "grid_min_rows_static")."""
+        "polish_waves", "grid_min_rows", "grid_min_rows_static", "polish_fused"; "last_polish" is read only)."""
         _check(lib().srb_ctx_set_option(self._h, OPTIONS[name], float(value)))
 
     def get_option(self, name: str) -> float:
         v = ctypes.c_double()
         _check(lib().srb_ctx_get_option(self._h, OPTIONS[name], ctypes.byref(v)))
         return v.value
+
+    def polish_fused_active(self) -> bool:
+        """True when the last launch ran the polish inside the solve kernel (SRB_OPT_LAST_POLISH = 2)."""
+        return self.get_option("last_polish") == 2.0
 
     def set_qp_init(self, mode: int = 1):
         """QP-stage starting point (srb_ctx_set_qp_init): 1 scaled (default), 0 iSWIFT's kkt_initialize."""
@@ -288,7 +292,7 @@ class BatchSolver:
         return a.value, b.value
 
     def last_polish_ms(self) -> float:
-        """HIP-event time of the last launch's polish kernel (srb_polish_kernel), ms."""
+        """HIP-event time of the last launch's polish kernel (srb_polish_kernel), ms (0 when fused)."""
         t = ctypes.c_float()
         _check(lib().srb_last_polish_ms(self._h, ctypes.byref(t)))
         return t.value

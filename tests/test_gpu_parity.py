@@ -304,8 +304,10 @@ def test_fused_polish_equals_separate_polish_kernel():
         try:
             assert s.get_option("polish_fused") == 1.0
             fu = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+            assert s.get_option("last_polish") == 2.0 and s.last_polish_ms() == 0.0
             s.set_option("polish_fused", 0)
             se = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+            assert s.get_option("last_polish") == 1.0
         finally:
             s.close()
         np.testing.assert_array_equal(fu["status"], se["status"])
