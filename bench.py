@@ -307,14 +307,16 @@ def srb12_executed_flops(N, K, iters):
 
 def traffic_from(name, agents):
     """roofline.traffic of a non-default path: hbm bytes per launch of its PMC summary
-    (tools/pmc_traffic.py, profiles/r03_pmc_traffic_<name>.json) when it matches the batch."""
-    f = os.path.join(ROOT, "profiles", f"r03_pmc_traffic_{name}.json")
-    try:
-        tj = json.load(open(f))
-        if tj.get("agents") in (agents, 0):
-            return tj.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
-    except Exception:
-        pass
+    (tools/pmc_traffic.py, profiles/r04_pmc_traffic_<name>.json; the LL kernel, unchanged since,
+    also r03's) when it matches the batch."""
+    for rnd in ("r04", "r03") if name == "ll" else ("r04",):
+        f = os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic_{name}.json")
+        try:
+            tj = json.load(open(f))
+            if tj.get("agents") in (agents, 0):
+                return tj.get("hbm_bytes_per_launch"), os.path.relpath(f, ROOT)
+        except Exception:
+            pass
     return None, None
 
 

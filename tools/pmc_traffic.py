@@ -6,7 +6,7 @@ HBM section) into per-launch HBM traffic figures that bench.py reports as roofli
         reads, 16-B/lane reads and 8-B/lane writes) -> counter units per true byte for each
         access width (the guide calibrates only 16-B/lane streams; our kernels load and store
         8 B per lane, so the factor is measured, not assumed)
-    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <agents> <out.json> [calib.json]
+    python tools/pmc_traffic.py <fetch_dir> <write_dir> <config> <agents> <out.json> [calib.json] [polish_fused]
         per-launch FETCH / WRITE of every srb_* kernel of a bench run (median over dispatches),
         raw and divided by the measured 8-B/lane factors of calib.json
 
@@ -56,7 +56,7 @@ def calib(fdir, wdir, out):
     print(json.dumps({k: v for k, v in d.items() if k != "raw"}))
 
 
-def traffic(fdir, wdir, cfg, agents, out, calib_json=None):
+def traffic(fdir, wdir, cfg, agents, out, calib_json=None, polish_fused=0):
     f, w = per_dispatch(fdir, "FETCH_SIZE"), per_dispatch(wdir, "WRITE_SIZE")
     cal = json.load(open(calib_json)) if calib_json else None
     kern = {}
@@ -72,7 +72,7 @@ def traffic(fdir, wdir, cfg, agents, out, calib_json=None):
     solve = kern.get("srb_nmpc_kernel", kern.get("srb12_kernel", kern.get("srb_ll_kernel", {})))
     d = {"config": int(cfg) if cfg.lstrip("-").isdigit() else cfg, "agents": int(agents), "kernels": kern,
          "hbm_bytes_per_launch": solve.get("hbm_bytes"),
-         "calibration": calib_json,
+         "calibration": calib_json, "polish_fused": int(polish_fused),
          "note": "FETCH_SIZE / WRITE_SIZE from separate rocprofv3 --pmc passes, median over dispatches, divided by "
                  "the 8-B/lane factors measured by tools/ubench/fetch_calib (calibration file); "
                  "hbm_bytes_per_launch = the solve kernel's"}
@@ -85,7 +85,8 @@ def main():
         calib(*sys.argv[2:5])
     else:
         fdir, wdir, cfg, agents, out = sys.argv[1:6]
-        traffic(fdir, wdir, cfg, agents, out, sys.argv[6] if len(sys.argv) > 6 else None)
+        traffic(fdir, wdir, cfg, agents, out, sys.argv[6] if len(sys.argv) > 6 else None,
+                int(sys.argv[7]) if len(sys.argv) > 7 else 0)
 
 
 if __name__ == "__main__":
