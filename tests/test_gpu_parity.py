@@ -312,7 +312,7 @@ def test_fused_polish_equals_separate_polish_kernel():
             s.close()
         np.testing.assert_array_equal(fu["status"], se["status"])
         np.testing.assert_allclose(fu["x"], se["x"], atol=1e-8, rtol=0)
-        np.testing.assert_allclose(fu["alpha"], se["alpha"], atol=1e-8, rtol=0)
+        np.testing.assert_allclose(fu["obj"], se["obj"], rtol=1e-12, atol=1e-9)
         assert (fu["status"][:, 1] == 0).mean() >= 0.99
         r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"][:128], b["ref"][:128],
                                b["foot"][:128], b["obstacles"], b["nbr_state"], nthreads=8)
@@ -625,6 +625,9 @@ def test_mpcdist_horizon_10_trot_cycles_vs_oracle():
     m.use_snopt = True
     p = oracle.params(N, C, K_obs=1, use_nlp=1)
     q = np.zeros(18); dq = np.zeros(18)
+    # moving start (test_cpp_shim's): from rest at the origin the agent sits inside the first
+    # obstacle's eps radius and the NLP ends FATAL (dual divergence) there, on the GPU and in the oracle alike
+    q[0], dq[0], q[1], dq[1] = 0.02, 0.1, -0.01, 0.02
     for cyc in range(3):
         ind = [1, 0, 0, 1] if cyc % 2 == 0 else [0, 1, 1, 0]          # trot: FR + RL, then FL + RR
         m.updateState(q, dq, ind, m.toePos_, np.zeros(4))

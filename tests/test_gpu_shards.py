@@ -161,12 +161,12 @@ for cycle in range(3):                                   # buffers reused across
     torch.cuda.synchronize()
     assert torch.equal(out, x + cycle)
     assert out.data_ptr() == ex.recv.data_ptr()           # equal shards: the receive buffer is the table
-# unequal shards (1000 agents over 3 ranks: 334 / 333 / 333): the padded receive buffer and the
+# unequal shards (1000 agents over 3 ranks: 333 / 333 / 334): the padded receive buffer and the
 # index_select into the table, on this GPU; the other two ranks' blocks are supplied by a stand-in for
 # the collective (one process cannot host three RCCL ranks on one device)
 full = torch.randn(1000, 4, dtype=torch.float64, device="cuda")
 ex3 = sd.NeighbourExchange(1000, 3, 1, x.device)
-assert ex3.flat and not ex3.equal and ex3.counts == [334, 333, 333]
+assert ex3.flat and not ex3.equal and ex3.counts == [333, 333, 334]
 lo, hi = sd.shard_range(1000, 3, 1)
 def fake_all_gather(recv, send):
     v = recv.view(3, ex3.cmax, 4)
