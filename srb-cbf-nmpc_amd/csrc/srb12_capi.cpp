@@ -3,7 +3,7 @@
 // The context owns device staging for the host-buffer entry point, a LIP-mode context whose
 // selection machinery (srb_knn_kernel and its grids, srb_capi.cpp) it reuses for the obstacle /
 // neighbour rows, and events around the two launches.  One 64-lane workgroup per agent runs
-// srb12_kernel_<TS> (srb12_kernels.hip), TS = row-slot trips per lane.
+// srb12_kernel_<TL>_<TO>_<NC>_<K1> (srb12_kernels.hip): row-slot trips per lane, (N, K) compiled in or 0.
 #include <hip/hip_runtime.h>
 #include <cmath>
 #include <cstring>
@@ -19,16 +19,16 @@ int srb_internal_mark_done(srb_ctx *c, hipStream_t s);
 
 typedef void (*srb12_fn)(Srb12KParams, int, const double *, const double *, const double *, const int *,
                          const double *, const double *, const int *, double *, double *, double *, int *, int *);
-#define DECL12(TL, TO)                                                                                          \
-    extern "C" __global__ void srb12_kernel_##TL##_##TO(Srb12KParams, int, const double *, const double *,      \
+#define DECL12(TL, TO, NC, K1)                                                                                  \
+    extern "C" __global__ void srb12_kernel_##TL##_##TO##_##NC##_##K1(Srb12KParams, int, const double *, const double *,      \
                                                         const double *, const int *, const double *,             \
                                                         const double *, const int *, double *, double *,         \
                                                         double *, int *, int *);
 SRB12_INSTANCES(DECL12)
 #undef DECL12
 extern "C" __global__ void srb12_pos_kernel(int n_agents, const double *x0g, double *pos);
-struct srb12_inst { int tl, to; srb12_fn fn; };
-#define ENTRY12(TL, TO) {TL, TO, srb12_kernel_##TL##_##TO},
+struct srb12_inst { int tl, to, nc, k1; srb12_fn fn; };
+#define ENTRY12(TL, TO, NC, K1) {TL, TO, NC, K1, srb12_kernel_##TL##_##TO##_##NC##_##K1},
 static const srb12_inst g_inst12[] = {SRB12_INSTANCES(ENTRY12)};
 #undef ENTRY12
 
@@ -83,8 +83,10 @@ extern "C" int srb12_nv(const srb12_params *p) { return 24 * p->N + 1; }
 static const srb12_inst *pick12(const srb12_params *p)
 {
     const int tl = srb12_leg_trips(p->N), to = srb12_obs_trips(p->N, p->K_obs + p->K_nbr);
-    for (const srb12_inst &in : g_inst12)
-        if (in.tl >= tl && in.to >= to) return &in;
+    for (const srb12_inst &in : g_inst12)      // the (N, K) compiled in
+        if (in.nc == p->N && in.k1 == p->K_obs + p->K_nbr + 1 && in.tl >= tl && in.to >= to) return &in;
+    for (const srb12_inst &in : g_inst12)      // run-time (N, K)
+        if (in.nc == 0 && in.tl >= tl && in.to >= to) return &in;
     return nullptr;
 }
 

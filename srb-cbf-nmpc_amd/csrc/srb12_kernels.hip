@@ -36,6 +36,10 @@
 #include <stdint.h>
 #include "srb_kernel_params.h"
 
+#ifndef SRB12_REFINE_PREDICTOR        // 1: refine the predictor's solve too (round-3 behaviour)
+#define SRB12_REFINE_PREDICTOR 0
+#endif
+
 #define SYNC() __syncthreads()
 #include "srb_wave.h"
 
@@ -44,6 +48,7 @@ namespace {
 struct Srb12Lds {
     double *Wl, *cs, *ct, *Kst, *Hst, *T, *Q3, *Rh, *Z, *xr;
     double *rX, *rU, *gX, *gU, *dX, *dU, *kff, *vv, *sc, *obs, *eps, *xsv;
+    double *wq, *wqN, *wr;                                  // the weights q, qN, r (lane-indexed reads)
     int *sel;
 };
 
@@ -62,6 +67,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     L.rX = p; L.rU = p + 13 * N; L.gX = p + 25 * N; L.gU = p + 38 * N; L.xsv = p; p += 50 * N;
     L.dX = p; p += 13 * N; L.dU = p; p += 12 * N; L.kff = p; p += 12 * N;
     L.vv = p; p += 16; L.sc = p; p += 16;
+    L.wq = p; L.wqN = p + 12; L.wr = p + 24; p += 28;
     L.obs = p; p += 2 * N * K; L.eps = p; p += K;
     L.sel = (int *)p;
     return L;
@@ -171,6 +177,14 @@ __device__ __forceinline__ double rowsum(double a)
     swap_d<32>(a, a0, a1); a = a0 + a1;
     swap_d<16>(a, a0, a1); return a0 + a1;
 }
+// a lane index the compiler cannot treat as loop-invariant: conditions on it are re-evaluated where
+// they are used (one VALU compare) instead of being hoisted into SGPR lane masks that stay live
+// across the stage loops (the masks of dozens of lane predicates spilled SGPRs into VGPR lanes)
+__device__ __forceinline__ int opq(int x)
+{
+    asm volatile("" : "+v"(x));
+    return x;
+}
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c)
 {
     return __builtin_amdgcn_mfma_f64_16x16x4f64(a, b, c, 0, 0, 0);
@@ -178,7 +192,7 @@ __device__ __forceinline__ d4 mfma(double a, double b, d4 c)
 
 } // namespace
 
-template <int TL, int TO>
+template <int TL, int TO, int NC, int K1>
 __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, const double *__restrict__ x0g,
         const double *__restrict__ xrefg, const double *__restrict__ footg, const int *__restrict__ contactg,
         const double *__restrict__ obstacles, const double *__restrict__ nbr_state, const int *__restrict__ sel_g,
@@ -186,7 +200,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         int *__restrict__ status_out, int *__restrict__ iters_out, double *lds)
 {
     const int tid = threadIdx.x, lane = tid;
-    const int N = prm.N, K = prm.K_obs + prm.K_nbr, NK = N * K, nv = 24 * N + 1, NL = 4 * N;
+    const int N = NC > 0 ? NC : prm.N, K = K1 > 0 ? K1 - 1 : prm.K_obs + prm.K_nbr;
+    const int NK = N * K, nv = 24 * N + 1, NL = 4 * N;
     const double Ts = prm.Ts, tsm = prm.Ts / prm.mass, mus = prm.mus;
     const double tol = prm.tol, th = tol / sqrt(3.0);
     const int ci = lane & 15, gi = lane >> 4;          // column / component, 16-lane row
@@ -201,6 +216,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // ---------------- inputs, per-grid model (orc12_dynamics), selected rows
     for (int i = tid; i < 12 * N; i += 64) L.xr[i] = xrefg[(size_t)agent * 12 * N + i];
     for (int i = tid; i < 4 * N; i += 64) L.ct[i] = contactg[(size_t)agent * 4 * N + i] ? 1.0 : 0.0;
+    // weights indexed by lane go through LDS: a lane-indexed read of the kernel-argument arrays is a
+    // vector memory load, one per use inside the factor's and the solves' stage loops
+    if (tid < 12) { L.wq[tid] = prm.q[tid]; L.wqN[tid] = prm.qN[tid]; }
+    if (tid < 3) L.wr[tid] = prm.r[tid];
     if (prm.use_nlp && tid < K) L.sel[tid] = sel_g[(size_t)agent * K + tid];
     SYNC();
     for (int e = tid; e < 4 * N; e += 64) {              // one (grid, leg) per lane: W_l = Ts Iw^-1 [r]x
@@ -253,6 +272,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     if (tid < 12) L.vv[tid] = x0[tid];
     if (tid == 0) L.Z[24 * N] = 0.0;                    // s
     SYNC();
+#pragma clang loop unroll(disable)
     for (int k = 0; k < N; k++) {                        // x_{k+1} = A_k x_k + B_k u_k + c_k
         double v = 0.0;
         if (tid < 12) {
@@ -284,7 +304,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // Q^_k (state block k, 13 x 13) entry: diag(q) + delta on the 12 states, the obstacle rows' (p_x,
     // p_y, s) block; the slack's own weight Sw + delta enters once, at s_0 (the factor's last pivot)
     auto qhat = [&](int k, int i, int j, double delta) {
-        double v = (i == j && i < 12) ? ((k == N - 1) ? prm.qN[i] : prm.q[i]) + delta : 0.0;
+        double v = (i == j && i < 12) ? ((k == N - 1) ? L.wqN[i] : L.wq[i]) + delta : 0.0;
         const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
         if (pi && pj) {
             const double *q3 = L.Q3 + 6 * k;
@@ -297,7 +317,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // R^_k entry (12 x 12): r + delta on the diagonal, each stance leg's 3 x 3 row block (Rh)
     auto rhat = [&](int k, int i, int j, double delta) {
         if (i >= 12 || j >= 12) return 0.0;
-        double v = (i == j) ? prm.r[i % 3] + delta : 0.0;
+        double v = (i == j) ? L.wr[i % 3] + delta : 0.0;
         if (i / 3 == j / 3) v += L.Rh[24 * k + 6 * (i / 3) + sym3(i % 3, j % 3)];
         return v;
     };
@@ -311,7 +331,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         d4 Vd;                                            // V in the MFMA accumulator layout: V[gi + 4 q][ci]
 #pragma unroll
         for (int q = 0; q < 4; q++) Vd[q] = qhat(N - 1, gi + 4 * q, ci, delta);
+#pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
+            const int lane = opq(tid), ci = lane & 15, gi = lane >> 4;
             const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
             // operand values: A~[4 kb + gi][ci] (B operand of A~, A operand of A~'), B~ likewise (rows
@@ -334,6 +356,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             for (int kb = 0; kb < 4; kb++) Vn = mfma(Ab[kb], G[kb], Vn);          // Q^_{k-1} + A~'G
             Hux = mfma(Bb1, G[1], Hux); Hux = mfma(Bb2, G[2], Hux);                // B~'G (12 x 13)
             Hu = mfma(Bb1, F[1], Hu); Hu = mfma(Bb2, F[2], Hu);                    // R^ + B~'F
+            S12ST(10);  // factor: operands and the products
             // to the column layout: Hu, Hux column-major in T (12 rows a column)
 #pragma unroll
             for (int q = 0; q < 3; q++) {
@@ -350,6 +373,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 for (int r = 0; r < 12; r++) col[r] = (lane < 25) ? src[r] : ((lane - 25 == r) ? 1.0 : 0.0);
             }
             SYNC();
+            S12ST(11);  // factor: to the column layout
             // Hu = L D L': forward elimination, row i -= (Hu[i][kk] / d_kk) row kk for i > kk, on every column.
             // Lane kk holds column kk, whose entries below the pivot are the multipliers (readlane)
             double dinv[12];
@@ -360,8 +384,13 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double t = col[kk] * rcp_d(piv);
 #pragma unroll
                 for (int i = kk + 1; i < 12; i++) col[i] = fma(-readlane_d(col[i], kk), t, col[i]);
-                dinv[kk] = (piv > 0.0) ? 1.0 / sqrt(piv) : 0.0;
+                // 1 / sqrt(piv): v_rsq_f64 and two Newton steps (a failed pivot's value is never used)
+                double rs = __builtin_amdgcn_rsq(piv);
+                rs = fma(0.5 * rs, fma(-piv * rs, rs, 1.0), rs);
+                rs = fma(0.5 * rs, fma(-piv * rs, rs, 1.0), rs);
+                dinv[kk] = rs;
             }
+            S12ST(12);  // factor: elimination
             // Y = D^-1/2 L^-1 Hux (lanes 12..24), Z = D^-1/2 L^-1 (lanes 25..36), back to T column-major
             if (lane >= 12 && lane < 37)
 #pragma unroll
@@ -385,6 +414,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 if (ci <= i) Hk[tri(i, ci)] = ZZ[q];
             }
             SYNC();
+            S12ST(13);  // factor: Y, Z, the Schur / gain / inverse products, stores
         }
         if (fail) return false;
         // the free initial slack closes the recursion: V_-1[12][12] + Sw + delta > 0 is the last
@@ -397,12 +427,15 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // entry) into dX (13 per grid), dU: w solves H w = -rhs on the dynamics' null space (x_0 fixed, s_0
     // free).  Component i = ci of every vector, replicated in the four rows; row gi takes columns
     // 4 gi .. 4 gi + 3 of each matrix-vector product (perm_d gathers them), rowsum adds the rows.
+    [[maybe_unused]] int sph = 4;                         // stamps: the phase a solve's set-up counts to
     auto riccati_solve = [&](int c, bool acc) {
-        const int i = ci, g = gi, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
+        S12ST(sph);
         const double *rX = c ? L.gX : L.rX, *rU = c ? L.gU : L.rU;
-        const int gsrc = 16 * g + 4 * g;                   // lane holding component 4 g (this row's copy)
-        double v = (i < 13) ? rX[13 * (N - 1) + i] : 0.0;
+        double v = (ci < 13) ? rX[13 * (N - 1) + ci] : 0.0;
+#pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
+            const int ln = opq(lane), i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
+            const int gsrc = 16 * g + 4 * g;               // lane holding component 4 g (this row's copy)
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
             const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
             const double v6 = bc16(v, 6), v7 = bc16(v, 7), v8 = bc16(v, 8), v9 = bc16(v, 9), v10 = bc16(v, 10), v11 = bc16(v, 11);
@@ -436,9 +469,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         }
         const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
         SYNC();                                            // kff
-        double prev = (i == 12) ? ds0 : 0.0;
-        const int lsrc = 16 * g + 3 * g;                   // lane holding component 3 g (leg g's first force)
+        S12ST(14);  // solve: backward sweep
+        double prev = (ci == 12) ? ds0 : 0.0;
+#pragma clang loop unroll(disable)
         for (int k = 0; k < N; k++) {
+            const int ln = opq(lane), i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0;
+            const int gsrc = 16 * g + 4 * g, lsrc = 16 * g + 3 * g;   // lanes of components 4 g, 3 g (leg g's first force)
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k;
             const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
             // du = kff + K dx: this row's state columns j = 4 g + m
@@ -475,15 +511,15 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             prev = dx;
         }
         SYNC();
+        S12ST(15);  // solve: forward sweep
     };
     // one step of iterative refinement of column 0 (correction in column 1): the residual of H w = -rhs
     // on the null space is the reduced gradient -- t_u = R^ du + rhs_u + B' mu, t_s = (Sw + delta) ds_0 +
     // rhs_s + mu_0[12], costates mu from the state rows -- and the correction solves with (0, t_u, t_s)
     auto refine = [&](double delta) {
-        const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
         const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
         double *tX = L.gX, *tU = L.gU;
-        auto qdx = [&](int k, const double *dx) {          // (Q^_k dx)[i]
+        auto qdx = [&](int k, const double *dx, int i) {   // (Q^_k dx)[i]
             double v = 0.0;
             for (int j = 0; j < 13; j++) {
                 const bool nz = (j == i) || ((i < 2 || i == 12) && (j < 2 || j == 12));
@@ -492,15 +528,17 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             return v;
         };
         for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
-        double m = (i < 13) ? qdx(N - 1, dX + 13 * (N - 1)) + rX[13 * (N - 1) + i] : 0.0;
+        double m = (ci < 13) ? qdx(N - 1, dX + 13 * (N - 1), ci) + rX[13 * (N - 1) + ci] : 0.0;
+#pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
+            const int i = opq(lane) & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
             double vb[13];
 #pragma unroll
             for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
-            if (lane < 12) {
+            if (opq(lane) < 12) {
                 const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                double t = fma(prm.r[a3] + delta, du[a3], rU[12 * k + i]);
+                double t = fma(L.wr[a3] + delta, du[a3], rU[12 * k + i]);
                 for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
                 t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
                 for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
@@ -512,7 +550,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 if (i >= 6 && i < 9) mn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], mn);
                 else if (i >= 9 && i < 12)
                     mn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], mn);
-                m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1)) + rX[13 * (k - 1) + i] : 0.0;
+                m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1), i) + rX[13 * (k - 1) + i] : 0.0;
             }
         }
         const double m12 = bc16(m, 12);
@@ -527,9 +565,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     auto grad_f = [&](double *gx, double *gu) {
         for (int e = tid; e < 12 * N; e += 64) {
             const int k = e / 12, i = e - 12 * k;
-            const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+            const double w = (k == N - 1) ? L.wqN[i] : L.wq[i];
             gx[13 * k + i] = w * (X[e] - L.xr[e]);
-            gu[e] = prm.r[i % 3] * U[e];
+            gu[e] = L.wr[i % 3] * U[e];
         }
         for (int k = tid; k < N; k += 64) gx[13 * k + 12] = 0.0;
     };
@@ -550,10 +588,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 double c0, c1, c2;
                 fric_coef(q, mus, c0, c1, c2);
                 const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
-                const double s = ls[t][q], z = lz[t][q];
-                const double rp = g + s - h, om = z / s;
+                const double s = ls[t][q], z = lz[t][q], is = rcp_d(s);
+                const double rp = g + s - h, om = z * is;
                 const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
-                const double w = z + r3 / s + om * rp;
+                const double w = z + r3 * is + om * rp;
                 r[0] = fma(w, c0, r[0]); r[1] = fma(w, c1, r[1]); r[2] = fma(w, c2, r[2]);
             }
             double *ru = L.rU + 3 * e;
@@ -565,10 +603,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             const int e = lane + 64 * t;
             double g, h, c0, c1;
             obs_row(e, g, h, c0, c1);
-            const double s = os[t], z = oz[t];
-            const double rp = g + s - h, om = z / s;
+            const double s = os[t], z = oz[t], is = rcp_d(s);
+            const double rp = g + s - h, om = z * is;
             const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
-            const double w = z + r3 / s + om * rp;
+            const double w = z + r3 * is + om * rp;
             double *rx = L.rX + 13 * (e / K);
             __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -596,8 +634,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double s = ls[t][q], z = lz[t][q];
                 const double rp = g + s - h;
                 const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
-                dls[t][q] = -rp - jd; dlz[t][q] = (r3 - z * dls[t][q]) / s;
-                ms = fmax(ms, -dls[t][q] / s); mz = fmax(mz, -dlz[t][q] / z);
+                const double is = rcp_d(s);
+                dls[t][q] = -rp - jd; dlz[t][q] = (r3 - z * dls[t][q]) * is;
+                ms = fmax(ms, -dls[t][q] * is); mz = fmax(mz, -dlz[t][q] * rcp_d(z));
             }
         }
 #pragma unroll
@@ -612,8 +651,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             const double s = os[t], z = oz[t];
             const double rp = g + s - h;
             const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
-            dos[t] = -rp - jd; doz[t] = (r3 - z * dos[t]) / s;
-            ms = fmax(ms, -dos[t] / s); mz = fmax(mz, -doz[t] / z);
+            const double is = rcp_d(s);
+            dos[t] = -rp - jd; doz[t] = (r3 - z * dos[t]) * is;
+            ms = fmax(ms, -dos[t] * is); mz = fmax(mz, -doz[t] * rcp_d(z));
         }
         double rv[2] = {ms, mz};
         wred<2, 3u>(rv);
@@ -700,7 +740,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         fric_coef(q, mus, c0, c1, c2);
                         const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
                         const double s = ls[t][q], z = lz[t][q];
-                        const double rp = g + s - h, om = z / s;
+                        const double rp = g + s - h, om = z * rcp_d(s);
                         nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
                         const double cc[3] = {c0, c1, c2};
 #pragma unroll
@@ -723,7 +763,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 double g, h, c0, c1;
                 obs_row(e, g, h, c0, c1);
                 const double s = os[t], z = oz[t];
-                const double rp = g + s - h, om = z / s;
+                const double rp = g + s - h, om = z * rcp_d(s);
                 nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
                 // obstacle row of grid k on (p_x, p_y, s): J = (c0, c1, -1), Lagrangian Hessian -2z on p_x, p_y
                 const int k = e / K;
@@ -746,14 +786,15 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             double nrd = 0.0, gm = 1.0;
             for (int e = tid; e < 12 * N; e += 64) {
                 const int k = e / 12, i = e - 12 * k;
-                const double w = (k == N - 1) ? prm.qN[i] : prm.q[i];
+                const double w = (k == N - 1) ? L.wqN[i] : L.wq[i];
                 gm = fmax(gm, fabs(w * (X[e] - L.xr[e])));
-                gm = fmax(gm, fabs(prm.r[i % 3] * U[e]));
+                gm = fmax(gm, fabs(L.wr[i % 3] * U[e]));
             }
             gm = fmax(gm, fabs(prm.Sw * L.Z[24 * N]));
             {
                 const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
                 double lam = (i < 13) ? L.gX[13 * (N - 1) + i] : 0.0;
+#pragma clang loop unroll(disable)
                 for (int k = N - 1; k >= 0; k--) {
                     const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
                     const double v6 = bc16(lam, 6), v7 = bc16(lam, 7), v8 = bc16(lam, 8);
@@ -795,9 +836,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             double dmax = 1.0;
             for (int e = tid; e < 12 * N; e += 64) {
                 const int k = e / 12, i = e - 12 * k;
-                const double qd = ((k == N - 1) ? prm.qN[i] : prm.q[i]) + (i < 2 ? L.Q3[6 * k + 2 * i] : 0.0);
+                const double qd = ((k == N - 1) ? L.wqN[i] : L.wq[i]) + (i < 2 ? L.Q3[6 * k + 2 * i] : 0.0);
                 const int l = i / 3, a = i % 3;
-                const double rd = prm.r[a] + L.Rh[24 * k + 6 * l + sym3(a, a)];
+                const double rd = L.wr[a] + L.Rh[24 * k + 6 * l + sym3(a, a)];
                 dmax = fmax(dmax, fmax(qd, rd));
             }
             dmax = wmax(dmax);
@@ -813,12 +854,16 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             if (!ok) { flag = 1; break; }
             S12ST(3);   // between factor and predictor
             // ---- predictor
-            // (the refinement only near the optimum, mu < 1e-3: far from it the step's accuracy is not
-            // what limits progress, and it costs a solve)
+            // (the refinement only near the optimum, mu < 1e-3, and only of the corrector: far from the
+            // optimum the step's accuracy is not what limits progress, and the predictor only sets sigma
+            // and the second-order term; each refinement costs a solve)
             const bool refn = mu < 1e-3;
+            sph = 4;
             build_rhs(0, 0.0);
             riccati_solve(0, false);
+#if SRB12_REFINE_PREDICTOR
             if (refn) refine(delta);
+#endif
             S12ST(4);   // predictor rhs + solve (+ refinement)
             double dls[TL][6], dlz[TL][6], dos[TO], doz[TO];
             double2 al = row_step(0, 0.0, dls, dlz, dos, doz);
@@ -844,6 +889,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             S12ST(5);   // predictor row step, sigma
             // ---- corrector
+            sph = 6;
             build_rhs(1, sigma * mu);
             riccati_solve(0, false);
             if (refn) refine(delta);
@@ -978,6 +1024,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 }
                 SYNC();
                 if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
+                sph = 9;
                 riccati_solve(1, false);                                    // d = -H^-1 grad (column 1)
                 // multipliers z_A += RHO (c_A + J_A d) at the linearisation point; then x += d
 #pragma unroll
@@ -1093,8 +1140,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         const double xv = L.Z[v];
         x_out[(size_t)agent * nv + v] = xv;
         double w, cl = 0.0;
-        if (v < 12 * N) { const int k = v / 12, i = v - 12 * k; w = (k == N - 1) ? prm.qN[i] : prm.q[i]; cl = -w * L.xr[v]; }
-        else if (v < 24 * N) w = prm.r[(v - 12 * N) % 3];
+        if (v < 12 * N) { const int k = v / 12, i = v - 12 * k; w = (k == N - 1) ? L.wqN[i] : L.wq[i]; cl = -w * L.xr[v]; }
+        else if (v < 24 * N) w = L.wr[(v - 12 * N) % 3];
         else w = prm.Sw;
         f += fma(0.5 * w * xv, xv, cl * xv);
     }
@@ -1106,8 +1153,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     }
 }
 
-#define SRB12_KERNEL(TL, TO)                                                                                    \
-    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TL##_##TO(                                  \
+#define SRB12_KERNEL(TL, TO, NC, K1)                                                                            \
+    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TL##_##TO##_##NC##_##K1(                    \
         Srb12KParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ xrefg,        \
         const double *__restrict__ footg, const int *__restrict__ contactg, const double *__restrict__ obstacles, \
         const double *__restrict__ nbr_state, const int *__restrict__ sel_g, double *__restrict__ x_qp_out,      \
@@ -1117,7 +1164,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        srb12_agent<TL, TO>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out,     \
+        srb12_agent<TL, TO, NC, K1>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out,     \
                             x_out, obj_out, status_out, iters_out, lds);                                       \
     }
 SRB12_INSTANCES(SRB12_KERNEL)

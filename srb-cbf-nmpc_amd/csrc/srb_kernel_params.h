@@ -176,8 +176,13 @@ struct Srb12KParams {
 #define SRB12_POL_PASSES 2
 #define SRB12_POL_PTOL 1e-9
 #define SRB12_POL_DXTOL 1e-7
-// kernel instances (TL, TO): leg-slot trips (4N legs over 64 lanes) and obstacle-slot trips (N K rows)
-#define SRB12_INSTANCES(X) X(1, 1) X(1, 2) X(1, 4) X(1, 8) X(1, 12) X(2, 4) X(2, 8) X(2, 12)
+// kernel instances (TL, TO, NC, K1): leg-slot trips (4N legs over 64 lanes), obstacle-slot trips (N K
+// rows), and the horizon N and rows per grid K compiled in (NC = N, K1 = K + 1) or read at run time
+// (NC = K1 = 0).  The host launches the compiled-in instance of the problem's (N, K) when there is one
+// (every LDS offset and e / K a constant: fewer instructions and SGPRs in the stage loops), else the
+// first run-time instance whose trips fit
+#define SRB12_INSTANCES(X) X(1, 2, 10, 12) X(2, 4, 20, 12) \
+    X(1, 1, 0, 0) X(1, 2, 0, 0) X(1, 4, 0, 0) X(1, 8, 0, 0) X(1, 12, 0, 0) X(2, 4, 0, 0) X(2, 8, 0, 0) X(2, 12, 0, 0)
 static inline int srb12_leg_trips(int N) { return (4 * N + 63) / 64; }
 static inline int srb12_obs_trips(int N, int K) { return (N * K + 63) / 64 > 0 ? (N * K + 63) / 64 : 1; }
 // doubles of LDS one agent needs (the carve in srb12_kernels.hip)
@@ -190,6 +195,6 @@ static inline int srb12_lds_doubles(int N, int K)
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
            + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)
            + 13 * N + 12 * N + 12 * N                   // solution, feed-forward -Hu^-1 gu
-           + 16 + 16                                    // vector, scalars
+           + 16 + 16 + 28                               // vector, scalars, the weights q, qN, r
            + 2 * N * K + K + K + 2;                     // obstacle positions, eps, sel (as ints)
 }

@@ -13,7 +13,8 @@ from srbnmpc import srb12, workload  # noqa: E402
 
 PHASES = ["inputs/model/rollout", "residuals+costates", "Riccati factor", "factor->predictor",
           "predictor rhs+solve", "predictor step+sigma", "corrector rhs+solve", "corrector step+update",
-          "exit test->polish", "active-set polish"]
+          "exit test->polish", "active-set polish", "factor: products", "factor: to columns",
+          "factor: elimination", "factor: Y Z products, stores", "solve: backward sweep", "solve: forward sweep"]
 A, N = 1024, 10
 b = workload.make_batch12(A, N, "trot", seed=0)
 s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
