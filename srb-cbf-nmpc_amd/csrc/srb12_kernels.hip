@@ -61,7 +61,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     L.Wl = p; p += 36 * N;  L.cs = p; p += 2 * N;  L.ct = p; p += 4 * N;
     L.Kst = p; p += 156 * N;                                // K_k = -Hu^-1 Hux, 12 x 13 row-major per grid
     L.Hst = p; p += 78 * N;                                 // Hu_k^-1, packed lower triangle per grid
-    L.T = p; p += 300;                                      // factor transposes (column-major 12-row blocks)
+    L.T = p; p += 316;                                      // factor transposes (column-major 12-row blocks) + 16 sink entries
     L.Q3 = p; p += 6 * N; L.Rh = p; p += 24 * N;
     L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N;
     L.rX = p; L.rU = p + 13 * N; L.gX = p + 25 * N; L.gU = p + 38 * N; L.xsv = p; p += 50 * N;
@@ -176,14 +176,6 @@ __device__ __forceinline__ double rowsum(double a)
     double a0, a1;
     swap_d<32>(a, a0, a1); a = a0 + a1;
     swap_d<16>(a, a0, a1); return a0 + a1;
-}
-// a lane index the compiler cannot treat as loop-invariant: conditions on it are re-evaluated where
-// they are used (one VALU compare) instead of being hoisted into SGPR lane masks that stay live
-// across the stage loops (the masks of dozens of lane predicates spilled SGPRs into VGPR lanes)
-__device__ __forceinline__ int opq(int x)
-{
-    asm volatile("" : "+v"(x));
-    return x;
 }
 __device__ __forceinline__ d4 mfma(double a, double b, d4 c)
 {
@@ -328,12 +320,37 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     double schur = 0.0;
     auto factor = [&](double delta) -> bool {
         int fail = 0;
+        // this lane's entries (i = gi + 4 q, j = ci) of Q^ and R^, branch-free: masks and clamped LDS
+        // indices (a diagonal weight, an obstacle-block entry Q3, a leg-block entry Rh)
+        auto qh = [&](int k, int q) {
+            const int i = gi + 4 * q, j = ci;
+            const bool dg = i == j && i < 12, ob = (i < 2 || i == 12) && (j < 2 || j == 12);
+            const int a = (i == 12) ? 2 : (i < 2 ? i : 0), b = (j == 12) ? 2 : (j < 2 ? j : 0);
+            const int lo = a < b ? a : b, hi = a < b ? b : a;
+            const double wd = ((k == N - 1) ? L.wqN : L.wq)[i < 12 ? i : 0], qo = L.Q3[6 * k + (hi * (hi + 1)) / 2 + lo];
+            // masks as factors: the loads stay unconditional (a select lets the compiler sink them into branches)
+            return (dg ? 1.0 : 0.0) * (wd + delta) + (ob ? 1.0 : 0.0) * qo;
+        };
+        auto rh = [&](int k, int q) {
+            const int i = gi + 4 * q, j = ci;
+            const bool in = i < 12 && j < 12, dg = in && i == j, bl = in && i / 3 == j / 3;
+            const int i3 = in ? i % 3 : 0, j3 = in ? j % 3 : 0, l = in ? i / 3 : 0;
+            const double wd = L.wr[i3], rb = L.Rh[24 * k + 6 * l + sym3(i3, j3)];
+            return (dg ? 1.0 : 0.0) * (wd + delta) + (bl ? 1.0 : 0.0) * rb;
+        };
+        // B~[i][ci] for the operand rows i = 4 + gi (kb 1) and 8 + gi (kb 2): tsm on v (rows 6..8) for the
+        // leg's own axis, W_l on omega (rows 9..11)
+        auto bt = [&](int i, const double *W, const double *ct) {
+            const int j = ci < 12 ? ci : 0, l = j / 3, a = j - 3 * l;
+            const bool v = ci < 12 && i >= 6 && i < 9 && a == i - 6, w = ci < 12 && i >= 9 && i < 12;
+            const double ctl = ct[l], wl = W[9 * l + 3 * (w ? i - 9 : 0) + a];
+            return (v ? tsm : 0.0) * ctl + (w ? 1.0 : 0.0) * wl;
+        };
         d4 Vd;                                            // V in the MFMA accumulator layout: V[gi + 4 q][ci]
 #pragma unroll
-        for (int q = 0; q < 4; q++) Vd[q] = qhat(N - 1, gi + 4 * q, ci, delta);
+        for (int q = 0; q < 4; q++) Vd[q] = qh(N - 1, q);
 #pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
-            const int lane = opq(tid), ci = lane & 15, gi = lane >> 4;
             const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
             // operand values: A~[4 kb + gi][ci] (B operand of A~, A operand of A~'), B~ likewise (rows
@@ -341,7 +358,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             double Ab[4];
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) Ab[kb] = atil(4 * kb + gi, ci, Ts, c, s);
-            const double Bb1 = btil(4 + gi, ci, W, ct, tsm), Bb2 = btil(8 + gi, ci, W, ct, tsm);
+            const double Bb1 = bt(4 + gi, W, ct), Bb2 = bt(8 + gi, W, ct);
             d4 G = {0.0, 0.0, 0.0, 0.0}, F = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) G = mfma(Vd[kb], Ab[kb], G);           // G = V A~
@@ -349,8 +366,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             d4 Vn, Hu, Hux = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                Vn[q] = (k > 0) ? qhat(k - 1, gi + 4 * q, ci, delta) : 0.0;
-                Hu[q] = rhat(k, gi + 4 * q, ci, delta);
+                Vn[q] = (k > 0) ? qh(k - 1, q) : 0.0;
+                Hu[q] = rh(k, q);
             }
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) Vn = mfma(Ab[kb], G[kb], Vn);          // Q^_{k-1} + A~'G
@@ -358,19 +375,22 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             Hu = mfma(Bb1, F[1], Hu); Hu = mfma(Bb2, F[2], Hu);                    // R^ + B~'F
             S12ST(10);  // factor: operands and the products
             // to the column layout: Hu, Hux column-major in T (12 rows a column)
+            // (stores are unconditional: lanes outside a block write to the sink entries T[300..315])
+            const int sink = 300 + ci;
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const int i = gi + 4 * q;
-                if (ci < 12) L.T[12 * ci + i] = Hu[q];
-                if (ci < 13) L.T[144 + 12 * ci + i] = Hux[q];
+                L.T[ci < 12 ? 12 * ci + i : sink] = Hu[q];
+                L.T[ci < 13 ? 144 + 12 * ci + i : sink] = Hux[q];
             }
             SYNC();
             // lane j < 12: column j of Hu; 12..24: column j - 12 of Hux; 25..36: column j - 25 of I
             double col[12];
             {
                 const double *src = (lane < 12) ? L.T + 12 * lane : L.T + 144 + 12 * (lane < 25 ? lane - 12 : 0);
+                const double mc = (lane < 25) ? 1.0 : 0.0;
 #pragma unroll
-                for (int r = 0; r < 12; r++) col[r] = (lane < 25) ? src[r] : ((lane - 25 == r) ? 1.0 : 0.0);
+                for (int r = 0; r < 12; r++) col[r] = mc * src[r] + ((lane - 25 == r) ? 1.0 : 0.0);
             }
             SYNC();
             S12ST(11);  // factor: to the column layout
@@ -392,17 +412,19 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             S12ST(12);  // factor: elimination
             // Y = D^-1/2 L^-1 Hux (lanes 12..24), Z = D^-1/2 L^-1 (lanes 25..36), back to T column-major
-            if (lane >= 12 && lane < 37)
+            {
+                const bool yz = lane >= 12 && lane < 37;
 #pragma unroll
-                for (int r = 0; r < 12; r++) L.T[12 * (lane - 12) + r] = col[r] * dinv[r];
+                for (int r = 0; r < 12; r++) L.T[yz ? 12 * (lane - 12) + r : sink] = col[r] * dinv[r];
+            }
             SYNC();
             // Y'Y (13 x 13), Hu^-1 = Z'Z (12 x 12), Z'Y = -K (12 x 13): operands Y[4 kb + gi][ci], Z[..][ci]
             d4 YY = {0.0, 0.0, 0.0, 0.0}, ZZ = {0.0, 0.0, 0.0, 0.0}, ZY = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kb = 0; kb < 3; kb++) {
                 const int r = 4 * kb + gi;
-                const double ya = (ci < 13) ? L.T[12 * ci + r] : 0.0;
-                const double za = (ci < 12) ? L.T[156 + 12 * ci + r] : 0.0;
+                const double yt = L.T[12 * (ci < 13 ? ci : 12) + r], zt = L.T[156 + 12 * (ci < 12 ? ci : 11) + r];
+                const double ya = (ci < 13) ? yt : 0.0, za = (ci < 12) ? zt : 0.0;
                 YY = mfma(ya, ya, YY); ZZ = mfma(za, za, ZZ); ZY = mfma(za, ya, ZY);
             }
             Vd = Vn - YY;                                  // V_{k-1} = Q^ + A~'G - Hux' Hu^-1 Hux
@@ -410,8 +432,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
             for (int q = 0; q < 3; q++) {
                 const int i = gi + 4 * q;
-                if (ci < 13) Kk[13 * i + ci] = -ZY[q];
-                if (ci <= i) Hk[tri(i, ci)] = ZZ[q];
+                *(ci < 13 ? Kk + 13 * i + ci : L.T + sink) = -ZY[q];
+                *(ci <= i ? Hk + tri(i, ci) : L.T + sink) = ZZ[q];
             }
             SYNC();
             S12ST(13);  // factor: Y, Z, the Schur / gain / inverse products, stores
@@ -431,41 +453,40 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     auto riccati_solve = [&](int c, bool acc) {
         S12ST(sph);
         const double *rX = c ? L.gX : L.rX, *rU = c ? L.gU : L.rU;
+        double *sink = L.T + 300 + ci;                      // stores of lanes outside a vector (T is free here)
         double v = (ci < 13) ? rX[13 * (N - 1) + ci] : 0.0;
+        // branch-free stage bodies: loads from clamped indices, masks as factors, stores to the sink
 #pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
-            const int ln = opq(lane), i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
+            const int ln = lane, i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
             const int gsrc = 16 * g + 4 * g;               // lane holding component 4 g (this row's copy)
+            const double m12 = (i < 12) ? 1.0 : 0.0, m13 = (i < 13) ? 1.0 : 0.0;
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
             const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
             const double v6 = bc16(v, 6), v7 = bc16(v, 7), v8 = bc16(v, 8), v9 = bc16(v, 9), v10 = bc16(v, 10), v11 = bc16(v, 11);
             // gu = rhs_u + B~'v
-            double gu = 0.0;
-            if (i < 12) {
-                gu = fma(ct[l] * tsm, a == 0 ? v6 : a == 1 ? v7 : v8, rU[12 * k + i]);
-                gu = fma(W[9 * l + a], v9, gu); gu = fma(W[9 * l + 3 + a], v10, gu); gu = fma(W[9 * l + 6 + a], v11, gu);
-            }
+            double gu = fma(ct[l] * tsm, a == 0 ? v6 : a == 1 ? v7 : v8, rU[12 * k + ir]);
+            gu = fma(W[9 * l + a], v9, gu); gu = fma(W[9 * l + 3 + a], v10, gu); gu = fma(W[9 * l + 6 + a], v11, gu);
+            gu *= m12;
             // K'gu (state i) and -Hu^-1 gu (input i): this row's four input columns j = 4 g + m
             double pk = 0.0, ph = 0.0;
+            const int i13 = (i < 13) ? i : 12;
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                const int j = 4 * g + m;
-                const double gj = perm_d(gu, gsrc + m);
-                if (j < 12) {
-                    pk = fma((i < 13) ? Kk[13 * j + i] : 0.0, gj, pk);
-                    ph = fma((i < 12) ? Hk[tri(i, j)] : 0.0, gj, ph);
-                }
+                const int j = 4 * g + m, jc = (j < 12) ? j : 11;
+                const double gj = perm_d(gu, gsrc + m) * ((j < 12) ? 1.0 : 0.0);
+                pk = fma(m13 * Kk[13 * jc + i13], gj, pk);
+                ph = fma(m12 * Hk[tri(ir, jc)], gj, ph);
             }
             rowsum2(pk, ph);
-            if (g == 0 && i < 12) L.kff[12 * k + i] = -ph;
+            *((g == 0 && i < 12) ? L.kff + 12 * k + i : sink) = -ph;
             // v_{k-1} = rhs_x(k-1) + A~'v + K'gu
             const double v0 = bc16(v, 0), v1 = bc16(v, 1), v2 = bc16(v, 2), v3 = bc16(v, 3), v4 = bc16(v, 4), v5 = bc16(v, 5);
-            double vn = v + pk;
-            if (i >= 6 && i < 9) vn = fma(Ts, i == 6 ? v0 : i == 7 ? v1 : v2, vn);
-            else if (i >= 9 && i < 12)
-                vn = fma(Ts, i == 9 ? fma(cc, v3, -sn * v4) : i == 10 ? fma(sn, v3, cc * v4) : v5, vn);
-            if (k > 0 && i < 13) vn += rX[13 * (k - 1) + i];
-            v = (i < 13) ? vn : 0.0;
+            const double av = (i >= 6 && i < 9) ? (i == 6 ? v0 : i == 7 ? v1 : v2)
+                            : (i == 9) ? fma(cc, v3, -sn * v4) : (i == 10) ? fma(sn, v3, cc * v4) : (i == 11) ? v5 : 0.0;
+            double vn = fma(Ts, av, v + pk);
+            if (k > 0) vn += rX[13 * (k - 1) + i13];
+            v = m13 * vn;
         }
         const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
         SYNC();                                            // kff
@@ -473,41 +494,41 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         double prev = (ci == 12) ? ds0 : 0.0;
 #pragma clang loop unroll(disable)
         for (int k = 0; k < N; k++) {
-            const int ln = opq(lane), i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0;
+            const int ln = lane, i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0;
             const int gsrc = 16 * g + 4 * g, lsrc = 16 * g + 3 * g;   // lanes of components 4 g, 3 g (leg g's first force)
+            const double m12 = (i < 12) ? 1.0 : 0.0;
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k;
             const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
             // du = kff + K dx: this row's state columns j = 4 g + m
             double pk = 0.0;
 #pragma unroll
             for (int m = 0; m < 4; m++) {
-                const int j = 4 * g + m;
-                const double dj = perm_d(prev, gsrc + m);
-                if (j < 13) pk = fma((i < 12) ? Kk[13 * ir + j] : 0.0, dj, pk);
+                const int j = 4 * g + m, jc = (j < 13) ? j : 12;
+                const double dj = perm_d(prev, gsrc + m) * ((j < 13) ? 1.0 : 0.0);
+                pk = fma(Kk[13 * ir + jc], dj, pk);
             }
-            double du = rowsum(pk) + ((i < 12) ? L.kff[12 * k + i] : 0.0);
-            if (i >= 12) du = 0.0;
-            if (g == 0 && i < 12) L.dU[12 * k + i] = acc ? L.dU[12 * k + i] + du : du;
+            const double du = m12 * (rowsum(pk) + L.kff[12 * k + ir]);
+            {
+                double *pu = (g == 0 && i < 12) ? L.dU + 12 * k + i : sink;
+                *pu = acc ? *pu + du : du;
+            }
             // dx_{k+1} = A~ dx + B~ du: row g adds leg g's forces (and row 0 the A~ part)
             const double d0 = perm_d(du, lsrc), d1 = perm_d(du, lsrc + 1), d2 = perm_d(du, lsrc + 2);
-            double pb = 0.0;
-            if (i >= 6 && i < 9) pb = ct[g] * tsm * (i == 6 ? d0 : i == 7 ? d1 : d2);
-            else if (i >= 9 && i < 12) {
-                const double *w = W + 9 * g + 3 * (i - 9);
-                pb = fma(w[0], d0, fma(w[1], d1, w[2] * d2));
-            }
-            if (g == 0) {
-                const double p6 = bc16(prev, 6), p7 = bc16(prev, 7), p8 = bc16(prev, 8);
-                const double p9 = bc16(prev, 9), p10 = bc16(prev, 10), p11 = bc16(prev, 11);
-                double ax = prev;
-                if (i < 3) ax = fma(Ts, i == 0 ? p6 : i == 1 ? p7 : p8, ax);
-                else if (i < 6)
-                    ax = fma(Ts, i == 3 ? fma(cc, p9, sn * p10) : i == 4 ? fma(-sn, p9, cc * p10) : p11, ax);
-                pb += ax;
-            }
+            const int i9 = (i >= 9 && i < 12) ? i - 9 : 0;
+            const double *w = W + 9 * g + 3 * i9;
+            const double bv = ct[g] * tsm * (i == 6 ? d0 : i == 7 ? d1 : d2), bw = fma(w[0], d0, fma(w[1], d1, w[2] * d2));
+            double pb = (i >= 6 && i < 9) ? bv : (i >= 9 && i < 12) ? bw : 0.0;
+            const double p6 = bc16(prev, 6), p7 = bc16(prev, 7), p8 = bc16(prev, 8);
+            const double p9 = bc16(prev, 9), p10 = bc16(prev, 10), p11 = bc16(prev, 11);
+            const double ap = (i < 3) ? (i == 0 ? p6 : i == 1 ? p7 : p8)
+                            : (i == 3) ? fma(cc, p9, sn * p10) : (i == 4) ? fma(-sn, p9, cc * p10) : (i == 5) ? p11 : 0.0;
+            pb += (g == 0) ? fma(Ts, ap, prev) : 0.0;
             double dx = rowsum(pb);
             if (i > 12) dx = 0.0;
-            if (g == 0 && i < 13) L.dX[13 * k + i] = acc ? L.dX[13 * k + i] + dx : dx;
+            {
+                double *px = (g == 0 && i < 13) ? L.dX + 13 * k + i : sink;
+                *px = acc ? *px + dx : dx;
+            }
             prev = dx;
         }
         SYNC();
@@ -519,38 +540,41 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     auto refine = [&](double delta) {
         const double *rX = L.rX, *rU = L.rU, *dX = L.dX, *dU = L.dU;
         double *tX = L.gX, *tU = L.gU;
-        auto qdx = [&](int k, const double *dx, int i) {   // (Q^_k dx)[i]
-            double v = 0.0;
-            for (int j = 0; j < 13; j++) {
-                const bool nz = (j == i) || ((i < 2 || i == 12) && (j < 2 || j == 12));
-                if (nz) v = fma(qhat(k, i, j, delta), dx[j], v);
-            }
-            return v;
+        double *sink = L.T + 300 + ci;
+        auto qdx = [&](int k, const double *dx, int i) {   // (Q^_k dx)[i], branch-free
+            const double wd = ((k == N - 1) ? L.wqN : L.wq)[i < 12 ? i : 0];
+            const bool ob = i < 2 || i == 12;
+            const int a = (i == 12) ? 2 : (i < 2 ? i : 0);
+            const double *q3 = L.Q3 + 6 * k;               // symmetric (p_x, p_y, s) block, packed lower triangle
+            const double b0 = q3[tri(a, 0)], b1 = q3[tri(a, 1)], b2 = q3[tri(a, 2)];
+            return (i < 12 ? 1.0 : 0.0) * (wd + delta) * dx[i < 13 ? i : 0] +
+                   (ob ? 1.0 : 0.0) * fma(b0, dx[0], fma(b1, dx[1], b2 * dx[12]));
         };
         for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
         double m = (ci < 13) ? qdx(N - 1, dX + 13 * (N - 1), ci) + rX[13 * (N - 1) + ci] : 0.0;
 #pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
-            const int i = opq(lane) & 15, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
+            const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
             const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
             double vb[13];
 #pragma unroll
             for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
-            if (opq(lane) < 12) {
+            {
                 const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                double t = fma(L.wr[a3] + delta, du[a3], rU[12 * k + i]);
+                double t = fma(L.wr[a3] + delta, du[a3], rU[12 * k + ir]);
+#pragma unroll
                 for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
                 t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
+#pragma unroll
                 for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
-                tU[12 * k + i] = t;
+                *((lane < 12) ? tU + 12 * k + i : sink) = t;
             }
             if (k > 0) {
                 const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                double mn = m;
-                if (i >= 6 && i < 9) mn = fma(Ts, i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2], mn);
-                else if (i >= 9 && i < 12)
-                    mn = fma(Ts, i == 9 ? fma(cc, vb[3], -sn * vb[4]) : i == 10 ? fma(sn, vb[3], cc * vb[4]) : vb[5], mn);
-                m = (i < 13) ? mn + qdx(k - 1, dX + 13 * (k - 1), i) + rX[13 * (k - 1) + i] : 0.0;
+                const double av = (i >= 6 && i < 9) ? (i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2])
+                                : (i == 9) ? fma(cc, vb[3], -sn * vb[4]) : (i == 10) ? fma(sn, vb[3], cc * vb[4]) : (i == 11) ? vb[5] : 0.0;
+                const double mn = fma(Ts, av, m);
+                m = (i < 13 ? 1.0 : 0.0) * (mn + qdx(k - 1, dX + 13 * (k - 1), i) + rX[13 * (k - 1) + (i < 13 ? i : 0)]);
             }
         }
         const double m12 = bc16(m, 12);

@@ -190,7 +190,7 @@ static inline int srb12_lds_doubles(int N, int K)
 {
     return 36 * N + 2 * N + 4 * N                        // W_l, (cos, sin) psi, contact
            + 156 * N + 78 * N                           // K_k, Hu_k^-1 (packed) per grid
-           + 300                                        // factor transposes
+           + 316                                        // factor transposes (+ 16 sink entries)
            + 6 * N + 24 * N                             // (p_x, p_y, s) blocks, force blocks
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
            + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)
