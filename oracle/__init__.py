@@ -333,7 +333,7 @@ class Orc12Params(ctypes.Structure):
                 ("Sw", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
                 ("tol", ctypes.c_double), ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int),
                 ("use_nlp", ctypes.c_int), ("z0", ctypes.c_double),
-                ("tol_final", ctypes.c_double), ("polish", ctypes.c_int)]
+                ("tol_final", ctypes.c_double), ("polish", ctypes.c_int), ("tol_qp", ctypes.c_double)]
 
 
 def params12(N: int = 10, **kw) -> Orc12Params:

@@ -186,6 +186,7 @@ typedef struct orc12_params {
     double z0;                          /* NLP initial duals z0 / max(s, 1) */
     double tol_final;                   /* complementarity tolerance of the last stage (srb12_params) */
     int polish;                         /* 1: active-set polish of the last stage's result */
+    double tol_qp;                      /* the QP stage's tolerance when the NLP follows (srb12_params) */
 } orc12_params;
 
 void orc12_params_default(orc12_params *p, int N);

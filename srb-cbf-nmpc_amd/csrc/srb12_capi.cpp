@@ -75,6 +75,7 @@ extern "C" void srb12_params_default(srb12_params *p, int N)
     p->z0 = 100.0;
     p->tol_final = 1e-9;
     p->polish = 1;
+    p->tol_qp = 1e-3;
 }
 
 extern "C" int srb12_nv(const srb12_params *p) { return 24 * p->N + 1; }
@@ -96,8 +97,9 @@ static int validate12(const srb12_params *p)
     if (p->N < 1 || p->N > SRB12_MAX_N) return srb_internal_fail(SRB_ERR_SIZE, "SRB-12 mode: need 1 <= N <= 24");
     if (p->K_obs < 0 || p->K_nbr < 0 || p->K_obs > SRB_KNN_MAX || p->K_nbr > SRB_KNN_MAX)
         return srb_internal_fail(SRB_ERR_ARG, "K_obs, K_nbr out of range (each <= 16)");
-    if (!(p->mass > 0) || !(p->Ts > 0) || !(p->tol > 0) || !(p->tol_final > 0) || !(p->mu >= 0) || !(p->fmax > 0) || !(p->Sw > 0))
-        return srb_internal_fail(SRB_ERR_ARG, "srb12_params out of range (mass, Ts, tol, tol_final, fmax, Sw > 0)");
+    if (!(p->mass > 0) || !(p->Ts > 0) || !(p->tol > 0) || !(p->tol_final > 0) || !(p->mu >= 0) || !(p->fmax > 0) ||
+        !(p->Sw > 0) || !(p->tol_qp >= 0))
+        return srb_internal_fail(SRB_ERR_ARG, "srb12_params out of range (mass, Ts, tol, tol_final, fmax, Sw > 0, tol_qp >= 0)");
     for (int i = 0; i < 12; i++)
         if (!(p->q[i] >= 0) || !(p->qN[i] >= 0)) return srb_internal_fail(SRB_ERR_ARG, "state weights must be >= 0");
     for (int i = 0; i < 3; i++)
@@ -121,6 +123,7 @@ static Srb12KParams make_k12(const srb12_params *p, int K_obs, int K_nbr)
     k.qp_maxit = p->qp_maxit; k.nlp_maxit = p->nlp_maxit;
     k.Ts = p->Ts; k.mass = p->mass; k.grav = p->grav; k.mus = p->mu / std::sqrt(2.0); k.fmax = p->fmax;
     k.Sw = p->Sw; k.eps_obs = p->eps_obs; k.eps_nbr = p->eps_nbr; k.tol = p->tol; k.z0 = p->z0; k.tol_final = p->tol_final; k.polish = p->polish ? 1 : 0;
+    k.tol_qp = p->tol_qp;
     std::memcpy(k.Ib, p->Ib, sizeof k.Ib);
     std::memcpy(k.q, p->q, sizeof k.q); std::memcpy(k.qN, p->qN, sizeof k.qN); std::memcpy(k.r, p->r, sizeof k.r);
     return k;

@@ -61,7 +61,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     L.Wl = p; p += 36 * N;  L.cs = p; p += 2 * N;  L.ct = p; p += 4 * N;
     L.Kst = p; p += 156 * N;                                // K_k = -Hu^-1 Hux, 12 x 13 row-major per grid
     L.Hst = p; p += 78 * N;                                 // Hu_k^-1, packed lower triangle per grid
-    L.T = p; p += 316;                                      // factor transposes (column-major 12-row blocks) + 16 sink entries
+    L.T = p; p += 324;                                      // factor transposes (12-entry columns) + 24 sink entries
     L.Q3 = p; p += 6 * N; L.Rh = p; p += 24 * N;
     L.Z = p; p += 24 * N + 4; L.xr = p; p += 12 * N;
     L.rX = p; L.rU = p + 13 * N; L.gX = p + 25 * N; L.gU = p + 38 * N; L.xsv = p; p += 50 * N;
@@ -144,15 +144,6 @@ __device__ __forceinline__ double atil(int i, int j, double Ts, double c, double
     if (i >= 3 && i < 6 && j >= 9 && j < 12) v = Ts * rzab(j - 9, i - 3, c, s);
     return v;
 }
-// B~_k[i][j] (13 x 12: state row i, input j = 3 leg + axis; zero beyond)
-__device__ __forceinline__ double btil(int i, int j, const double *W, const double *ct, double tsm)
-{
-    if (j >= 12) return 0.0;
-    const int l = j / 3, a = j - 3 * l;
-    if (i >= 6 && i < 9) return (a == i - 6) ? ct[l] * tsm : 0.0;
-    if (i >= 9 && i < 12) return W[9 * l + 3 * (i - 9) + a];
-    return 0.0;
-}
 // value of x held by lane `src` (any 64-bit register): ds_bpermute, no LDS memory traffic
 __device__ __forceinline__ double perm_d(double x, int src)
 {
@@ -195,7 +186,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     const int N = NC > 0 ? NC : prm.N, K = K1 > 0 ? K1 - 1 : prm.K_obs + prm.K_nbr;
     const int NK = N * K, nv = 24 * N + 1, NL = 4 * N;
     const double Ts = prm.Ts, tsm = prm.Ts / prm.mass, mus = prm.mus;
-    const double tol = prm.tol, th = tol / sqrt(3.0);
+    const double tol = prm.tol;
     const int ci = lane & 15, gi = lane >> 4;          // column / component, 16-lane row
     Srb12Lds L = carve12(lds, N, K);
     double *X = L.Z, *U = L.Z + 12 * N;
@@ -283,6 +274,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     double ls[TL][6], lz[TL][6], lsa[TL][6], lza[TL][6];
     double os[TO], oz[TO], osa[TO], oza[TO];
     bool lon[TL], oon[TO];
+    bool obs_on = false;                                  // the stage has obstacle rows (uniform)
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
     const int nstage = prm.use_nlp ? 2 : 1;
     // obstacle row e at the current iterate: g, h and the Jacobian (c0, c1) on (p_x, p_y) (-1 on s)
@@ -374,14 +366,14 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             Hux = mfma(Bb1, G[1], Hux); Hux = mfma(Bb2, G[2], Hux);                // B~'G (12 x 13)
             Hu = mfma(Bb1, F[1], Hu); Hu = mfma(Bb2, F[2], Hu);                    // R^ + B~'F
             S12ST(10);  // factor: operands and the products
-            // to the column layout: Hu, Hux column-major in T (12 rows a column)
-            // (stores are unconditional: lanes outside a block write to the sink entries T[300..315])
-            const int sink = 300 + ci;
+            // to the column layout: Hu, Hux in T, 12 entries a column, row r at position 3 (r % 4) + r / 4 so
+            // that the three rows gi + 4 q an MFMA-layout lane holds are adjacent (merged LDS accesses).
+            // Stores are unconditional: lanes outside a block write to the sink entries T[300..323]
+            const int sink = 300;
+            {
+                double *bh = L.T + (ci < 12 ? 12 * ci + 3 * gi : sink), *bx = L.T + (ci < 13 ? 144 + 12 * ci + 3 * gi : sink + 4);
 #pragma unroll
-            for (int q = 0; q < 3; q++) {
-                const int i = gi + 4 * q;
-                L.T[ci < 12 ? 12 * ci + i : sink] = Hu[q];
-                L.T[ci < 13 ? 144 + 12 * ci + i : sink] = Hux[q];
+                for (int q = 0; q < 3; q++) { bh[q] = Hu[q]; bx[q] = Hux[q]; }
             }
             SYNC();
             // lane j < 12: column j of Hu; 12..24: column j - 12 of Hux; 25..36: column j - 25 of I
@@ -390,7 +382,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double *src = (lane < 12) ? L.T + 12 * lane : L.T + 144 + 12 * (lane < 25 ? lane - 12 : 0);
                 const double mc = (lane < 25) ? 1.0 : 0.0;
 #pragma unroll
-                for (int r = 0; r < 12; r++) col[r] = mc * src[r] + ((lane - 25 == r) ? 1.0 : 0.0);
+                for (int r = 0; r < 12; r++) col[r] = mc * src[3 * (r % 4) + r / 4] + ((lane - 25 == r) ? 1.0 : 0.0);
             }
             SYNC();
             S12ST(11);  // factor: to the column layout
@@ -413,19 +405,22 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             S12ST(12);  // factor: elimination
             // Y = D^-1/2 L^-1 Hux (lanes 12..24), Z = D^-1/2 L^-1 (lanes 25..36), back to T column-major
             {
-                const bool yz = lane >= 12 && lane < 37;
+                double *by = L.T + ((lane >= 12 && lane < 37) ? 12 * (lane - 12) : sink + 12);
 #pragma unroll
-                for (int r = 0; r < 12; r++) L.T[yz ? 12 * (lane - 12) + r : sink] = col[r] * dinv[r];
+                for (int r = 0; r < 12; r++) by[3 * (r % 4) + r / 4] = col[r] * dinv[r];
             }
             SYNC();
             // Y'Y (13 x 13), Hu^-1 = Z'Z (12 x 12), Z'Y = -K (12 x 13): operands Y[4 kb + gi][ci], Z[..][ci]
+            // (rows 4 kb + gi at positions 3 gi + kb: adjacent)
             d4 YY = {0.0, 0.0, 0.0, 0.0}, ZZ = {0.0, 0.0, 0.0, 0.0}, ZY = {0.0, 0.0, 0.0, 0.0};
+            {
+                const double *py = L.T + 12 * (ci < 13 ? ci : 12) + 3 * gi, *pz = L.T + 156 + 12 * (ci < 12 ? ci : 11) + 3 * gi;
+                const double my = (ci < 13) ? 1.0 : 0.0, mz = (ci < 12) ? 1.0 : 0.0;
 #pragma unroll
-            for (int kb = 0; kb < 3; kb++) {
-                const int r = 4 * kb + gi;
-                const double yt = L.T[12 * (ci < 13 ? ci : 12) + r], zt = L.T[156 + 12 * (ci < 12 ? ci : 11) + r];
-                const double ya = (ci < 13) ? yt : 0.0, za = (ci < 12) ? zt : 0.0;
-                YY = mfma(ya, ya, YY); ZZ = mfma(za, za, ZZ); ZY = mfma(za, ya, ZY);
+                for (int kb = 0; kb < 3; kb++) {
+                    const double ya = my * py[kb], za = mz * pz[kb];
+                    YY = mfma(ya, ya, YY); ZZ = mfma(za, za, ZZ); ZY = mfma(za, ya, ZY);
+                }
             }
             Vd = Vn - YY;                                  // V_{k-1} = Q^ + A~'G - Hux' Hu^-1 Hux
             double *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
@@ -433,7 +428,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             for (int q = 0; q < 3; q++) {
                 const int i = gi + 4 * q;
                 *(ci < 13 ? Kk + 13 * i + ci : L.T + sink) = -ZY[q];
-                *(ci <= i ? Hk + tri(i, ci) : L.T + sink) = ZZ[q];
+                *(ci <= i ? Hk + tri(i, ci) : L.T + sink + 1) = ZZ[q];
             }
             SYNC();
             S12ST(13);  // factor: Y, Z, the Schur / gain / inverse products, stores
@@ -601,11 +596,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         grad_f(L.rX, L.rU);
         if (tid == 0) L.sc[2] = prm.Sw * L.Z[24 * N];
         SYNC();
+        // (branch-free: a row that is not active contributes w = 0 through its mask, at a clamped index)
 #pragma unroll
         for (int t = 0; t < TL; t++) {
-            if (!lon[t]) continue;
-            const int e = lane + 64 * t;
-            const double *u = U + 3 * e;
+            const int e = lane + 64 * t, ec = e < NL ? e : 0;
+            const double mo = lon[t] ? 1.0 : 0.0;
+            const double *u = U + 3 * ec;
             double r[3] = {0.0, 0.0, 0.0};
 #pragma unroll
             for (int q = 0; q < 6; q++) {
@@ -615,23 +611,24 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double s = ls[t][q], z = lz[t][q], is = rcp_d(s);
                 const double rp = g + s - h, om = z * is;
                 const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
-                const double w = z + r3 * is + om * rp;
+                const double w = mo * (z + r3 * is + om * rp);
                 r[0] = fma(w, c0, r[0]); r[1] = fma(w, c1, r[1]); r[2] = fma(w, c2, r[2]);
             }
-            double *ru = L.rU + 3 * e;
-            ru[0] += r[0]; ru[1] += r[1]; ru[2] += r[2];
+            double *ru = (e < NL) ? L.rU + 3 * e : L.T + 300 + 4 * (lane & 3);   // (a lane past the legs: the sink,
+            ru[0] += r[0]; ru[1] += r[1]; ru[2] += r[2];                           //  never row 0's entries: a plain RMW)
         }
+        if (obs_on)
 #pragma unroll
         for (int t = 0; t < TO; t++) {
-            if (!oon[t]) continue;
-            const int e = lane + 64 * t;
+            const int e = lane + 64 * t, ec = oon[t] ? e : 0;
+            const double mo = oon[t] ? 1.0 : 0.0;
             double g, h, c0, c1;
-            obs_row(e, g, h, c0, c1);
+            obs_row(ec, g, h, c0, c1);
             const double s = os[t], z = oz[t], is = rcp_d(s);
             const double rp = g + s - h, om = z * is;
             const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
-            const double w = z + r3 * is + om * rp;
-            double *rx = L.rX + 13 * (e / K);
+            const double w = mo * (z + r3 * is + om * rp);
+            double *rx = L.rX + 13 * (ec / K);
             __hip_atomic_fetch_add(&rx[0], w * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&rx[1], w * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             __hip_atomic_fetch_add(&rx[12], -w, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -644,11 +641,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         double ms = 0.0, mz = 0.0;
 #pragma unroll
         for (int t = 0; t < TL; t++) {
-#pragma unroll
-            for (int q = 0; q < 6; q++) dls[t][q] = dlz[t][q] = 0.0;
-            if (!lon[t]) continue;
-            const int e = lane + 64 * t;
-            const double *u = U + 3 * e, *du = L.dU + 3 * e;
+            const int e = lane + 64 * t, ec = e < NL ? e : 0;
+            const double mo = lon[t] ? 1.0 : 0.0;
+            const double *u = U + 3 * ec, *du = L.dU + 3 * ec;
 #pragma unroll
             for (int q = 0; q < 6; q++) {
                 double c0, c1, c2;
@@ -659,25 +654,26 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 const double rp = g + s - h;
                 const double r3 = -s * z + (pass ? smu - lsa[t][q] * lza[t][q] : 0.0);
                 const double is = rcp_d(s);
-                dls[t][q] = -rp - jd; dlz[t][q] = (r3 - z * dls[t][q]) * is;
-                ms = fmax(ms, -dls[t][q] * is); mz = fmax(mz, -dlz[t][q] * rcp_d(z));
+                dls[t][q] = mo * (-rp - jd); dlz[t][q] = mo * (r3 - z * dls[t][q]) * is;
+                ms = fmax(ms, -dls[t][q] * is); mz = fmax(mz, -dlz[t][q] * rcp_d(z + (1.0 - mo)));
             }
         }
 #pragma unroll
         for (int t = 0; t < TO; t++) {
             dos[t] = doz[t] = 0.0;
-            if (!oon[t]) continue;
-            const int e = lane + 64 * t;
+            if (!obs_on) continue;
+            const int e = lane + 64 * t, ec = oon[t] ? e : 0;
+            const double mo = oon[t] ? 1.0 : 0.0;
             double g, h, c0, c1;
-            obs_row(e, g, h, c0, c1);
-            const double *dx = L.dX + 13 * (e / K);
+            obs_row(ec, g, h, c0, c1);
+            const double *dx = L.dX + 13 * (ec / K);
             const double jd = c0 * dx[0] + c1 * dx[1] - dx[12];
             const double s = os[t], z = oz[t];
             const double rp = g + s - h;
             const double r3 = -s * z + (pass ? smu - osa[t] * oza[t] : 0.0);
             const double is = rcp_d(s);
-            dos[t] = -rp - jd; doz[t] = (r3 - z * dos[t]) * is;
-            ms = fmax(ms, -dos[t] * is); mz = fmax(mz, -doz[t] * rcp_d(z));
+            dos[t] = mo * (-rp - jd); doz[t] = mo * (r3 - z * dos[t]) * is;
+            ms = fmax(ms, -dos[t] * is); mz = fmax(mz, -doz[t] * rcp_d(z + (1.0 - mo)));
         }
         double rv[2] = {ms, mz};
         wred<2, 3u>(rv);
@@ -688,6 +684,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
+        obs_on = nl && NK > 0;
         // active rows and the starting slacks / duals (oracle ipm(): QP s = h - g, z = 1 / max(s, 1);
         // NLP shifted so min s = 1 when a row is violated, z = z0 / max(s, 1))
         double mcount = 0.0, mn = 1e300;
@@ -738,8 +735,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         }
         const double inv_m = 1.0 / fmax(mcount, 1.0);
         const int maxit = nl ? prm.nlp_maxit : prm.qp_maxit;
-        // the last stage's complementarity test is tol_final (the forces' accuracy: DESIGN.md 11)
-        const double mtol = (stage == nstage - 1) ? prm.tol_final : tol;
+        // a QP stage that the NLP follows runs to tol_qp (the NLP's warm start only); the last stage's
+        // complementarity test is tol_final (the forces' accuracy: DESIGN.md 11); oracle/srb12.c the same
+        const double tol_s = (!nl && prm.use_nlp && prm.tol_qp > 0.0) ? prm.tol_qp : tol, th_s = tol_s / sqrt(3.0);
+        const double mtol = (stage == nstage - 1) ? prm.tol_final : tol_s;
         int flag = 2, it = 0;
         double sigma = 0.0;
 #pragma clang loop unroll(disable)
@@ -753,44 +752,47 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             double nrp = 0.0, sz = 0.0, zmx = 0.0;
 #pragma unroll
             for (int t = 0; t < TL; t++) {
-                const int e = lane + 64 * t;
-                if (e >= NL) continue;
+                // branch-free: a leg out of range or in swing has z = 0 (rh, gz vanish) and a masked r_p;
+                // its stores go to the sink
+                const int e = lane + 64 * t, ec = e < NL ? e : 0;
+                const double mo = lon[t] ? 1.0 : 0.0;
                 double gz[3] = {0.0, 0.0, 0.0}, rh[6] = {0.0, 0.0, 0.0, 0.0, 0.0, 0.0};
-                if (lon[t]) {
-                    const double *u = U + 3 * e;
+                const double *u = U + 3 * ec;
 #pragma unroll
-                    for (int q = 0; q < 6; q++) {
-                        double c0, c1, c2;
-                        fric_coef(q, mus, c0, c1, c2);
-                        const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
-                        const double s = ls[t][q], z = lz[t][q];
-                        const double rp = g + s - h, om = z * rcp_d(s);
-                        nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
-                        const double cc[3] = {c0, c1, c2};
+                for (int q = 0; q < 6; q++) {
+                    double c0, c1, c2;
+                    fric_coef(q, mus, c0, c1, c2);
+                    const double g = c0 * u[0] + c1 * u[1] + c2 * u[2], h = (q == 5) ? prm.fmax : 0.0;
+                    const double s = ls[t][q], z = mo * lz[t][q];
+                    const double rp = mo * (g + s - h), om = z * rcp_d(s);
+                    nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
+                    const double cc[3] = {c0, c1, c2};
 #pragma unroll
-                        for (int a = 0; a < 3; a++) {
-                            gz[a] = fma(z, cc[a], gz[a]);
+                    for (int a = 0; a < 3; a++) {
+                        gz[a] = fma(z, cc[a], gz[a]);
 #pragma unroll
-                            for (int b = a; b < 3; b++) rh[sym3(a, b)] = fma(om * cc[a], cc[b], rh[sym3(a, b)]);
-                        }
+                        for (int b = a; b < 3; b++) rh[sym3(a, b)] = fma(om * cc[a], cc[b], rh[sym3(a, b)]);
                     }
-                    double *gu = L.gU + 3 * e;
-                    gu[0] += gz[0]; gu[1] += gz[1]; gu[2] += gz[2];
                 }
+                double *gu = (e < NL) ? L.gU + 3 * e : L.T + 300 + 4 * (lane & 3);
+                gu[0] += gz[0]; gu[1] += gz[1]; gu[2] += gz[2];
+                double *rhp = (e < NL) ? L.Rh + 6 * e : L.T + 300;
 #pragma unroll
-                for (int m = 0; m < 6; m++) L.Rh[6 * e + m] = rh[m];
+                for (int m = 0; m < 6; m++) rhp[m] = rh[m];
             }
+            if (obs_on)
 #pragma unroll
             for (int t = 0; t < TO; t++) {
-                if (!oon[t]) continue;
-                const int e = lane + 64 * t;
+                // branch-free: a lane past the last row adds zeros to row 0's grid
+                const int e = lane + 64 * t, ec = oon[t] ? e : 0;
+                const double mo = oon[t] ? 1.0 : 0.0;
                 double g, h, c0, c1;
-                obs_row(e, g, h, c0, c1);
-                const double s = os[t], z = oz[t];
-                const double rp = g + s - h, om = z * rcp_d(s);
+                obs_row(ec, g, h, c0, c1);
+                const double s = os[t], z = mo * oz[t];
+                const double rp = mo * (g + s - h), om = z * rcp_d(s);
                 nrp = fma(rp, rp, nrp); sz = fma(s, z, sz); zmx = fmax(zmx, z);
                 // obstacle row of grid k on (p_x, p_y, s): J = (c0, c1, -1), Lagrangian Hessian -2z on p_x, p_y
-                const int k = e / K;
+                const int k = ec / K;
                 double *gx = L.gX + 13 * k, *q3 = L.Q3 + 6 * k;
                 __hip_atomic_fetch_add(&gx[0], z * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&gx[1], z * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
@@ -823,20 +825,19 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                     const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
                     const double v6 = bc16(lam, 6), v7 = bc16(lam, 7), v8 = bc16(lam, 8);
                     const double v9 = bc16(lam, 9), v10 = bc16(lam, 10), v11 = bc16(lam, 11);
-                    if (lane < 12) {
-                        double ru = fma(ct[l] * tsm, jj == 0 ? v6 : jj == 1 ? v7 : v8, L.gU[12 * k + i]);
+                    {
+                        double ru = fma(ct[l] * tsm, jj == 0 ? v6 : jj == 1 ? v7 : v8, L.gU[12 * k + ir]);
                         ru = fma(W[9 * l + jj], v9, ru); ru = fma(W[9 * l + 3 + jj], v10, ru); ru = fma(W[9 * l + 6 + jj], v11, ru);
+                        ru *= (lane < 12) ? 1.0 : 0.0;
                         nrd = fma(ru, ru, nrd);
                     }
                     if (k > 0) {
                         const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
                         const double v0 = bc16(lam, 0), v1 = bc16(lam, 1), v2 = bc16(lam, 2);
                         const double v3 = bc16(lam, 3), v4 = bc16(lam, 4), v5 = bc16(lam, 5);
-                        double ln = lam;
-                        if (i >= 6 && i < 9) ln = fma(Ts, i == 6 ? v0 : i == 7 ? v1 : v2, ln);
-                        else if (i >= 9 && i < 12)
-                            ln = fma(Ts, i == 9 ? fma(cc, v3, -sn * v4) : i == 10 ? fma(sn, v3, cc * v4) : v5, ln);
-                        lam = (i < 13) ? ln + L.gX[13 * (k - 1) + i] : 0.0;
+                        const double av = (i >= 6 && i < 9) ? (i == 6 ? v0 : i == 7 ? v1 : v2)
+                                        : (i == 9) ? fma(cc, v3, -sn * v4) : (i == 10) ? fma(sn, v3, cc * v4) : (i == 11) ? v5 : 0.0;
+                        lam = ((i < 13) ? 1.0 : 0.0) * (fma(Ts, av, lam) + L.gX[13 * (k - 1) + (i < 13 ? i : 0)]);
                     }
                 }
                 const double l12 = bc16(lam, 12);
@@ -849,12 +850,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             const double mu = sz * inv_m;
             double *dbgrow = (agent == prm.dbg_agent && prm.dbg && it < 64) ? prm.dbg + 8 * (64 * stage + it) : nullptr;
-            if (dbgrow && tid == 0) { dbgrow[0] = nrd; dbgrow[1] = th * gm; dbgrow[2] = nrp; dbgrow[3] = mu; }
+            if (dbgrow && tid == 0) { dbgrow[0] = nrd; dbgrow[1] = th_s * gm; dbgrow[2] = nrp; dbgrow[3] = mu; }
             // divergence (the LIP mode's rule, SRB_Z_DIV; oracle/srb12.c the same): a dual beyond 1e10 means
             // infeasible rows -- FATAL at this finite iterate
             if (!isfinite(nrd) || !isfinite(nrp) || !isfinite(sz) || !(zmx <= SRB_Z_DIV)) { flag = 3; break; }
             S12ST(1);   // residuals, weights, scatter, costates
-            if (nrd < th * gm && nrp < th && mu < mtol) { flag = 0; break; }
+            if (nrd < th_s * gm && nrp < th_s && mu < mtol) { flag = 0; break; }
 
             // ---- factorisation (backward Riccati over the 13-state) with the inertia shift delta (NLP)
             double dmax = 1.0;

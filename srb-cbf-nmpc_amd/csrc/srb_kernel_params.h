@@ -162,7 +162,7 @@ struct SrbLLKParams {
 struct Srb12KParams {
     int N, K_obs, K_nbr, use_nlp;
     int qp_maxit, nlp_maxit, polish;
-    double Ts, mass, grav, mus, fmax, Sw, eps_obs, eps_nbr, tol, z0, tol_final;
+    double Ts, mass, grav, mus, fmax, Sw, eps_obs, eps_nbr, tol, z0, tol_final, tol_qp;
     double Ib[9];                     // body inertia (fast_MPC.cpp:41-43)
     double q[12], qN[12], r[3];       // stage / terminal state weights, force weights
     int dbg_agent;                    // >= 0: that agent records a per-iteration trace into dbg
@@ -190,7 +190,7 @@ static inline int srb12_lds_doubles(int N, int K)
 {
     return 36 * N + 2 * N + 4 * N                        // W_l, (cos, sin) psi, contact
            + 156 * N + 78 * N                           // K_k, Hu_k^-1 (packed) per grid
-           + 316                                        // factor transposes (+ 16 sink entries)
+           + 324                                        // factor transposes (+ 24 sink entries)
            + 6 * N + 24 * N                             // (p_x, p_y, s) blocks, force blocks
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
            + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)

@@ -21,7 +21,7 @@ _p12_fields = [("N", ctypes.c_int), ("K_obs", ctypes.c_int), ("K_nbr", ctypes.c_
                ("Sw", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
                ("tol", ctypes.c_double), ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int),
                ("use_nlp", ctypes.c_int), ("z0", ctypes.c_double),
-               ("tol_final", ctypes.c_double), ("polish", ctypes.c_int)]
+               ("tol_final", ctypes.c_double), ("polish", ctypes.c_int), ("tol_qp", ctypes.c_double)]
 
 
 class Params12(ctypes.Structure):
