@@ -135,10 +135,12 @@ __device__ __forceinline__ int rnd4(int x) { return (x + 3) & ~3; }
 // value of lane k of this lane's 16-lane row: one v_mov_b64_dpp row_newbcast:k (gfx90a+),
 // a VALU result the next instruction can consume -- no SGPR round trip as with readlane.
 // k must fold to a constant (unrolled loops).
+// (row_newbcast writes every lane, so the "old" operand is never used: passing v with bound_ctrl
+// lets the compiler emit the DPP move alone, without first zeroing its destination)
 __device__ __forceinline__ double bc16(double v, int k)
 {
     switch (k) {
-#define SRB_BC(K) case K: return __builtin_amdgcn_update_dpp(0.0, v, 0x150 + K, 0xf, 0xf, false);
+#define SRB_BC(K) case K: return __builtin_amdgcn_update_dpp(v, v, 0x150 + K, 0xf, 0xf, true);
     SRB_BC(0) SRB_BC(1) SRB_BC(2) SRB_BC(3) SRB_BC(4) SRB_BC(5) SRB_BC(6) SRB_BC(7)
     SRB_BC(8) SRB_BC(9) SRB_BC(10) SRB_BC(11) SRB_BC(12) SRB_BC(13) SRB_BC(14) default: SRB_BC(15)
 #undef SRB_BC
