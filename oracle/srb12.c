@@ -202,7 +202,7 @@ static int reduced_pd(const p12_t *P, const double *Hf)
  * 1e-3 N from the optimum there; the active set's KKT point is exact. */
 #define ORC12_POL_RHO 1e9
 #define ORC12_POL_KAPPA 1e4
-#define ORC12_POL_IT 3
+#define ORC12_POL_IT 5
 #define ORC12_POL_PASSES 2
 #define ORC12_POL_PTOL 1e-9
 #define ORC12_POL_DXTOL 1e-7

@@ -83,7 +83,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
             __builtin_amdgcn_sched_barrier(0);                                                       \
             const unsigned long long t_ = __builtin_amdgcn_s_memtime();                              \
             __builtin_amdgcn_sched_barrier(0);                                                       \
-            if (tid == 0) prm.dbg[SRB12_DBG_TRACE + (slot)] += (double)(t_ - tprev);                  \
+            if (tid == 0) stl[slot] += (double)(t_ - tprev);  /* LDS: no global round trip per stamp */ \
             tprev = t_;                                                                              \
         }                                                                                            \
     } while (0)
@@ -193,6 +193,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     const double *x0 = x0g + 12 * (size_t)agent;
 #ifdef SRB12_STAMPS
     const bool dstamp = agent == prm.dbg_agent && prm.dbg != nullptr;
+    double *stl = (double *)L.sel + K + 2;              // 16 stamp accumulators (srb12_lds_doubles)
+    if (tid < 16) stl[tid] = 0.0;
     unsigned long long tprev = dstamp ? __builtin_amdgcn_s_memtime() : 0ull;
 #endif
 
@@ -1159,6 +1161,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         SYNC();
         S12ST(9);
     }
+#ifdef SRB12_STAMPS
+    SYNC();
+    if (dstamp && tid < 16) prm.dbg[SRB12_DBG_TRACE + tid] += stl[tid];
+#endif
     // ---- outputs: x and 0.5 x'Px + c'x
     double f = 0.0;
     for (int v = tid; v < nv; v += 64) {

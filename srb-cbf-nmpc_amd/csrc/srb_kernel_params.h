@@ -172,7 +172,7 @@ struct Srb12KParams {
 // active-set polish of the last stage's result (oracle/srb12.c ORC12_POL_*, the same constants)
 #define SRB12_POL_RHO 1e9
 #define SRB12_POL_KAPPA 1e4
-#define SRB12_POL_IT 3
+#define SRB12_POL_IT 5
 #define SRB12_POL_PASSES 2
 #define SRB12_POL_PTOL 1e-9
 #define SRB12_POL_DXTOL 1e-7
@@ -196,5 +196,6 @@ static inline int srb12_lds_doubles(int N, int K)
            + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)
            + 13 * N + 12 * N + 12 * N                   // solution, feed-forward -Hu^-1 gu
            + 16 + 16 + 28                               // vector, scalars, the weights q, qN, r
-           + 2 * N * K + K + K + 2;                     // obstacle positions, eps, sel (as ints)
+           + 2 * N * K + K + K + 2                      // obstacle positions, eps, sel (as ints)
+           + 16;                                        // stamp accumulators (diagnostic build make s12st)
 }
