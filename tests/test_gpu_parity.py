@@ -297,14 +297,18 @@ def test_fused_polish_equals_separate_polish_kernel():
     Same algorithm from the same float z snapshot, so the results agree to round-off (the two
     kernels run at different waves per agent, so the reduction orders differ) and every status
     is identical; both match the oracle at NLP_TOL."""
-    for (N, C, Ko, Kn, A, seed) in [(10, 2, 3, 8, 1024, 5), (10, 4, 1, 0, 256, 6)]:
+    # (10, 4): nz = N (C - 1) + 1 = 31 > 16, an instance that does not fuse: both launches use the kernel
+    for (N, C, Ko, Kn, A, seed, fuses) in [(10, 2, 3, 8, 1024, 5, True), (10, 4, 1, 0, 256, 6, False)]:
         b = workload.make_batch(A, N, C, seed=seed)
         p = srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn)
         s = srbnmpc.BatchSolver(p, A)
         try:
             assert s.get_option("polish_fused") == 1.0
             fu = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
-            assert s.get_option("last_polish") == 2.0 and s.last_polish_ms() == 0.0
+            if fuses:
+                assert s.get_option("last_polish") == 2.0 and s.last_polish_ms() == 0.0
+            else:
+                assert s.get_option("last_polish") == 1.0
             s.set_option("polish_fused", 0)
             se = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
             assert s.get_option("last_polish") == 1.0
