@@ -145,7 +145,10 @@ int srb_ctx_waves(srb_ctx *ctx);
  *   SRB_OPT_POLISH_FUSED         1 (default) the polish runs at the end of the solve kernel (problems with
  *                                N(C-1)+1 <= 16), 0 as a kernel of its own after it; the same results
  *   SRB_OPT_LAST_POLISH          read only: how the last launch polished, 0 not at all, 1 polish kernel,
- *                                2 fused into the solve kernel */
+ *                                2 fused into the solve kernel
+ *   SRB_OPT_TIMING               1 (default): HIP events around the launch's kernels (srb_last_kernel_ms,
+ *                                srb_last_polish_ms); 0: none (each event record is a marker the queue
+ *                                drains to: a few us per call, measured in bench.py's timed loop) */
 #define SRB_OPT_POLISH 1
 #define SRB_OPT_POLISH_RHO 2
 #define SRB_OPT_POLISH_WAVES 3
@@ -153,6 +156,7 @@ int srb_ctx_waves(srb_ctx *ctx);
 #define SRB_OPT_GRID_MIN_ROWS_STATIC 5
 #define SRB_OPT_POLISH_FUSED 6
 #define SRB_OPT_LAST_POLISH 7
+#define SRB_OPT_TIMING 8
 int srb_ctx_set_option(srb_ctx *ctx, int opt, double value);
 int srb_ctx_get_option(srb_ctx *ctx, int opt, double *value);
 
@@ -366,6 +370,8 @@ int srb12_solve_batch(srb12_ctx *ctx, int n_agents, const srb12_batch *host_io);
 int srb12_solve_batch_device(srb12_ctx *ctx, int n_agents, const srb12_batch *dev_io, void *stream);
 /* HIP-event times of the last call's selection and solve kernels (ms) */
 int srb12_last_kernel_ms(srb12_ctx *ctx, float *select_ms, float *solve_ms);
+/* 1 (default): HIP events around the selection and solve kernels (srb12_last_kernel_ms); 0: none */
+int srb12_ctx_set_timing(srb12_ctx *ctx, int on);
 int srb12_lds_bytes(const srb12_params *p);
 
 const char *srb_last_error(void);

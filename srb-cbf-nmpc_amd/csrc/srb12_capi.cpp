@@ -48,6 +48,7 @@ struct srb12_ctx {
     hipEvent_t done;
     hipStream_t last;
     bool timed, any;
+    int timing;                    // srb12_ctx_set_timing (default 1)
     double *pos;                   // [max_agents][4] CoM rows for the selection
     int *sel;                      // [max_agents][2 SRB_KNN_MAX]
     double *x0, *xref, *foot, *obstacles, *nbr, *x_qp, *x, *obj;
@@ -173,7 +174,7 @@ extern "C" int srb12_ctx_create(const srb12_params *p, int max_agents, int devic
     CREATE_CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     CREATE_CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
     CREATE_CHK(hipMalloc(&c->dbg, (2 * 64 * 8 + 16) * sizeof(double)));
-    c->dbg_agent = -1;
+    c->dbg_agent = -1; c->timing = 1;
 #undef CREATE_CHK
     *out = c;
     return SRB_OK;
@@ -235,7 +236,7 @@ static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_
     if (!in) return srb_internal_fail(SRB_ERR_SIZE, "no SRB-12 kernel instance covers the row slots");
     const size_t lds = (size_t)srb12_lds_doubles(p->N, Ko + Kn) * sizeof(double);
     int *sel = d->sel ? d->sel : c->sel;
-    H12CHK(hipEventRecord(c->ev[0], s));
+    if (c->timing) H12CHK(hipEventRecord(c->ev[0], s));
     if (Ko + Kn > 0) {
         hipLaunchKernelGGL(srb12_pos_kernel, dim3((n_agents + 255) / 256), dim3(256), 0, s, n_agents, d->x0, c->pos);
         H12CHK(hipGetLastError());
@@ -246,12 +247,12 @@ static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_
         // this launch (grid_reserve waits on it)
         if ((rc = srb_internal_mark_done(c->sel_ctx, s))) return rc;
     }
-    H12CHK(hipEventRecord(c->ev[1], s));
+    if (c->timing) H12CHK(hipEventRecord(c->ev[1], s));
     hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64), lds, s, k, n_agents, d->x0, d->xref, d->foot, d->contact,
                        d->obstacles, d->nbr_state, (const int *)sel, d->x_qp, d->x, d->obj, d->status, d->iters);
     H12CHK(hipGetLastError());
-    H12CHK(hipEventRecord(c->ev[2], s));
-    c->timed = true;
+    if (c->timing) H12CHK(hipEventRecord(c->ev[2], s));
+    c->timed = c->timing != 0;
     return SRB_OK;
 }
 
@@ -334,6 +335,13 @@ extern "C" int srb12_solve_batch(srb12_ctx *c, int n_agents, const srb12_batch *
         if (Kt > 0) H12CHK(hipMemcpyAsync(h->sel, c->sel, A * Kt * sizeof(int), hipMemcpyDeviceToHost, s));
     }
     H12CHK(hipStreamSynchronize(s));
+    return SRB_OK;
+}
+
+extern "C" int srb12_ctx_set_timing(srb12_ctx *c, int on)
+{
+    if (!c) return srb_internal_fail(SRB_ERR_ARG, "null ctx");
+    c->timing = on ? 1 : 0;
     return SRB_OK;
 }
 

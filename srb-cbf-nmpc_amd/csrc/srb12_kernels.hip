@@ -39,6 +39,12 @@
 #ifndef SRB12_REFINE_PREDICTOR        // 1: refine the predictor's solve too (round-3 behaviour)
 #define SRB12_REFINE_PREDICTOR 0
 #endif
+#ifndef SRB12_REFINE                  // 0: no iterative refinement at all (A/B builds)
+#define SRB12_REFINE 1
+#endif
+#ifndef SRB12_REFINE_MU               // the corrector's solve is refined once mu < this
+#define SRB12_REFINE_MU 1e-3
+#endif
 
 #define SYNC() __syncthreads()
 #include "srb_wave.h"
@@ -884,7 +890,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // (the refinement only near the optimum, mu < 1e-3, and only of the corrector: far from the
             // optimum the step's accuracy is not what limits progress, and the predictor only sets sigma
             // and the second-order term; each refinement costs a solve)
-            const bool refn = mu < 1e-3;
+            const bool refn = mu < SRB12_REFINE_MU;
             sph = 4;
             build_rhs(0, 0.0);
             riccati_solve(0, false);
@@ -919,7 +925,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             sph = 6;
             build_rhs(1, sigma * mu);
             riccati_solve(0, false);
-            if (refn) refine(delta);
+            if (SRB12_REFINE && refn) refine(delta);
             S12ST(6);   // corrector rhs + solve (+ refinement)
             al = row_step(1, sigma * mu, dls, dlz, dos, doz);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);

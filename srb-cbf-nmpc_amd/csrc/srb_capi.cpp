@@ -117,6 +117,7 @@ struct srb_ctx {
     // agent, the selection-grid thresholds
     int polish, polish_waves, grid_min_rows, grid_min_rows_static, polish_fused;
     int last_polish;               // how the last launch polished: 0 no, 1 polish kernel, 2 fused
+    int timing;                    // 1: HIP events around the kernels (srb_last_kernel_ms); 0: none
     double polish_rho;
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
@@ -306,7 +307,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
-    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -424,8 +425,9 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     c->last_nw = in->nw;
     HIPCHK(hipSetDevice(c->device));
     const int n_obs = k.K_obs > 0 ? d->n_obs : 0, n_all = k.K_nbr > 0 ? d->n_all : 0;
-    c->timed = true;
-    HIPCHK(hipEventRecord(c->ev[0], s));
+    // timing events (SRB_OPT_TIMING): each record is a marker the queue drains to, a few us a step
+    c->timed = c->timing != 0;
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
     // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
     int *sel = d->sel ? d->sel : c->sel;
     if (use_nlp && k.K_obs + k.K_nbr > 0) {
@@ -433,7 +435,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
                                k.K_nbr, d->obstacles_version, sel, s);
         if (rc) return rc;
     }
-    HIPCHK(hipEventRecord(c->ev[2], s));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
     // the solve kernel, then (NLP stage) the active-set polish of its result: fused into the solve
     // kernel's end (SRB_OPT_POLISH_FUSED, instances up to NZL 16), else srb_polish_kernel (same instance
     // geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
@@ -446,7 +448,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
                        polish ? c->zpol : nullptr, c->zstride);
     HIPCHK(hipGetLastError());
-    HIPCHK(hipEventRecord(c->ev[3], s));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[3], s));
     if (polish) {
         // the polish kernel reads only the solve's outputs (x, status, sel, zpol by global slot
         // index), so it runs at its own waves per agent: at least two (its registers fit two
@@ -462,7 +464,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
                            d->alpha_buf ? d->alpha : nullptr, (const int *)sel, (const float *)c->zpol, c->zstride);
         HIPCHK(hipGetLastError());
     }
-    HIPCHK(hipEventRecord(c->ev[1], s));
+    if (c->timing) HIPCHK(hipEventRecord(c->ev[1], s));
     return SRB_OK;
 }
 
@@ -495,6 +497,9 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
         c->polish_fused = (int)v; return SRB_OK;
     case SRB_OPT_LAST_POLISH:
         return fail(SRB_ERR_ARG, "SRB_OPT_LAST_POLISH is read only");
+    case SRB_OPT_TIMING:
+        if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_TIMING: 0 or 1");
+        c->timing = (int)v; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS:
     case SRB_OPT_GRID_MIN_ROWS_STATIC:
         if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
@@ -516,6 +521,7 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_GRID_MIN_ROWS_STATIC: *v = c->grid_min_rows_static; return SRB_OK;
     case SRB_OPT_POLISH_FUSED: *v = c->polish_fused; return SRB_OK;
     case SRB_OPT_LAST_POLISH: *v = c->last_polish; return SRB_OK;
+    case SRB_OPT_TIMING: *v = c->timing; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }

@@ -59,6 +59,7 @@ def _lib():
         L.srb12_solve_batch.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch12)]
         L.srb12_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch12), ctypes.c_void_p]
         L.srb12_last_kernel_ms.argtypes = [ctypes.c_void_p, ctypes.POINTER(ctypes.c_float), ctypes.POINTER(ctypes.c_float)]
+        L.srb12_ctx_set_timing.argtypes = [ctypes.c_void_p, ctypes.c_int]
         _bound = True
     return L
 
@@ -155,6 +156,10 @@ class Solver12:
         a, b = ctypes.c_float(), ctypes.c_float()
         _check(_lib().srb12_last_kernel_ms(self._h, ctypes.byref(a), ctypes.byref(b)))
         return a.value, b.value
+
+    def set_timing(self, on: bool):
+        """HIP events around the kernels (srb12_ctx_set_timing; default on): last_kernel_ms needs them."""
+        _check(_lib().srb12_ctx_set_timing(self._h, 1 if on else 0))
 
 
 def split(p: Params12, x):
