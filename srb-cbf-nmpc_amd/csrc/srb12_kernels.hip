@@ -756,6 +756,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             for (int e = tid; e < 6 * N; e += 64) L.Q3[e] = 0.0;
             if (tid == 0) { L.sc[0] = prm.Sw * L.Z[24 * N]; L.sc[1] = prm.Sw; }    // grad_s f, H_ss (inertia scale)
             SYNC();
+            S12ST(3);   // (stamps: the gradient; slot 3 also takes the factor -> predictor gap)
             // ---- rows: residuals, weights, J'z and J'WJ into the per-grid blocks
             double nrp = 0.0, sz = 0.0, zmx = 0.0;
 #pragma unroll
@@ -814,6 +815,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 __hip_atomic_fetch_add(&L.sc[1], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
             }
             SYNC();
+            S12ST(8);   // (stamps: the rows; slot 8 also takes the exit test -> polish gap)
             // ---- costates and the dual residual (13-state: the slack rides along as x[12], s_{k+1} = s_k):
             //      lam_{N-1} = gX_{N-1}, lam_{k-1} = gX_{k-1} + A~_k' lam_k, r_u,k = gU_k + B_k' lam_k,
             //      r_s = Sw s + lam_0[12] (the free initial slack)

@@ -323,6 +323,26 @@ def test_fused_polish_equals_separate_polish_kernel():
         np.testing.assert_allclose(xus(N, fu["x"][:128]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
+def test_timing_option_changes_nothing_but_the_events():
+    """SRB_OPT_TIMING = 0 (bench.py's timed loop): no HIP events around the kernels, so the kernel
+    times are unavailable, and the results are bit-identical to a timed launch."""
+    N, C, Ko, Kn, A = 10, 2, 3, 8, 256
+    b = workload.make_batch(A, N, C, seed=9)
+    s = srbnmpc.BatchSolver(srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn), A)
+    try:
+        on = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+        assert s.last_kernel_ms()[1] > 0.0
+        s.set_option("timing", 0)
+        assert s.get_option("timing") == 0.0
+        off = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+        with pytest.raises(RuntimeError):
+            s.last_kernel_ms()
+    finally:
+        s.close()
+    for k in ("x", "obj", "status", "iters"):
+        np.testing.assert_array_equal(on[k], off[k])
+
+
 def test_config5_full_size_vs_oracle_and_acceptable_exit():
     """bench config 5 (2048 agents, N = 20, 3 static + 8 neighbour rows) at full size, EVERY
     agent within NLP_TOL (1e-4) of the oracle in X, U, s.

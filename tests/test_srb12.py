@@ -341,6 +341,12 @@ def test_srb12_abi_rejects_bad_arguments():
     p = srb12.default_params(N)
     p.r[1] = 0.0
     assert L.srb12_ctx_create(ctypes.byref(p), 4, 0, ctypes.byref(h)) == -1        # SRB_ERR_ARG
+    p = srb12.default_params(N)
+    assert p.tol_qp == 1e-3
+    p.tol_qp = -1e-3
+    assert L.srb12_ctx_create(ctypes.byref(p), 4, 0, ctypes.byref(h)) == -1        # SRB_ERR_ARG
+    assert b"tol_qp" in srbnmpc_last_error()
+    assert L.srb12_ctx_set_timing(None, 0) == -1
 
 
 def srbnmpc_last_error():

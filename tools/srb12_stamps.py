@@ -11,9 +11,9 @@ import numpy as np  # noqa: E402
 
 from srbnmpc import srb12, workload  # noqa: E402
 
-PHASES = ["inputs/model/rollout", "residuals+costates", "Riccati factor", "factor->predictor",
+PHASES = ["inputs/model/rollout", "costates+norms+exit", "Riccati factor", "gradient (+factor->pred)",
           "predictor rhs+solve", "predictor step+sigma", "corrector rhs+solve", "corrector step+update",
-          "exit test->polish", "active-set polish", "factor: products", "factor: to columns",
+          "row loops (+exit->polish)", "active-set polish", "factor: products", "factor: to columns",
           "factor: elimination", "factor: Y Z products, stores", "solve: backward sweep", "solve: forward sweep"]
 A, N = 1024, 10
 b = workload.make_batch12(A, N, "trot", seed=0)
