@@ -46,7 +46,17 @@
 #define SRB12_REFINE_MU 1e-3
 #endif
 
-#define SYNC() __syncthreads()
+// one wave per SIMD is the design point (four agents per CU by LDS): the scheduler may spend every
+// register on latency hiding instead of trimming live ranges for an occupancy the LDS rules out
+#ifndef SRB12_WPE
+#define SRB12_WPE __attribute__((amdgpu_waves_per_eu(1, 1)))
+#endif
+
+// The workgroup is one wavefront (launch bound 64): its LDS accesses are executed in issue order, so a
+// barrier needs no hardware wait -- a wavefront-scope fence (no s_waitcnt) and a wave barrier keep the
+// compiler from moving memory accesses across it.  (__syncthreads would add an lgkmcnt(0) wait for the
+// stores before every barrier.)
+#define SYNC() do { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
 #include "srb_wave.h"
 
 namespace {
@@ -320,8 +330,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     double schur = 0.0;
     auto factor = [&](double delta) -> bool {
         int fail = 0;
-        // this lane's entries (i = gi + 4 q, j = ci) of Q^ and R^, branch-free: masks and clamped LDS
-        // indices (a diagonal weight, an obstacle-block entry Q3, a leg-block entry Rh)
+        // this lane's entries (i = gi + 4 q, j = ci) of Q^, branch-free: masks and clamped LDS indices (a
+        // diagonal weight, an obstacle-block entry Q3); R^ likewise (a leg-block entry Rh) in the stage loop
         auto qh = [&](int k, int q) {
             const int i = gi + 4 * q, j = ci;
             const bool dg = i == j && i < 12, ob = (i < 2 || i == 12) && (j < 2 || j == 12);
@@ -331,43 +341,66 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             // masks as factors: the loads stay unconditional (a select lets the compiler sink them into branches)
             return (dg ? 1.0 : 0.0) * (wd + delta) + (ob ? 1.0 : 0.0) * qo;
         };
-        auto rh = [&](int k, int q) {
-            const int i = gi + 4 * q, j = ci;
-            const bool in = i < 12 && j < 12, dg = in && i == j, bl = in && i / 3 == j / 3;
-            const int i3 = in ? i % 3 : 0, j3 = in ? j % 3 : 0, l = in ? i / 3 : 0;
-            const double wd = L.wr[i3], rb = L.Rh[24 * k + 6 * l + sym3(i3, j3)];
-            return (dg ? 1.0 : 0.0) * (wd + delta) + (bl ? 1.0 : 0.0) * rb;
-        };
-        // B~[i][ci] for the operand rows i = 4 + gi (kb 1) and 8 + gi (kb 2): tsm on v (rows 6..8) for the
-        // leg's own axis, W_l on omega (rows 9..11)
-        auto bt = [&](int i, const double *W, const double *ct) {
-            const int j = ci < 12 ? ci : 0, l = j / 3, a = j - 3 * l;
-            const bool v = ci < 12 && i >= 6 && i < 9 && a == i - 6, w = ci < 12 && i >= 9 && i < 12;
-            const double ctl = ct[l], wl = W[9 * l + 3 * (w ? i - 9 : 0) + a];
-            return (v ? tsm : 0.0) * ctl + (w ? 1.0 : 0.0) * wl;
-        };
         d4 Vd;                                            // V in the MFMA accumulator layout: V[gi + 4 q][ci]
 #pragma unroll
         for (int q = 0; q < 4; q++) Vd[q] = qh(N - 1, q);
+        // per-lane index pieces of the stage operands (qh, rh, bt above, split into the LDS reads -- one
+        // batch, one round trip per stage -- and the masked arithmetic after them)
+        int qoi[4], rbi[4], wqi[4], wri[4];
+        double qdm[4], qom[4], rdm[4], rbm[4];
+#pragma unroll
+        for (int q = 0; q < 4; q++) {
+            const int i = gi + 4 * q, j = ci;
+            {
+                const bool dg = i == j && i < 12, ob = (i < 2 || i == 12) && (j < 2 || j == 12);
+                const int a = (i == 12) ? 2 : (i < 2 ? i : 0), b = (j == 12) ? 2 : (j < 2 ? j : 0);
+                const int lo = a < b ? a : b, hi = a < b ? b : a;
+                wqi[q] = i < 12 ? i : 0; qoi[q] = (hi * (hi + 1)) / 2 + lo;
+                qdm[q] = dg ? 1.0 : 0.0; qom[q] = ob ? 1.0 : 0.0;
+            }
+            {
+                const bool in = i < 12 && j < 12, dg = in && i == j, bl = in && i / 3 == j / 3;
+                const int i3 = in ? i % 3 : 0, j3 = in ? j % 3 : 0, l = in ? i / 3 : 0;
+                wri[q] = i3; rbi[q] = 6 * l + sym3(i3, j3);
+                rdm[q] = dg ? 1.0 : 0.0; rbm[q] = bl ? 1.0 : 0.0;
+            }
+        }
+        const int bl_ = (ci < 12 ? ci : 0) / 3, ba_ = (ci < 12 ? ci : 0) - 3 * bl_;
+        const int i1 = 4 + gi, i2 = 8 + gi;
+        const bool bv1 = ci < 12 && i1 >= 6 && i1 < 9 && ba_ == i1 - 6, bv2 = ci < 12 && i2 >= 6 && i2 < 9 && ba_ == i2 - 6;
+        const bool bw2 = ci < 12 && i2 >= 9 && i2 < 12;
+        const int bwi = 9 * bl_ + 3 * (bw2 ? i2 - 9 : 0) + ba_;
 #pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
+            // the stage's LDS operands in one batch (Q^_{k-1}: k = 0 reads grid 0, masked below)
+            __builtin_amdgcn_sched_barrier(0);
+            const int km = k > 0 ? k - 1 : 0;
             const double c = L.cs[2 * k], s = L.cs[2 * k + 1];
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+            const double ctl = L.ct[4 * k + bl_], wl2 = L.Wl[36 * k + bwi];
+            double qd[4], qo[4], rd[4], rb[4];
+#pragma unroll
+            for (int q = 0; q < 4; q++) {
+                qd[q] = L.wq[wqi[q]]; qo[q] = L.Q3[6 * km + qoi[q]];
+                rd[q] = L.wr[wri[q]]; rb[q] = L.Rh[24 * k + rbi[q]];
+            }
+            __builtin_amdgcn_sched_barrier(0);
             // operand values: A~[4 kb + gi][ci] (B operand of A~, A operand of A~'), B~ likewise (rows
             // 4..11 only: kb = 1, 2)
             double Ab[4];
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) Ab[kb] = atil(4 * kb + gi, ci, Ts, c, s);
-            const double Bb1 = bt(4 + gi, W, ct), Bb2 = bt(8 + gi, W, ct);
+            const double Bb1 = (bv1 ? tsm : 0.0) * ctl;
+            const double Bb2 = (bv2 ? tsm : 0.0) * ctl + (bw2 ? 1.0 : 0.0) * wl2;
             d4 G = {0.0, 0.0, 0.0, 0.0}, F = {0.0, 0.0, 0.0, 0.0};
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) G = mfma(Vd[kb], Ab[kb], G);           // G = V A~
             F = mfma(Vd[1], Bb1, F); F = mfma(Vd[2], Bb2, F);                      // F = V B~
             d4 Vn, Hu, Hux = {0.0, 0.0, 0.0, 0.0};
+            const double mk = (k > 0) ? 1.0 : 0.0;
 #pragma unroll
             for (int q = 0; q < 4; q++) {
-                Vn[q] = (k > 0) ? qh(k - 1, q) : 0.0;
-                Hu[q] = rh(k, q);
+                Vn[q] = mk * (qdm[q] * (qd[q] + delta) + qom[q] * qo[q]);
+                Hu[q] = rdm[q] * (rd[q] + delta) + rbm[q] * rb[q];
             }
 #pragma unroll
             for (int kb = 0; kb < 4; kb++) Vn = mfma(Ab[kb], G[kb], Vn);          // Q^_{k-1} + A~'G
@@ -453,87 +486,155 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // free).  Component i = ci of every vector, replicated in the four rows; row gi takes columns
     // 4 gi .. 4 gi + 3 of each matrix-vector product (perm_d gathers them), rowsum adds the rows.
     [[maybe_unused]] int sph = 4;                         // stamps: the phase a solve's set-up counts to
+    // A~_k applied to a replicated 13-vector, less the identity part over Ts, branch-free (a select chain
+    // over DPP results compiles to exec-mask branches inside the stage loops):
+    //   atv: (A~' v)[i] - v[i] = Ts (v[i-6] for i = 6, 7, 8, 11; the Rz' rows on v[3], v[4] for i = 9, 10)
+    //   apv: (A~  v)[i] - v[i] = Ts (v[i+6] for i = 0, 1, 2, 5; the Rz rows on v[9], v[10] for i = 3, 4)
+    // one row shift by six brings v[i -/+ 6] to lane i, a swap of the two rotation lanes brings the other
+    // component; the per-lane coefficients (1 on a copy lane, cos on a rotation lane; +-sin on the swapped
+    // component) are three lane constants per form
+    const double m12 = (ci < 12) ? 1.0 : 0.0, m13 = (ci < 13) ? 1.0 : 0.0, mg0 = (gi == 0) ? 1.0 : 0.0;
+    const double ea0 = (ci % 3 == 0) ? 1.0 : 0.0, ea1 = (ci % 3 == 1) ? 1.0 : 0.0, ea2 = (ci % 3 == 2) ? 1.0 : 0.0;
+    const double tP = (ci >= 6 && ci < 12 && ci != 9 && ci != 10) ? 1.0 : 0.0, tQ = (ci == 9 || ci == 10) ? 1.0 : 0.0;
+    const double tR = (ci == 9) ? -1.0 : (ci == 10) ? 1.0 : 0.0;
+    const double aP = (ci < 6 && ci != 3 && ci != 4) ? 1.0 : 0.0, aQ = (ci == 3 || ci == 4) ? 1.0 : 0.0;
+    const double aR = (ci == 3) ? 1.0 : (ci == 4) ? -1.0 : 0.0;
+#ifndef SRB12_DPPSHIFT
+#define SRB12_DPPSHIFT 1
+#endif
+#if !SRB12_DPPSHIFT
+    const double e0 = ci == 0 ? 1.0 : 0.0, e1 = ci == 1 ? 1.0 : 0.0, e2 = ci == 2 ? 1.0 : 0.0, e3 = ci == 3 ? 1.0 : 0.0;
+    const double e4 = ci == 4 ? 1.0 : 0.0, e5 = ci == 5 ? 1.0 : 0.0, e6 = ci == 6 ? 1.0 : 0.0, e7 = ci == 7 ? 1.0 : 0.0;
+    const double e8 = ci == 8 ? 1.0 : 0.0, e9 = ci == 9 ? 1.0 : 0.0, e10 = ci == 10 ? 1.0 : 0.0, e11 = ci == 11 ? 1.0 : 0.0;
+    auto atv = [&](double v, double cc, double sn) {
+        const double v0 = bc16(v, 0), v1 = bc16(v, 1), v2 = bc16(v, 2), v3 = bc16(v, 3), v4 = bc16(v, 4), v5 = bc16(v, 5);
+        const double sel = fma(e6, v0, fma(e7, v1, fma(e8, v2, e11 * v5)));
+        const double c3 = fma(e9, cc, e10 * sn), c4 = fma(e10, cc, -(e9 * sn));
+        return sel + fma(c3, v3, c4 * v4);
+    };
+    auto apv = [&](double p, double cc, double sn) {
+        const double p6 = bc16(p, 6), p7 = bc16(p, 7), p8 = bc16(p, 8), p9 = bc16(p, 9), p10 = bc16(p, 10), p11 = bc16(p, 11);
+        const double sel = fma(e0, p6, fma(e1, p7, fma(e2, p8, e5 * p11)));
+        const double c9 = fma(e3, cc, -(e4 * sn)), c10 = fma(e3, sn, e4 * cc);
+        return sel + fma(c9, p9, c10 * p10);
+    };
+#else
+    auto atv = [&](double v, double cc, double sn) {
+        const double s6 = dpp_d<0x116>(v);                // row_shr:6 -- lane i: v[i - 6]
+        const double t = dpp_d<0xD8>(s6);                 // quad_perm [0,2,1,3] -- lanes 9, 10 swapped
+        return fma(fma(tQ, cc, tP), s6, (tR * sn) * t);   // 9: cc v3 - sn v4, 10: cc v4 + sn v3
+    };
+    auto apv = [&](double p, double cc, double sn) {
+        const double s6 = dpp_d<0x106>(p);                // row_shl:6 -- lane i: p[i + 6]
+        const double t = dpp_d<0x141>(s6);                // row_half_mirror -- lanes 3, 4 swapped
+        return fma(fma(aQ, cc, aP), s6, (aR * sn) * t);   // 3: cc p9 + sn p10, 4: cc p10 - sn p9
+    };
+#endif
+    // the per-stage operands of the two sweeps, read in one batch at the top of the stage (one LDS round
+    // trip; scheduling barriers keep the compiler from interleaving each read with its first use), so
+    // the stage's dependent chain (broadcasts, ds_bpermute gathers, permlane sums) waits on no LDS read.
+    // (A variant that loaded stage k - 1's operands during stage k, two stages a trip, measured slower,
+    // 0.850 against 0.828 ms a step.)
+    struct BwOps { double ct, ru, w0, w1, w2, cc, sn, rx, kk[4], hk[4]; };
+    struct FwOps { double ct, kff, w0, w1, w2, cc, sn, kk[4]; };
     auto riccati_solve = [&](int c, bool acc) {
         S12ST(sph);
         const double *rX = c ? L.gX : L.rX, *rU = c ? L.gU : L.rU;
         double *sink = L.T + 300 + ci;                      // stores of lanes outside a vector (T is free here)
-        double v = (ci < 13) ? rX[13 * (N - 1) + ci] : 0.0;
-        // branch-free stage bodies: loads from clamped indices, masks as factors, stores to the sink
-#pragma clang loop unroll(disable)
-        for (int k = N - 1; k >= 0; k--) {
-            const int ln = lane, i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l;
-            const int gsrc = 16 * g + 4 * g;               // lane holding component 4 g (this row's copy)
-            const double m12 = (i < 12) ? 1.0 : 0.0, m13 = (i < 13) ? 1.0 : 0.0;
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k, *Hk = L.Hst + 78 * k;
-            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-            const double v6 = bc16(v, 6), v7 = bc16(v, 7), v8 = bc16(v, 8), v9 = bc16(v, 9), v10 = bc16(v, 10), v11 = bc16(v, 11);
-            // gu = rhs_u + B~'v
-            double gu = fma(ct[l] * tsm, a == 0 ? v6 : a == 1 ? v7 : v8, rU[12 * k + ir]);
-            gu = fma(W[9 * l + a], v9, gu); gu = fma(W[9 * l + 3 + a], v10, gu); gu = fma(W[9 * l + 6 + a], v11, gu);
-            gu *= m12;
-            // K'gu (state i) and -Hu^-1 gu (input i): this row's four input columns j = 4 g + m
-            double pk = 0.0, ph = 0.0;
-            const int i13 = (i < 13) ? i : 12;
+        const int i = ci, g = gi, ir = (i < 12) ? i : 0, l = ir / 3, a = ir - 3 * l, i13 = (i < 13) ? i : 12;
+        const int gsrc = 16 * g + 4 * g;                   // lane holding component 4 g (this row's copy)
+        // (lanes i >= 13 read clamped entries: their K'gu and -Hu^-1 gu never leave the lane -- v is
+        // masked, kff goes to the sink -- and the row sums stay within one component i)
+        auto bw_load = [&](int k) {
+            BwOps o;
+            __builtin_amdgcn_sched_barrier(0);
+            const double *W = L.Wl + 36 * k;
+            o.ct = L.ct[4 * k + l]; o.ru = rU[12 * k + ir];
+            o.w0 = W[9 * l + a]; o.w1 = W[9 * l + 3 + a]; o.w2 = W[9 * l + 6 + a];
+            o.cc = L.cs[2 * k]; o.sn = L.cs[2 * k + 1];
+            o.rx = rX[13 * (k > 0 ? k - 1 : 0) + i13];
 #pragma unroll
             for (int m = 0; m < 4; m++) {
                 const int j = 4 * g + m, jc = (j < 12) ? j : 11;
-                const double gj = perm_d(gu, gsrc + m) * ((j < 12) ? 1.0 : 0.0);
-                pk = fma(m13 * Kk[13 * jc + i13], gj, pk);
-                ph = fma(m12 * Hk[tri(ir, jc)], gj, ph);
+                o.kk[m] = L.Kst[156 * k + 13 * jc + i13];
+                o.hk[m] = L.Hst[78 * k + tri(ir, jc)];
+            }
+            __builtin_amdgcn_sched_barrier(0);
+            return o;
+        };
+        double v = (ci < 13) ? rX[13 * (N - 1) + ci] : 0.0;
+        // backward stage k: gu = rhs_u + B~'v, kff = -Hu^-1 gu, v_{k-1} = rhs_x(k-1) + A~'v + K'gu
+        auto bw_stage = [&](int k, const BwOps &o) {
+            const double v6 = bc16(v, 6), v7 = bc16(v, 7), v8 = bc16(v, 8), v9 = bc16(v, 9), v10 = bc16(v, 10), v11 = bc16(v, 11);
+            double gu = fma(o.ct * tsm, fma(ea0, v6, fma(ea1, v7, ea2 * v8)), o.ru);
+            gu = fma(o.w0, v9, gu); gu = fma(o.w1, v10, gu); gu = fma(o.w2, v11, gu);
+            // K'gu (state i) and -Hu^-1 gu (input i): this row's four input columns j = 4 g + m
+            // (the gathers are issued together, one LDS round trip: the barrier keeps the scheduler from
+            // interleaving each with its use)
+            double gr[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) gr[m] = perm_d(gu, gsrc + m);
+            __builtin_amdgcn_sched_barrier(0);
+            double pk = 0.0, ph = 0.0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) {
+                const double gj = gr[m] * ((4 * g + m < 12) ? 1.0 : 0.0);
+                pk = fma(o.kk[m], gj, pk);
+                ph = fma(o.hk[m], gj, ph);
             }
             rowsum2(pk, ph);
             *((g == 0 && i < 12) ? L.kff + 12 * k + i : sink) = -ph;
-            // v_{k-1} = rhs_x(k-1) + A~'v + K'gu
-            const double v0 = bc16(v, 0), v1 = bc16(v, 1), v2 = bc16(v, 2), v3 = bc16(v, 3), v4 = bc16(v, 4), v5 = bc16(v, 5);
-            const double av = (i >= 6 && i < 9) ? (i == 6 ? v0 : i == 7 ? v1 : v2)
-                            : (i == 9) ? fma(cc, v3, -sn * v4) : (i == 10) ? fma(sn, v3, cc * v4) : (i == 11) ? v5 : 0.0;
-            double vn = fma(Ts, av, v + pk);
-            if (k > 0) vn += rX[13 * (k - 1) + i13];
-            v = m13 * vn;
-        }
+            v = m13 * (fma(Ts, atv(v, o.cc, o.sn), v + pk) + (k > 0 ? 1.0 : 0.0) * o.rx);
+        };
+#pragma clang loop unroll(disable)
+        for (int k = N - 1; k >= 0; k--) bw_stage(k, bw_load(k));
         const double ds0 = -(bc16(v, 12) + L.sc[2 + c]) / schur;
         SYNC();                                            // kff
         S12ST(14);  // solve: backward sweep
-        double prev = (ci == 12) ? ds0 : 0.0;
-#pragma clang loop unroll(disable)
-        for (int k = 0; k < N; k++) {
-            const int ln = lane, i = ln & 15, g = ln >> 4, ir = (i < 12) ? i : 0;
-            const int gsrc = 16 * g + 4 * g, lsrc = 16 * g + 3 * g;   // lanes of components 4 g, 3 g (leg g's first force)
-            const double m12 = (i < 12) ? 1.0 : 0.0;
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k, *Kk = L.Kst + 156 * k;
-            const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-            // du = kff + K dx: this row's state columns j = 4 g + m
-            double pk = 0.0;
+        const int lsrc = 16 * g + 3 * g, i9 = (i >= 9 && i < 12) ? i - 9 : 0;   // lane of leg g's first force
+        const double mv = (i >= 6 && i < 9) ? 1.0 : 0.0, mw = (i >= 9 && i < 12) ? 1.0 : 0.0;
+        auto fw_load = [&](int k) {
+            FwOps o;
+            __builtin_amdgcn_sched_barrier(0);
+            const double *w = L.Wl + 36 * k + 9 * g + 3 * i9;
+            o.ct = L.ct[4 * k + g]; o.kff = L.kff[12 * k + ir];
+            o.w0 = w[0]; o.w1 = w[1]; o.w2 = w[2];
+            o.cc = L.cs[2 * k]; o.sn = L.cs[2 * k + 1];
 #pragma unroll
             for (int m = 0; m < 4; m++) {
                 const int j = 4 * g + m, jc = (j < 13) ? j : 12;
-                const double dj = perm_d(prev, gsrc + m) * ((j < 13) ? 1.0 : 0.0);
-                pk = fma(Kk[13 * ir + jc], dj, pk);
+                o.kk[m] = L.Kst[156 * k + 13 * ir + jc];
             }
-            const double du = m12 * (rowsum(pk) + L.kff[12 * k + ir]);
-            {
-                double *pu = (g == 0 && i < 12) ? L.dU + 12 * k + i : sink;
-                *pu = acc ? *pu + du : du;
-            }
-            // dx_{k+1} = A~ dx + B~ du: row g adds leg g's forces (and row 0 the A~ part)
+            __builtin_amdgcn_sched_barrier(0);
+            return o;
+        };
+        double prev = (ci == 12) ? ds0 : 0.0;
+        // forward stage k: du = kff + K dx, dx_{k+1} = A~ dx + B~ du (row g adds leg g's forces, row 0
+        // the A~ part)
+        auto fw_stage = [&](int k, const FwOps &f) {
+            double *pu = (g == 0 && i < 12) ? L.dU + 12 * k + i : sink;
+            double *px = (g == 0 && i < 13) ? L.dX + 13 * k + i : sink;
+            const double pu0 = acc ? *pu : 0.0, px0 = acc ? *px : 0.0;
+            double gr[4];
+#pragma unroll
+            for (int m = 0; m < 4; m++) gr[m] = perm_d(prev, gsrc + m);
+            __builtin_amdgcn_sched_barrier(0);
+            double pk = 0.0;
+#pragma unroll
+            for (int m = 0; m < 4; m++) pk = fma(f.kk[m], gr[m] * ((4 * g + m < 13) ? 1.0 : 0.0), pk);
+            const double du = m12 * (rowsum(pk) + f.kff);
+            *pu = acc ? pu0 + du : du;
             const double d0 = perm_d(du, lsrc), d1 = perm_d(du, lsrc + 1), d2 = perm_d(du, lsrc + 2);
-            const int i9 = (i >= 9 && i < 12) ? i - 9 : 0;
-            const double *w = W + 9 * g + 3 * i9;
-            const double bv = ct[g] * tsm * (i == 6 ? d0 : i == 7 ? d1 : d2), bw = fma(w[0], d0, fma(w[1], d1, w[2] * d2));
-            double pb = (i >= 6 && i < 9) ? bv : (i >= 9 && i < 12) ? bw : 0.0;
-            const double p6 = bc16(prev, 6), p7 = bc16(prev, 7), p8 = bc16(prev, 8);
-            const double p9 = bc16(prev, 9), p10 = bc16(prev, 10), p11 = bc16(prev, 11);
-            const double ap = (i < 3) ? (i == 0 ? p6 : i == 1 ? p7 : p8)
-                            : (i == 3) ? fma(cc, p9, sn * p10) : (i == 4) ? fma(-sn, p9, cc * p10) : (i == 5) ? p11 : 0.0;
-            pb += (g == 0) ? fma(Ts, ap, prev) : 0.0;
-            double dx = rowsum(pb);
-            if (i > 12) dx = 0.0;
-            {
-                double *px = (g == 0 && i < 13) ? L.dX + 13 * k + i : sink;
-                *px = acc ? *px + dx : dx;
-            }
+            __builtin_amdgcn_sched_barrier(0);
+            const double bv = f.ct * tsm * fma(ea0, d0, fma(ea1, d1, ea2 * d2)), bw = fma(f.w0, d0, fma(f.w1, d1, f.w2 * d2));
+            double pb = fma(mv, bv, mw * bw);
+            pb = fma(mg0, fma(Ts, apv(prev, f.cc, f.sn), prev), pb);
+            const double dx = m13 * rowsum(pb);
+            *px = acc ? px0 + dx : dx;
             prev = dx;
-        }
+        };
+#pragma clang loop unroll(disable)
+        for (int k = 0; k < N; k++) fw_stage(k, fw_load(k));
         SYNC();
         S12ST(15);  // solve: forward sweep
     };
@@ -555,33 +656,36 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         };
         for (int e = tid; e < 13 * N; e += 64) tX[e] = 0.0;
         double m = (ci < 13) ? qdx(N - 1, dX + 13 * (N - 1), ci) + rX[13 * (N - 1) + ci] : 0.0;
+        const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l, i13 = (i < 13) ? i : 12;
+        const int qa = (i == 12) ? 2 : (i < 2 ? i : 0);
+        const double mob = (i < 2 || i == 12) ? 1.0 : 0.0;
 #pragma clang loop unroll(disable)
         for (int k = N - 1; k >= 0; k--) {
-            const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, a3 = ir - 3 * l;
-            const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
-            double vb[13];
-#pragma unroll
-            for (int j = 0; j < 13; j++) vb[j] = bc16(m, j);
-            {
-                const double *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
-                double t = fma(L.wr[a3] + delta, du[a3], rU[12 * k + ir]);
-#pragma unroll
-                for (int bb = 0; bb < 3; bb++) t = fma(rh[sym3(a3, bb)], du[bb], t);
-                t = fma(ct[l] * tsm, a3 == 0 ? vb[6] : a3 == 1 ? vb[7] : vb[8], t);
-#pragma unroll
-                for (int a = 0; a < 3; a++) t = fma(W[9 * l + 3 * a + a3], vb[9 + a], t);
-                *((lane < 12) ? tU + 12 * k + i : sink) = t;
-            }
-            if (k > 0) {
-                const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                const double av = (i >= 6 && i < 9) ? (i == 6 ? vb[0] : i == 7 ? vb[1] : vb[2])
-                                : (i == 9) ? fma(cc, vb[3], -sn * vb[4]) : (i == 10) ? fma(sn, vb[3], cc * vb[4]) : (i == 11) ? vb[5] : 0.0;
-                const double mn = fma(Ts, av, m);
-                m = (i < 13 ? 1.0 : 0.0) * (mn + qdx(k - 1, dX + 13 * (k - 1), i) + rX[13 * (k - 1) + (i < 13 ? i : 0)]);
-            }
+            // the stage's LDS operands in one batch (one round trip); Q^_{k-1} dx_{k-1}: k = 0 reads grid 0
+            __builtin_amdgcn_sched_barrier(0);
+            const int km = k > 0 ? k - 1 : 0;
+            const double *W = L.Wl + 36 * k + 9 * l + a3, *du = dU + 12 * k + 3 * l, *rh = L.Rh + 24 * k + 6 * l;
+            const double du0 = du[0], du1 = du[1], du2 = du[2], dua = dU[12 * k + ir];
+            const double rh0 = rh[sym3(a3, 0)], rh1 = rh[sym3(a3, 1)], rh2 = rh[sym3(a3, 2)];
+            const double ru = rU[12 * k + ir], ctl = L.ct[4 * k + l], wr = L.wr[a3];
+            const double w0 = W[0], w1 = W[3], w2 = W[6], cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
+            const double *q3 = L.Q3 + 6 * km, *dx = dX + 13 * km;
+            const double wd = L.wq[ir], b0 = q3[tri(qa, 0)], b1 = q3[tri(qa, 1)], b2 = q3[tri(qa, 2)];
+            const double dxi = dx[i13], dx0 = dx[0], dx1 = dx[1], dx12 = dx[12], rxn = rX[13 * km + i13];
+            __builtin_amdgcn_sched_barrier(0);
+            const double v6 = bc16(m, 6), v7 = bc16(m, 7), v8 = bc16(m, 8), v9 = bc16(m, 9), v10 = bc16(m, 10), v11 = bc16(m, 11);
+            double t = fma(wr + delta, dua, ru);
+            t = fma(rh0, du0, t); t = fma(rh1, du1, t); t = fma(rh2, du2, t);
+            t = fma(ctl * tsm, fma(ea0, v6, fma(ea1, v7, ea2 * v8)), t);
+            t = fma(w0, v9, t); t = fma(w1, v10, t); t = fma(w2, v11, t);
+            *((lane < 12) ? tU + 12 * k + i : sink) = t;
+            // m_{k-1} = rhs_x(k-1) + Q^_{k-1} dx_{k-1} + A~'m (k = 0: m_0 stays)
+            const double qd = m12 * (wd + delta) * dxi + mob * fma(b0, dx0, fma(b1, dx1, b2 * dx12));
+            const double mn = m13 * (fma(Ts, atv(m, cc, sn), m) + qd + rxn);
+            m = (k > 0) ? mn : m;
         }
-        const double m12 = bc16(m, 12);
-        if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + m12;
+        const double ms = bc16(m, 12);
+        if (tid == 0) L.sc[3] = fma(prm.Sw + delta, dX[12], L.sc[2]) + ms;
         SYNC();
         riccati_solve(1, true);
     };
@@ -828,28 +932,34 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             gm = fmax(gm, fabs(prm.Sw * L.Z[24 * N]));
             {
-                const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l;
+                // (the operands of stage k in one batch of LDS reads, as in the solves)
+                const int i = ci, ir = (i < 12) ? i : 0, l = ir / 3, jj = ir - 3 * l, i13 = (i < 13) ? i : 12;
+                struct CsOps { double ct, gu, w0, w1, w2, cc, sn, gx; };
+                auto cs_load = [&](int k) {
+                    CsOps o;
+                    __builtin_amdgcn_sched_barrier(0);
+                    const double *W = L.Wl + 36 * k + 9 * l + jj;
+                    o.ct = L.ct[4 * k + l]; o.gu = L.gU[12 * k + ir];
+                    o.w0 = W[0]; o.w1 = W[3]; o.w2 = W[6];
+                    o.cc = L.cs[2 * k]; o.sn = L.cs[2 * k + 1];
+                    o.gx = L.gX[13 * (k > 0 ? k - 1 : 0) + i13];
+                    __builtin_amdgcn_sched_barrier(0);
+                    return o;
+                };
                 double lam = (i < 13) ? L.gX[13 * (N - 1) + i] : 0.0;
-#pragma clang loop unroll(disable)
-                for (int k = N - 1; k >= 0; k--) {
-                    const double *W = L.Wl + 36 * k, *ct = L.ct + 4 * k;
+                auto cs_stage = [&](int k, const CsOps &o) {
                     const double v6 = bc16(lam, 6), v7 = bc16(lam, 7), v8 = bc16(lam, 8);
                     const double v9 = bc16(lam, 9), v10 = bc16(lam, 10), v11 = bc16(lam, 11);
-                    {
-                        double ru = fma(ct[l] * tsm, jj == 0 ? v6 : jj == 1 ? v7 : v8, L.gU[12 * k + ir]);
-                        ru = fma(W[9 * l + jj], v9, ru); ru = fma(W[9 * l + 3 + jj], v10, ru); ru = fma(W[9 * l + 6 + jj], v11, ru);
-                        ru *= (lane < 12) ? 1.0 : 0.0;
-                        nrd = fma(ru, ru, nrd);
-                    }
-                    if (k > 0) {
-                        const double cc = L.cs[2 * k], sn = L.cs[2 * k + 1];
-                        const double v0 = bc16(lam, 0), v1 = bc16(lam, 1), v2 = bc16(lam, 2);
-                        const double v3 = bc16(lam, 3), v4 = bc16(lam, 4), v5 = bc16(lam, 5);
-                        const double av = (i >= 6 && i < 9) ? (i == 6 ? v0 : i == 7 ? v1 : v2)
-                                        : (i == 9) ? fma(cc, v3, -sn * v4) : (i == 10) ? fma(sn, v3, cc * v4) : (i == 11) ? v5 : 0.0;
-                        lam = ((i < 13) ? 1.0 : 0.0) * (fma(Ts, av, lam) + L.gX[13 * (k - 1) + (i < 13 ? i : 0)]);
-                    }
-                }
+                    double ru = fma(o.ct * tsm, fma(ea0, v6, fma(ea1, v7, ea2 * v8)), o.gu);
+                    ru = fma(o.w0, v9, ru); ru = fma(o.w1, v10, ru); ru = fma(o.w2, v11, ru);
+                    ru *= m12 * mg0;                         // one row of the four copies
+                    nrd = fma(ru, ru, nrd);
+                    // lam_{k-1} (k = 0: lam_0 stays, its slack entry closes r_s)
+                    const double ln = m13 * (fma(Ts, atv(lam, o.cc, o.sn), lam) + o.gx);
+                    lam = (k > 0) ? ln : lam;
+                };
+#pragma clang loop unroll(disable)
+                for (int k = N - 1; k >= 0; k--) cs_stage(k, cs_load(k));
                 const double l12 = bc16(lam, 12);
                 if (tid == 0) { const double rs = L.sc[0] + l12; nrd = fma(rs, rs, nrd); }
             }
@@ -1193,7 +1303,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 }
 
 #define SRB12_KERNEL(TL, TO, NC, K1)                                                                            \
-    extern "C" __global__ void __launch_bounds__(64) srb12_kernel_##TL##_##TO##_##NC##_##K1(                    \
+    extern "C" __global__ void __launch_bounds__(64) SRB12_WPE srb12_kernel_##TL##_##TO##_##NC##_##K1(          \
         Srb12KParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ xrefg,        \
         const double *__restrict__ footg, const int *__restrict__ contactg, const double *__restrict__ obstacles, \
         const double *__restrict__ nbr_state, const int *__restrict__ sel_g, double *__restrict__ x_qp_out,      \
