@@ -893,7 +893,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
                 for (int m = 0; m < 6; m++) rhp[m] = rh[m];
             }
-            if (obs_on)
+            if (obs_on) {
+            // (the slack's curvature sum H_ss += om goes through a wave sum: an LDS atomic to one address
+            // from every lane compiles to a 64-step scalar loop)
+            double oms = 0.0;
 #pragma unroll
             for (int t = 0; t < TO; t++) {
                 // branch-free: a lane past the last row adds zeros to row 0's grid
@@ -916,7 +919,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 __hip_atomic_fetch_add(&q3[3], -om * c0, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&q3[4], -om * c1, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                 __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
-                __hip_atomic_fetch_add(&L.sc[1], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
+                oms += om;
+            }
+            oms = wsum(oms);
+            if (tid == 0) L.sc[1] += oms;
             }
             SYNC();
             S12ST(8);   // (stamps: the rows; slot 8 also takes the exit test -> polish gap)

@@ -42,7 +42,21 @@
 #include "srb_kernel_params.h"
 
 #define WAVE 64
-#define SYNC() __syncthreads()
+// Barrier of the NW-wave workgroup.  NW = 1 (one agent per wave, the large-batch instances): the LDS
+// accesses of one wavefront execute in issue order, so a wavefront-scope fence (no s_waitcnt) and a wave
+// barrier suffice -- __syncthreads would wait for every outstanding LDS store first.  (Every SYNC site
+// sits in a function templated on NW.)
+template <int NW>
+__device__ __forceinline__ void srb_sync()
+{
+    if constexpr (NW == 1) {
+        __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront");
+        __builtin_amdgcn_wave_barrier();
+    } else {
+        __syncthreads();
+    }
+}
+#define SYNC() srb_sync<NW>()
 
 #include "srb_wave.h"
 
@@ -387,7 +401,7 @@ __device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, in
 // (y = M g; y += M (g - Hs y)): the explicit inverse alone is not backward stable, and near
 // the end of an interior-point solve Hs carries barrier weights of 1e8..1e12.
 // g, y, r, out: LDS vectors (zero beyond nz).  Returns out in registers (uniform).
-template <int NZL>
+template <int NZL, int NW>
 __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *Hs, const double *Zs, double dl, const double *g,
                                          double *y, double *r, double *out, double (&res)[NZL], int nz, int lane)
 {
@@ -834,7 +848,7 @@ _Pragma("unroll")                                                               
             if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);                                                                           \
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
             if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; } /* not PD: reject */                                            \
-            la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);                                                                    \
+            la_solve<NZL, NW>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);                                                                    \
             double mdx = 0.0;                                                                                                                 \
 _Pragma("unroll")                                                                                                                             \
             for (int t = 0; t < TS; t++)                                                                                                      \
@@ -1007,7 +1021,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 qp_flag = 1;                                  // x stays xbar (last iterate is returned)
                 continue;
             }
-            la_solve<NZL>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
+            la_solve<NZL, NW>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
             // x = xbar + Z xi ; zi = h - G x ; s, z shifted (Auxilary.c:716-746)
             double mn = 1e300, mx = -1e300;
 #pragma unroll
@@ -1133,7 +1147,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_reduced<NZL>(Mi, nz, lane, 0);
-            la_solve<NZL>(Mi, ZZ, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
+            la_solve<NZL, NW>(Mi, ZZ, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
@@ -1350,7 +1364,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
-                la_solve<NZL>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
+                la_solve<NZL, NW>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
