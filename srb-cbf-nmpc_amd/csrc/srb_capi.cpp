@@ -14,13 +14,13 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
-#define DECL_NMPC(NZL, TS, NW)                                                                                \
-    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS##_##NW(                                           \
+#define DECL_NMPC(NZL, TS, NW, NC, CC, KC)                                                                    \
+    extern "C" __global__ void srb_nmpc_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                     \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
         double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
         const double *alpha_buf, double *alpha_out, const int *sel_g, float *zpol_g, int zstride);            \
-    extern "C" __global__ void srb_polish_kernel_##NZL##_##TS##_##NW(                                         \
+    extern "C" __global__ void srb_polish_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                   \
         SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
         const double *obstacles, const double *nbr_state, double *x_out, double *obj_out, int *status_out,     \
         const double *alpha_buf, double *alpha_out, const int *sel_g, const float *zpol_g, int zstride);
@@ -42,8 +42,10 @@ extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const
 extern "C" __global__ void srb_grid_build_kernel(const double *tab0, int stride0, int n0, SrbGrid *g0, int *off0,
                                                  double2 *spos0, int *sidx0, const double *tab1, int stride1, int n1,
                                                  SrbGrid *g1, int *off1, double2 *spos1, int *sidx1);
-struct srb_instance { int nzl, ts, nw; srb_kernel_fn fn; srb_polish_fn polish; };
-#define ENTRY_NMPC(NZL, TS, NW) {NZL, TS, NW, srb_nmpc_kernel_##NZL##_##TS##_##NW, srb_polish_kernel_##NZL##_##TS##_##NW},
+struct srb_instance { int nzl, ts, nw, nc, cc, kc; srb_kernel_fn fn; srb_polish_fn polish; };
+#define ENTRY_NMPC(NZL, TS, NW, NC, CC, KC)                                                                   \
+    {NZL, TS, NW, NC, CC, KC, srb_nmpc_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC,                       \
+     srb_polish_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 #undef ENTRY_NMPC
 
@@ -72,6 +74,7 @@ static const srb_instance *pick_instance(const SrbKParams &k, int nw = 1)
         const int want = pass == 0 ? nw : pass == 1 ? (nw == 4 ? 2 : 1) : 1;
         for (const srb_instance &in : g_instances)
             if (in.nw == want && in.nzl >= k.nz && 64 * in.nw * in.ts >= S &&
+                (in.nc == 0 || (in.nc == k.N && in.cc == k.C && in.kc == k.K_obs + k.K_nbr)) &&
                 (size_t)srb_lds_doubles(k, in.nzl, in.nw) * sizeof(double) <= g_lds_max)
                 return &in;
     }

@@ -648,7 +648,9 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
     constexpr int LDR = NZL + 1, LDH = NZL + 1; \
     constexpr int NTH = 64 * NW; \
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6; \
-    const int N = prm.N, C = prm.C, K = prm.K_obs + prm.K_nbr, n = prm.n, nz = prm.nz; \
+    /* the compiled shape (NC, CC, KC > 0) or the run-time one; n = (6 + C) N + 1, nz = N (C - 1) + 1 */ \
+    const int N = NC > 0 ? NC : prm.N, C = CC > 0 ? CC : prm.C, K = KC > 0 ? KC : prm.K_obs + prm.K_nbr; \
+    const int n = (NC > 0 && CC > 0) ? (6 + CC) * NC + 1 : prm.n, nz = (NC > 0 && CC > 0) ? NC * (CC - 1) + 1 : prm.nz; \
     const int NK = N * K, NE = 2 * (N - 1); \
     const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N); \
     /* stored term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | zero rows up to rO, a */ \
@@ -938,7 +940,7 @@ _Pragma("unroll")                                                               
 // the row slots and the term-row passes are split across the waves and combined through LDS;
 // the reduced-system factorisation and solves run redundantly in every wave (identical data,
 // identical results, no communication).
-template <int NZL, int TS, int NW>
+template <int NZL, int TS, int NW, int NC, int CC, int KC>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
                 const double *__restrict__ obstacles, int n_obs,
@@ -1550,7 +1552,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 // status (-> OPTIMAL) only when the polish is accepted.  A kernel of its own: inside the solve
 // kernel the polish's registers competed with the interior-point loop's and pushed its spills
 // from 8 to 100-200 (configs[2] 0.40 -> 0.47-0.66 ms); here the loop is untouched.
-template <int NZL, int TS, int NW>
+template <int NZL, int TS, int NW, int NC, int CC, int KC>
 __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
                 const double *__restrict__ obstacles, const double *__restrict__ nbr_state,
@@ -1626,8 +1628,9 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
 
 }
 
-#define SRB_NMPC_KERNEL(NZL, TS, NW)                                                                           \
-    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE srb_nmpc_kernel_##NZL##_##TS##_##NW(        \
+#define SRB_NMPC_KERNEL(NZL, TS, NW, NC, CC, KC)                                                               \
+    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE                                              \
+    srb_nmpc_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                                                 \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
         const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
         const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
@@ -1638,11 +1641,12 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        nmpc_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
+        nmpc_agent<NZL, TS, NW, NC, CC, KC>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
                                 x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, sel_g, \
                                 zpol_g, zstride, lds);                                                         \
     }                                                                                                          \
-    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE srb_polish_kernel_##NZL##_##TS##_##NW(      \
+    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE                                              \
+    srb_polish_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                                               \
         SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
         const double *__restrict__ footg, const double *__restrict__ obstacles,                                 \
         const double *__restrict__ nbr_state, double *__restrict__ x_out, double *__restrict__ obj_out,          \
@@ -1652,7 +1656,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
         const int agent = blockIdx.x;                                                                          \
         if (agent >= n_agents) return;                                                                         \
-        polish_agent<NZL, TS, NW>(prm, agent, x0g, refg, footg, obstacles, nbr_state, x_out, obj_out,          \
+        polish_agent<NZL, TS, NW, NC, CC, KC>(prm, agent, x0g, refg, footg, obstacles, nbr_state, x_out, obj_out,          \
                                   status_out, alpha_buf, alpha_out, sel_g, zpol_g, zstride, lds);             \
     }
 

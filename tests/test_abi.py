@@ -32,10 +32,12 @@ def test_library_contains_gfx950_code_object():
     import re
     hdr = open(os.path.join(ROOT, "srb-cbf-nmpc_amd", "csrc", "srb_kernel_params.h")).read()
     # the product list (the #else branch; SRB_DEV_INSTANCES builds only a few for register reports)
-    inst = re.findall(r"X\((\d+), (\d+), (\d+)\)", hdr.split("#define SRB_KERNEL_INSTANCES(X) \\")[1].split("#endif")[0])
-    assert len(inst) >= 4 and any(nw == "4" for _, _, nw in inst)
-    for nzl, ts, nw in inst:                  # every register-bound instance is in the code object
-        assert f"srb_nmpc_kernel_{nzl}_{ts}_{nw}".encode() in data
+    inst = re.findall(r"X\((\d+), (\d+), (\d+), (\d+), (\d+), (\d+)\)",
+                      hdr.split("#define SRB_KERNEL_INSTANCES(X) \\")[1].split("#define SRB_KI_PART0")[0])
+    assert len(inst) >= 4 and any(i[2] == "4" for i in inst)
+    assert any(i[3] != "0" for i in inst) and sum(i[3] == "0" for i in inst) >= 4   # compiled shapes + run-time ones
+    for i in inst:                            # every register-bound instance is in the code object
+        assert ("srb_nmpc_kernel_" + "_".join(i)).encode() in data
 
 
 def test_param_defaults_are_the_reference_constants():
