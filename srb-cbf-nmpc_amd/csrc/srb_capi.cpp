@@ -74,7 +74,8 @@ static const srb_instance *pick_instance(const SrbKParams &k, int nw = 1)
         const int want = pass == 0 ? nw : pass == 1 ? (nw == 4 ? 2 : 1) : 1;
         for (const srb_instance &in : g_instances)
             if (in.nw == want && in.nzl >= k.nz && 64 * in.nw * in.ts >= S &&
-                (in.nc == 0 || (in.nc == k.N && in.cc == k.C && in.kc == k.K_obs + k.K_nbr)) &&
+                (in.nc == 0 || in.nc == k.N) && (in.cc == 0 || in.cc == k.C) &&
+                (in.kc == 0 || in.kc == k.K_obs + k.K_nbr) &&
                 (size_t)srb_lds_doubles(k, in.nzl, in.nw) * sizeof(double) <= g_lds_max)
                 return &in;
     }

@@ -2,7 +2,7 @@
 (diagnostic): python tools/phase_icount.py [kernel-name-substring]"""
 import re, subprocess, sys, tempfile, os
 lib = os.path.join(os.path.dirname(__file__), '..', 'srb-cbf-nmpc_amd', 'srbnmpc', 'libsrbnmpc_stamps.so')
-name = sys.argv[1] if len(sys.argv) > 1 else 'srb_nmpc_kernel_12_3'
+name = sys.argv[1] if len(sys.argv) > 1 else 'srb_nmpc_kernel_12_4_1_10_2_11'
 d = tempfile.mkdtemp()
 subprocess.run(['/opt/rocm/lib/llvm/bin/llvm-objcopy', '--dump-section=.hip_fatbin=%s/f' % d, lib], check=True)
 subprocess.run(['/opt/rocm/lib/llvm/bin/clang-offload-bundler', '--unbundle', '--type=o', '--input=%s/f' % d,
