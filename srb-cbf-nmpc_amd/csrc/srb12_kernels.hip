@@ -534,7 +534,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     // trip; scheduling barriers keep the compiler from interleaving each read with its first use), so
     // the stage's dependent chain (broadcasts, ds_bpermute gathers, permlane sums) waits on no LDS read.
     // (A variant that loaded stage k - 1's operands during stage k, two stages a trip, measured slower,
-    // 0.850 against 0.828 ms a step.)
+    // 0.850 against 0.828 ms a step, and failed the GPU parity tests -- cause not found.)
     struct BwOps { double ct, ru, w0, w1, w2, cc, sn, rx, kk[4], hk[4]; };
     struct FwOps { double ct, kff, w0, w1, w2, cc, sn, kk[4]; };
     auto riccati_solve = [&](int c, bool acc) {
