@@ -303,26 +303,6 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         g = -(dx * dx + dy * dy) - L.Z[24 * N];
         h = -L.eps[j];
     };
-    // Q^_k (state block k, 13 x 13) entry: diag(q) + delta on the 12 states, the obstacle rows' (p_x,
-    // p_y, s) block; the slack's own weight Sw + delta enters once, at s_0 (the factor's last pivot)
-    auto qhat = [&](int k, int i, int j, double delta) {
-        double v = (i == j && i < 12) ? ((k == N - 1) ? L.wqN[i] : L.wq[i]) + delta : 0.0;
-        const bool pi = i < 2 || i == 12, pj = j < 2 || j == 12;
-        if (pi && pj) {
-            const double *q3 = L.Q3 + 6 * k;
-            const int a = (i == 12) ? 2 : i, b = (j == 12) ? 2 : j;
-            const int lo = a < b ? a : b, hi = a < b ? b : a;
-            v += (lo == 0) ? (hi == 0 ? q3[0] : hi == 1 ? q3[1] : q3[3]) : (lo == 1) ? (hi == 1 ? q3[2] : q3[4]) : q3[5];
-        }
-        return v;
-    };
-    // R^_k entry (12 x 12): r + delta on the diagonal, each stance leg's 3 x 3 row block (Rh)
-    auto rhat = [&](int k, int i, int j, double delta) {
-        if (i >= 12 || j >= 12) return 0.0;
-        double v = (i == j) ? L.wr[i % 3] + delta : 0.0;
-        if (i / 3 == j / 3) v += L.Rh[24 * k + 6 * (i / 3) + sym3(i % 3, j % 3)];
-        return v;
-    };
 
     // ---------------- backward Riccati factor over the 13-state with the shift delta.  false when a
     // pivot (the inertia test) or the initial slack's Schur complement is not positive.  Reads the

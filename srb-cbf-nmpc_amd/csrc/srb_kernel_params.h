@@ -6,7 +6,9 @@
 #ifndef SRB_REFINE
 #define SRB_REFINE 1      // iterative-refinement steps per reduced Newton solve
 #endif
+#ifndef SRB_KNN_WAVES
 #define SRB_KNN_WAVES 4   // waves per agent in the selection kernel (srb_knn_kernel)
+#endif
 #define SRB_GRID_CELLS 16384      // cells of the selection grid (LDS counters of srb_grid_build_kernel)
 #define SRB_GRID_MIN_ROWS 8192    // tables this long get a grid (shorter: brute-force scan)
 #define SRB_GRID_MIN_ROWS_STATIC 4096   // versioned static obstacle tables (grid built once, reused):
@@ -83,8 +85,8 @@ struct SrbKParams {
 // threads, see srb_kernels.hip), and the problem shape (N, C, K = K_obs + K_nbr) the instance is
 // compiled for -- 0: read at run time.  A compiled shape makes every LDS offset and loop bound of
 // the agent a constant (the bench shapes configs[1] and configs[2] / [3]: 12 % and 7 % faster steps;
-// the N = 20 shape compiled so spilled to scratch and ran 16 % slower, with a different polish
-// outcome on a quarter of the agents -- not instanced).  The
+// the N = 20 shape compiled whole spilled to scratch and ran 16 % slower, with a different polish
+// outcome on a quarter of the agents, so its instance fixes C and K only: 1.7 % faster).  The
 // host launches the first fitting instance of this list (an exact shape first, then the run-time
 // ones) with NW = 4 for small batches (one agent per CU, all four SIMDs) and NW = 1 otherwise
 // (srb_capi.cpp).
@@ -96,7 +98,7 @@ struct SrbKParams {
 #else
 // the host picks the first fitting instance of this list (srb_capi.cpp), so its order matters
 #define SRB_KERNEL_INSTANCES(X) \
-    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) \
+    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) X(24, 4, 2, 0, 2, 11) \
     X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) X(12, 3, 1, 0, 0, 0) X(12, 4, 1, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(32, 4, 1, 0, 0, 0) X(32, 8, 1, 0, 0, 0) \
     X(8, 1, 4, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 1, 4, 0, 0, 0) X(16, 2, 4, 0, 0, 0) X(32, 2, 4, 0, 0, 0) \
@@ -105,7 +107,7 @@ struct SrbKParams {
 // srb_kernels.hip once per part (-DSRB_PART=0..3, in parallel)
 #define SRB_KI_PART0(X) X(12, 4, 1, 10, 2, 11) X(12, 4, 1, 0, 0, 0) X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) \
     X(12, 3, 1, 0, 0, 0) X(8, 1, 4, 0, 0, 0)
-#define SRB_KI_PART1(X) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
+#define SRB_KI_PART1(X) X(24, 4, 2, 0, 2, 11) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(12, 2, 2, 0, 0, 0)
 #define SRB_KI_PART2(X) X(12, 1, 4, 10, 2, 3) X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(16, 1, 4, 0, 0, 0) \
     X(16, 2, 4, 0, 0, 0) X(16, 2, 2, 0, 0, 0)
