@@ -7,7 +7,7 @@
 #define SRB_REFINE 1      // iterative-refinement steps per reduced Newton solve
 #endif
 #ifndef SRB_KNN_WAVES
-#define SRB_KNN_WAVES 4   // waves per agent in the selection kernel (srb_knn_kernel)
+#define SRB_KNN_WAVES 2   // waves per agent in the selection kernel (srb_knn_kernel; 2: 1 % faster configs[2] step than 4, round 4)
 #endif
 #define SRB_GRID_CELLS 16384      // cells of the selection grid (LDS counters of srb_grid_build_kernel)
 #define SRB_GRID_MIN_ROWS 8192    // tables this long get a grid (shorter: brute-force scan)
