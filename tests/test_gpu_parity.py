@@ -127,6 +127,7 @@ CONFIGS = [
     (4, 2, 1, 0, 16, 1),      # reference mode, trot domain
     (10, 2, 3, 0, 64, 1),     # BASELINE configs[1]
     (10, 2, 3, 8, 96, 1),     # configs[2] shape (inter-agent rows), small batch
+    (10, 2, 3, 8, 512, 1),    # configs[2] shape on more agents than CUs: the compiled-shape instance 12_4_1_10_2_11
     (20, 2, 3, 0, 24, 1),     # horizon 20
     (10, 4, 3, 0, 16, 1),     # standing, 4 contacts
     (10, 2, 0, 0, 32, 1),     # no obstacles: velocity rows only
