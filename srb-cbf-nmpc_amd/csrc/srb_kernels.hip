@@ -211,8 +211,10 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     };
     {
         const int chunk = cnt / NW, tb = wv * chunk;
+#pragma clang loop unroll(disable)
         for (int t0 = tb; t0 < tb + chunk; t0 += 16) batch(t0, false);
         const int och = nko / NW, ob = rO + wv * och;
+#pragma clang loop unroll(disable)
         for (int t0 = ob; t0 < ob + och; t0 += 16) batch(t0, !SRB_OBS_STORED(NZL));
     }
     double gs[NTC];
@@ -291,6 +293,7 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
     for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
     auto range = [&](int tb, int te, bool gen) {
         int t0 = tb;
+#pragma clang loop unroll(disable)
         for (; t0 + 32 <= te; t0 += 32) {
             double a[8][NTC], c[8];
 #pragma unroll
@@ -306,6 +309,7 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
                 for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
         }
+#pragma clang loop unroll(disable)
         for (; t0 < te; t0 += 4) {
             const int r = t0 + kq;
             const double cc = CF[r];
