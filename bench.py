@@ -493,6 +493,8 @@ def main():
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
                     help="PMC summary (tools/pmc_traffic.py); default profiles/r04_pmc_traffic_c<config>.json")
+    ap.add_argument("--lib", default=None,
+                    help="diagnostics: time the variant build libsrbnmpc_<tag>.so instead of the product library")
     ap.add_argument("--plumbing", action="store_true",
                     help="CPU check of the multi-process launch only (gloo, no GPU, no solve; tests/test_bench_launch.py)")
     args = ap.parse_args()
@@ -511,6 +513,8 @@ def main():
     if args.plumbing:
         plumbing(args, world, rank)
         return
+    if args.lib:
+        srbnmpc.use_library(args.lib)
     if world > 1:
         os.environ.setdefault("MASTER_ADDR", "127.0.0.1")
         dist.init_process_group("nccl", rank=rank, world_size=world, device_id=torch.device("cuda", local_rank))

@@ -146,7 +146,7 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
  * (H_L = Q_qp - 2 sum z_A on the obstacle positions), whose fixed point is the exact KKT point
  * for that active set (c_A = 0).  The result replaces the iterate only if it is primal feasible
  * (every row within ORC_POLISH_PTOL of its bound), dual feasible (z_A >= 0), the Newton
- * iteration has converged and the reduced stationarity Z'(grad f + J_A' z_A) is at round-off
+ * iteration has converged, the equality rows hold to ORC_POLISH_EQTOL and the reduced stationarity Z'(grad f + J_A' z_A) is at round-off
  * level; the solve then ends OPTIMAL.  Otherwise the interior-point result stands.
  */
 #ifndef ORC_POLISH_ON
@@ -157,6 +157,7 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #define ORC_POLISH_PASSES 4       /* active-set passes (the most negative z_A leaves, violated rows join) */
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
+#define ORC_POLISH_EQTOL 1e-8     /* the equality rows hold to this at an accepted point (kernel SRB_POLISH_EQTOL) */
 #define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */
 #define ORC_POLISH_DX1 1e-4       /* a Newton step this small whose active rows then hold to CTOL ends the pass */
 #define ORC_POLISH_CTOL 1e-10
@@ -280,10 +281,14 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
             gz = fmax(gz, fabs(acc)); res = fmax(res, fabs(gr[a] + acc));
         }
         const int dual_ok = nact == 0 || zmin >= -1e-9 * zm;
+        /* the equality rows (LIP dynamics, CoP, sum lambda; dec_vars_constr_cost.h:154-206) at the
+         * polished point: the kernel's SRB_POLISH_EQTOL test (the LU step keeps them to round-off) */
+        double eqr = 0.0;
+        for (int k = 0; k < P->p; k++) eqr = fmax(eqr, fabs(dotv(P->A + (size_t)k * n, xt, n) - P->b[k]));
         /* converged Newton iteration (the last correction) stands for stationarity: the step solves
          * grad f + H dx + J_A' z_A+ = 0, so at x + dx the reduced gradient of the Lagrangian is
          * O(|H| |dx|); `res` (the reduced stationarity itself) is reported by the trace only */
-        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL;
+        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL && eqr <= ORC_POLISH_EQTOL;
         if (trace)
             fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  last dx %.2e  stat %.2e (scale %.2e)  -> %s\n",
                     pass, nact, pv, cv, nact ? zmin : 0.0, zm, lastdx, res, fmax(1.0, fmax(gf, gz)), ok ? "accepted" : "rejected");

@@ -192,7 +192,7 @@ static int reduced_pd(const p12_t *P, const double *Hf)
  * (H_L: the cost Hessian and -2 y on (p_x, p_y) of active obstacle rows, y = z_A + RHO c_A the current
  * multiplier estimate).  At most IT steps per
  * pass (fewer once |dx| <= DXTOL); accepted when every row holds to PTOL, the active rows to PTOL,
- * z_A >= -1e-9 max|z_A| and the last step is <= DXTOL; otherwise the most negative multiplier
+ * z_A >= -1e-9 max|z_A|, the last step is <= DXTOL and the dynamics hold to DYNTOL; otherwise the most negative multiplier
  * leaves A, violated rows join and the next pass starts again from the interior-point point (at most
  * PASSES).  The steps after a pass's first reuse its factor (the kernel's rule: one Riccati factor per
  * pass; measured no different in acceptance or accuracy from refactoring every step).  Unlike the LIP
@@ -206,6 +206,7 @@ static int reduced_pd(const p12_t *P, const double *Hf)
 #define ORC12_POL_PASSES 2
 #define ORC12_POL_PTOL 1e-9
 #define ORC12_POL_DXTOL 1e-7
+#define ORC12_POL_DYNTOL 1e-8        /* max |x_{k+1} - A_k x_k - B_k u_k - c_k| of an accepted point */
 
 /* diagnostics for the tests: polishes rejected, accepted, Newton steps in all, most steps of one solve */
 int orc12_polish_stats[4];
@@ -284,7 +285,16 @@ static int polish12(const p12_t *P, int nl, double *x, const double *s, const do
         }
         if (getenv("ORC12_TRACE"))
             fprintf(stderr, "      polish pass %d: primal %.2e |c_A| %.2e -min z_A %.2e last dx %.2e\n", pass, pv, cv, nzmin, lastdx);
-        if (pv <= ORC12_POL_PTOL && cv <= ORC12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= ORC12_POL_DXTOL) {
+        /* and the dynamics: the rows alone would pass a point the Newton steps carried off them (the
+         * kernel's SRB12_POL_DYNTOL test; the LU step keeps them to round-off here) */
+        double dres = 0.0;
+        for (int r = 0; r < p; r++) {
+            double v = -P->beq[r];
+            for (int j = 0; j < n; j++) v += P->Aeq[(size_t)r * n + j] * xt[j];
+            dres = fmax(dres, fabs(v));
+        }
+        if (pv <= ORC12_POL_PTOL && cv <= ORC12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= ORC12_POL_DXTOL &&
+            dres <= ORC12_POL_DYNTOL) {
             memcpy(x, xt, sizeof(double) * n);
             accepted = 1;
             break;

@@ -11,6 +11,8 @@
 #include "srbnmpc.h"
 #include "srb_kernel_params.h"
 
+#define SRB12_DBG_LEN (2 * 64 * 8 + 16 + 128)   // trace, stamp sums, state checks (srb12_kernels.hip)
+
 int srb_internal_fail(int code, const char *msg);
 int srb_internal_select(srb_ctx *c, int n_agents, const double *x0, const double *obstacles, int n_obs,
                         const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
@@ -81,12 +83,14 @@ extern "C" void srb12_params_default(srb12_params *p, int N)
 
 extern "C" int srb12_nv(const srb12_params *p) { return 24 * p->N + 1; }
 
-// the first instance with enough leg-slot and obstacle-slot trips (the list is ordered by cost)
-static const srb12_inst *pick12(const srb12_params *p)
+// the first instance with enough leg-slot and obstacle-slot trips (the list is ordered by cost) for
+// horizon N and K rows per grid -- the rows the launch actually selects (clamp_rows: a compiled-in K
+// must equal them, the kernel reads sel at that stride and carves its LDS for them)
+static const srb12_inst *pick12(int N, int K)
 {
-    const int tl = srb12_leg_trips(p->N), to = srb12_obs_trips(p->N, p->K_obs + p->K_nbr);
+    const int tl = srb12_leg_trips(N), to = srb12_obs_trips(N, K);
     for (const srb12_inst &in : g_inst12)      // the (N, K) compiled in
-        if (in.nc == p->N && in.k1 == p->K_obs + p->K_nbr + 1 && in.tl >= tl && in.to >= to) return &in;
+        if (in.nc == N && in.k1 == K + 1 && in.tl >= tl && in.to >= to) return &in;
     for (const srb12_inst &in : g_inst12)      // run-time (N, K)
         if (in.nc == 0 && in.tl >= tl && in.to >= to) return &in;
     return nullptr;
@@ -105,7 +109,7 @@ static int validate12(const srb12_params *p)
         if (!(p->q[i] >= 0) || !(p->qN[i] >= 0)) return srb_internal_fail(SRB_ERR_ARG, "state weights must be >= 0");
     for (int i = 0; i < 3; i++)
         if (!(p->r[i] > 0)) return srb_internal_fail(SRB_ERR_ARG, "force weights must be > 0");
-    if (!pick12(p)) return srb_internal_fail(SRB_ERR_SIZE, "no SRB-12 kernel instance covers the row slots");
+    if (!pick12(p->N, p->K_obs + p->K_nbr)) return srb_internal_fail(SRB_ERR_SIZE, "no SRB-12 kernel instance covers the row slots");
     if ((size_t)srb12_lds_doubles(p->N, p->K_obs + p->K_nbr) * sizeof(double) > 160 * 1024)
         return srb_internal_fail(SRB_ERR_SIZE, "per-agent LDS exceeds 160 KiB");
     return SRB_OK;
@@ -173,7 +177,7 @@ extern "C" int srb12_ctx_create(const srb12_params *p, int max_agents, int devic
     CREATE_CHK(hipMalloc(&c->obj, A * sizeof(double)));
     CREATE_CHK(hipMalloc(&c->status, A * 2 * sizeof(int)));
     CREATE_CHK(hipMalloc(&c->iters, A * 2 * sizeof(int)));
-    CREATE_CHK(hipMalloc(&c->dbg, (2 * 64 * 8 + 16) * sizeof(double)));
+    CREATE_CHK(hipMalloc(&c->dbg, SRB12_DBG_LEN * sizeof(double)));
     c->dbg_agent = -1; c->timing = 1;
 #undef CREATE_CHK
     *out = c;
@@ -232,7 +236,7 @@ static int launch12(srb12_ctx *c, int n_agents, const srb12_batch *d, hipStream_
     clamp_rows(p, d, &Ko, &Kn);
     Srb12KParams k = make_k12(p, Ko, Kn);
     k.dbg_agent = c->dbg_agent; k.dbg = c->dbg;
-    const srb12_inst *in = pick12(p);
+    const srb12_inst *in = pick12(p->N, Ko + Kn);
     if (!in) return srb_internal_fail(SRB_ERR_SIZE, "no SRB-12 kernel instance covers the row slots");
     const size_t lds = (size_t)srb12_lds_doubles(p->N, Ko + Kn) * sizeof(double);
     int *sel = d->sel ? d->sel : c->sel;
@@ -369,6 +373,17 @@ extern "C" int srb12_debug_trace(srb12_ctx *c, int agent, double *out)
         H12CHK(hipMemcpy(out, c->dbg, (2 * 64 * 8 + 16) * sizeof(double), hipMemcpyDeviceToHost));
     }
     c->dbg_agent = agent;
-    H12CHK(hipMemset(c->dbg, 0, (2 * 64 * 8 + 16) * sizeof(double)));
+    H12CHK(hipMemset(c->dbg, 0, SRB12_DBG_LEN * sizeof(double)));
+    return SRB_OK;
+}
+
+// diagnostics (not in the public header): the 128 state checks of the traced agent that a -DSRB12_CHECK
+// build records in its polish (srb12_kernels.hip S12CK; tools/srb12_check.py); zeros in other builds
+extern "C" int srb12_debug_check(srb12_ctx *c, double *out)
+{
+    if (!c || !out) return srb_internal_fail(SRB_ERR_ARG, "null argument");
+    H12CHK(hipSetDevice(c->device));
+    if (c->any) H12CHK(hipEventSynchronize(c->done));
+    H12CHK(hipMemcpy(out, c->dbg + (2 * 64 * 8 + 16), 128 * sizeof(double), hipMemcpyDeviceToHost));
     return SRB_OK;
 }

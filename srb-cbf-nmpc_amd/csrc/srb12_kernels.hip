@@ -92,6 +92,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
 // per-phase cycle stamps of the traced agent (diagnostic build -DSRB12_STAMPS, libsrbnmpc_s12st.so):
 // s_memtime deltas accumulated into prm.dbg[SRB12_DBG_TRACE + slot], read by srb12_debug_trace
 #define SRB12_DBG_TRACE (2 * 64 * 8)
+#define SRB12_DBG_CHECK (SRB12_DBG_TRACE + 16)      // diagnostic build -DSRB12_CHECK: 128 state checks
 #ifdef SRB12_STAMPS
 #define S12ST(slot)                                                                                  \
     do {                                                                                             \
@@ -682,6 +683,42 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         }
         for (int k = tid; k < N; k += 64) gx[13 * k + 12] = 0.0;
     };
+    // max_k |x_{k+1} - A_k x_k - B_k u_k - c_k| at the iterate (x_0 given): the dynamics every returned
+    // point must satisfy (dec_vars_constr_cost.h:154-206 in the LIP mode); the polish's acceptance tests it
+    auto dyn_res = [&]() -> double {
+        double r = 0.0;
+        for (int e = tid; e < 12 * N; e += 64) {
+            const int k = e / 12, i = e - 12 * k;
+            const double *xp = (k == 0) ? x0 : X + 12 * (k - 1);
+            double v = a_mul(i, xp, Ts, L.cs[2 * k], L.cs[2 * k + 1]) + b_mul(i, U + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+            if (i == 8) v -= Ts * prm.grav;
+            r = fmax(r, fabs(X[e] - v));
+        }
+        return wmax(r);
+    };
+#ifdef SRB12_CHECK
+    // diagnostic build (make s12chk): state checks of the traced agent into prm.dbg[SRB12_DBG_CHECK + slot]
+    const bool dchk = agent == prm.dbg_agent && prm.dbg != nullptr;
+    auto lds_sum = [&](const double *p, int n) {
+        double a = 0.0;
+        for (int v = tid; v < n; v += 64) a += fabs(p[v]);
+        return wsum(a);
+    };
+    // the solve's consistency: max_k |dx_{k+1} - A~ dx_k - B~ du_k| (dx_0 = 0 but its slack)
+    auto sol_res = [&]() -> double {
+        double r = 0.0;
+        for (int e = tid; e < 12 * N; e += 64) {
+            const int k = e / 12, i = e - 12 * k;
+            double v = b_mul(i, L.dU + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm);
+            if (k > 0) v += a_mul(i, L.dX + 13 * (k - 1), Ts, L.cs[2 * k], L.cs[2 * k + 1]);
+            r = fmax(r, fabs(L.dX[13 * k + i] - v));
+        }
+        return wmax(r);
+    };
+#define S12CK(slot, expr) do { const double v_ = (expr); if (dchk && tid == 0) prm.dbg[SRB12_DBG_CHECK + (slot)] = v_; } while (0)
+#else
+#define S12CK(slot, expr) do { } while (0)
+#endif
     // right-hand side of pass (0 predictor, 1 corrector) into column 0:
     // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
     auto build_rhs = [&](int pass, double smu) {
@@ -1086,7 +1123,10 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             ozz[t] = oact[t] ? oz[t] : 0.0;
         }
         SYNC();
+        S12CK(0, (double)fin_flag); S12CK(1, dyn_res()); S12CK(2, lds_sum(L.Z, nv)); S12CK(3, X[0]);
         for (int v = tid; v < nv; v += 64) L.xsv[v] = L.Z[v];
+        SYNC();
+        S12CK(4, lds_sum(L.xsv, nv));
         bool accepted = false;
 #pragma clang loop unroll(disable)
         for (int pass = 0; pass < SRB12_POL_PASSES; pass++) {
@@ -1155,8 +1195,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 }
                 SYNC();
                 if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
+                S12CK(8 + 40 * pass + 8 * pit, schur);
                 sph = 9;
                 riccati_solve(1, false);                                    // d = -H^-1 grad (column 1)
+                S12CK(9 + 40 * pass + 8 * pit, sol_res()); S12CK(10 + 40 * pass + 8 * pit, L.dX[0]);
+                S12CK(11 + 40 * pass + 8 * pit, L.dU[2]); S12CK(12 + 40 * pass + 8 * pit, lds_sum(L.xsv, nv));
                 // multipliers z_A += RHO (c_A + J_A d) at the linearisation point; then x += d
 #pragma unroll
                 for (int t = 0; t < TL; t++) {
@@ -1190,8 +1233,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 }
                 if (tid == 0) { L.Z[24 * N] += dsv; mdx = fmax(mdx, fabs(dsv)); }
                 lastdx = wmax(mdx);
+                SYNC();
+                S12CK(13 + 40 * pass + 8 * pit, lastdx); S12CK(14 + 40 * pass + 8 * pit, dyn_res());
+                S12CK(15 + 40 * pass + 8 * pit, X[0]);
                 if (lastdx <= SRB12_POL_DXTOL) break;
             }
+            S12CK(100 + pass, bad ? 1.0 : 0.0);
             if (bad) break;
             SYNC();
             // acceptance at the polished point
@@ -1223,7 +1270,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 wred<4, 15u>(rv);
                 pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3];
             }
-            if (pv <= SRB12_POL_PTOL && cv <= SRB12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB12_POL_DXTOL) {
+            // the dynamics too: the rows alone would pass a point the Newton steps carried off them
+            const double dres = dyn_res();
+            S12CK(102 + 8 * pass, pv); S12CK(103 + 8 * pass, cv); S12CK(104 + 8 * pass, nzmin); S12CK(105 + 8 * pass, zm);
+            S12CK(106 + 8 * pass, dres); S12CK(107 + 8 * pass, lds_sum(L.xsv, nv)); S12CK(108 + 8 * pass, X[0]);
+            if (pv <= SRB12_POL_PTOL && cv <= SRB12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB12_POL_DXTOL &&
+                dres <= SRB12_POL_DYNTOL) {
                 accepted = true;
                 break;
             }
@@ -1263,6 +1315,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         if (!accepted)
             for (int v = tid; v < nv; v += 64) L.Z[v] = L.xsv[v];
         SYNC();
+        S12CK(120, accepted ? 1.0 : 0.0); S12CK(121, lds_sum(L.Z, nv)); S12CK(122, X[0]); S12CK(123, dyn_res());
         S12ST(9);
     }
 #ifdef SRB12_STAMPS

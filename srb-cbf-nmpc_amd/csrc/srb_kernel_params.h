@@ -57,6 +57,8 @@
 #endif
 #define SRB_POLISH_PTOL 1e-9
 #define SRB_POLISH_DXTOL 1e-7
+// and only where the equality rows (LIP dynamics, CoP, sum lambda) hold to this (lip_eq_res, srb_kernels.hip)
+#define SRB_POLISH_EQTOL 1e-8
 // a Newton step <= DX1 after which every active row holds to CTOL (its quadratic remainder) ends the
 // pass as converged without the verifying step (oracle ORC_POLISH_DX1 / ORC_POLISH_CTOL)
 #define SRB_POLISH_DX1 1e-4
@@ -188,6 +190,7 @@ struct Srb12KParams {
 #define SRB12_POL_PASSES 2
 #define SRB12_POL_PTOL 1e-9
 #define SRB12_POL_DXTOL 1e-7
+#define SRB12_POL_DYNTOL 1e-8      // accepted only where max_k |x_{k+1} - A_k x_k - B_k u_k - c_k| <= this
 // kernel instances (TL, TO, NC, K1): leg-slot trips (4N legs over 64 lanes), obstacle-slot trips (N K
 // rows), and the horizon N and rows per grid K compiled in (NC = N, K1 = K + 1) or read at run time
 // (NC = K1 = 0).  The host launches the compiled-in instance of the problem's (N, K) when there is one

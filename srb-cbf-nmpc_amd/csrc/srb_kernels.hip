@@ -638,6 +638,35 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
         }
 }
 
+// Largest residual, over this thread's grids k = tid, tid + NTH, .., of the equality rows every returned
+// point must satisfy (dec_vars_constr_cost.h:154-206): the LIP dynamics X_k = Ad X_{k-1} + Bd U_k
+// (X_{-1} = x0), the CoP rows u_k = F_k lambda_k and sum lambda_k = 1.  The polish steps move along the
+// null-space basis, so these hold to round-off; its acceptance checks it (SRB_POLISH_EQTOL).
+__device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double *x0, const double *xs, const double *foot,
+                                             int N, int C, int tid, int NTH)
+{
+    double r = 0.0;
+    for (int k = tid; k < N; k += NTH) {
+        const double *xp = k ? xs + 4 * (k - 1) : x0;
+        const double u0 = xs[4 * N + 2 * k], u1 = xs[4 * N + 2 * k + 1];
+#pragma unroll
+        for (int d = 0; d < 4; d++) {
+            const double v = prm.Ad[4 * d] * xp[0] + prm.Ad[4 * d + 1] * xp[1] + prm.Ad[4 * d + 2] * xp[2] +
+                             prm.Ad[4 * d + 3] * xp[3] + prm.Bd[2 * d] * u0 + prm.Bd[2 * d + 1] * u1;
+            r = fmax(r, fabs(xs[4 * k + d] - v));
+        }
+        double g0 = 0.0, g1 = 0.0, sl = 0.0;
+#pragma unroll
+        for (int j = 0; j < 4; j++)
+            if (j < C) {
+                const double lam = xs[6 * N + C * k + j];
+                g0 = fma(foot[(2 * k) * C + j], lam, g0); g1 = fma(foot[(2 * k + 1) * C + j], lam, g1); sl += lam;
+            }
+        r = fmax(r, fmax(fabs(u0 - g0), fmax(fabs(u1 - g1), fabs(sl - 1.0))));
+    }
+    return r;
+}
+
 // --------------------------------------------------------------------------- shared agent code
 // The solve kernel and the polish kernel run on the same per-agent LDS layout and rebuild the
 // same null-space basis, so the code they share is written once, as statement macros expanded in
@@ -883,7 +912,7 @@ _Pragma("unroll")                                                               
         if (bad) break;                                                                                                                       \
         SYNC();                                                                                                                               \
  /* ---- acceptance at the polished point */                                                                                                  \
-        double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0, vi = -1e300;                                                                  \
+        double pv = -1e300, cv = 0.0, nzmin = -1e300, zm = 1.0, vi = -1e300, eqr = 0.0;                                                       \
         {                                                                                                                                     \
             const double s_var = xs[n - 1];                                                                                                   \
 _Pragma("unroll")                                                                                                                             \
@@ -900,13 +929,14 @@ _Pragma("unroll")                                                               
                         else if (q.m[r] != 0.0) vi = fmax(vi, v);                                                                             \
                     }                                                                                                                         \
                 }                                                                                                                             \
-            double rv[5] = {pv, cv, nzmin, zm, vi};                                                                                           \
-            wred_x<5, 0x1Fu, NW>(rv, red + 7 * 8 * NW, tid);                                                                                  \
-            pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4];                                                                    \
+            double rv[6] = {pv, cv, nzmin, zm, vi, lip_eq_res(prm, x0, xs, foot, N, C, tid, NTH)};                                            \
+            wred_x<6, 0x3Fu, NW>(rv, red + 7 * 8 * NW, tid);                                                                                  \
+            pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4]; eqr = rv[5];                                                       \
         }                                                                                                                                     \
         POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);                           \
         POLDBG(pass, 5, lastdx);                                                                                                              \
-        if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL) {                             \
+        if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&                             \
+            eqr <= SRB_POLISH_EQTOL) {                                                                                                        \
             POLDBG(pass, 6, 1.0);                                                                                                             \
             accepted = true;                                                                                                                  \
             break;                                                                                                                            \

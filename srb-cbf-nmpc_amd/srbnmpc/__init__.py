@@ -19,8 +19,9 @@ import os
 import numpy as np
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# SRBNMPC_LIB names an alternative build in this directory (diagnostic A/B runs only)
-LIB_PATH = os.path.join(_HERE, os.environ.get("SRBNMPC_LIB", "libsrbnmpc.so"))
+# the product library; no environment variable can change it: a diagnostic A/B
+# build is selected only by an explicit use_library() call (bench.py --lib, pytest --srbnmpc-lib)
+LIB_PATH = os.path.join(_HERE, "libsrbnmpc.so")
 
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
@@ -72,6 +73,19 @@ class Prep(ctypes.Structure):
 
 
 _lib = None
+
+
+def use_library(name: str):
+    """Diagnostics only: load the variant build `name` (libsrbnmpc_<tag>.so in this package
+    directory) instead of the product library.  Must precede the first load."""
+    global LIB_PATH
+    base = os.path.basename(name)
+    if base != name or not (base == "libsrbnmpc.so" or (base.startswith("libsrbnmpc_") and base.endswith(".so"))):
+        raise ValueError(f"srbnmpc.use_library: expected libsrbnmpc.so or libsrbnmpc_<tag>.so, got {name!r}")
+    path = os.path.join(_HERE, base)
+    if _lib is not None and path != LIB_PATH:
+        raise RuntimeError(f"srbnmpc.use_library: {LIB_PATH} is already loaded")
+    LIB_PATH = path
 
 
 def lib():

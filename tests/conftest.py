@@ -13,8 +13,17 @@ for p in (ROOT, os.path.join(ROOT, "srb-cbf-nmpc_amd"), os.path.join(ROOT, "test
 GOLDEN = os.path.join(ROOT, "tests", "golden")
 
 
+def pytest_addoption(parser):
+    parser.addoption("--srbnmpc-lib", default=None,
+                     help="diagnostics: run the tests against the variant build libsrbnmpc_<tag>.so")
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs an MI355X (runs through the HIP C ABI)")
+    name = config.getoption("--srbnmpc-lib")
+    if name:
+        import srbnmpc
+        srbnmpc.use_library(name)
 
 
 def _ensure_built():

@@ -187,7 +187,7 @@ def test_no_environment_variable_changes_the_numerics():
     change a solution.  Checked on the built library's dynamic symbols and strings."""
     path = srbnmpc.LIB_PATH
     if os.path.basename(path) != "libsrbnmpc.so":
-        pytest.skip("a diagnostic build is selected (SRBNMPC_LIB)")
+        pytest.skip("a diagnostic build is selected (--srbnmpc-lib)")
     blob = open(path, "rb").read()
     for name in (b"SRB_POLISH_RHO", b"SRB_NMPC_NW", b"SRB_POLISH_NW", b"SRB_GRID_MIN_ROWS", b"SRB_HL_STEP"):
         assert name not in blob, name
@@ -202,3 +202,20 @@ def test_no_environment_variable_changes_the_numerics():
     hdr = open(os.path.join(ROOT, "include", "srbnmpc.h")).read()
     for k, code in srbnmpc.OPTIONS.items():
         assert re.search(rf"#define SRB_OPT_{k.upper()} {code}\b", hdr), k
+
+
+def test_stray_environment_variable_does_not_change_the_library():
+    """the product package loads libsrbnmpc.so whatever the environment holds; a
+    diagnostic build is chosen only by an explicit srbnmpc.use_library() call (bench.py --lib,
+    pytest --srbnmpc-lib), which accepts nothing but a libsrbnmpc[_<tag>].so in the package."""
+    import subprocess
+    import sys
+    code = ("import sys; sys.path[:0] = [sys.argv[1]]; import os, srbnmpc; "
+            "print(os.path.basename(srbnmpc.LIB_PATH))")
+    env = dict(os.environ, SRBNMPC_LIB="libsrbnmpc_nowpe.so", SRB_LIB="x.so")
+    pkg = os.path.join(os.path.dirname(os.path.dirname(os.path.abspath(__file__))), "srb-cbf-nmpc_amd")
+    out = subprocess.run([sys.executable, "-c", code, pkg], env=env, capture_output=True, text=True, check=True)
+    assert out.stdout.strip() == "libsrbnmpc.so"
+    for bad in ("/tmp/libsrbnmpc_x.so", "../libsrbnmpc.so", "libother.so", "libsrbnmpc_x.txt"):
+        with pytest.raises(ValueError):
+            srbnmpc.use_library(bad)

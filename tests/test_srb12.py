@@ -326,6 +326,33 @@ def test_srb12_variants_vs_oracle(Nh, Ko, Kn, use_nlp):
     np.testing.assert_allclose(out["x"][:, 12 * Nh:], r["x"][:, 12 * Nh:], atol=1e-4)      # forces: 1e-4 N
 
 
+@pytest.mark.gpu
+@pytest.mark.parametrize("n_obs,n_all", [(2, 6), (0, 1), (1, 0), (0, 0)])
+def test_srb12_tables_shorter_than_k_vs_oracle(n_obs, n_all):
+    """the horizon-10, 3 + 8 row shape -- which has a compiled-in (N, K) instance --
+    with fewer static obstacles than K_obs and fewer other agents than K_nbr.  The rows clamp to the
+    tables ("up to K nearest"), the launch picks the instance of the clamped K (the compiled K = 11
+    would read sel misaligned and carve LDS for rows the oracle does not have), and every agent
+    matches the oracle, which clamps the same way."""
+    _gpu()
+    A = max(n_all, 4)
+    b = workload.make_batch12(A, N, "trot", seed=37)
+    obs = b["obstacles"][:n_obs]
+    nbr = b["nbr_state"][:n_all] if n_all > 0 else None
+    A = n_all if n_all > 0 else A
+    args = (b["x0"][:A], b["xref"][:A], b["foot"][:A], b["contact"][:A], obs if n_obs else None, nbr)
+    prm = srb12.default_params(N, K_obs=3, K_nbr=8)
+    s = srb12.Solver12(prm, A)
+    out = s.solve(*args)
+    s.close()
+    Ko, Kn = srb12.n_selected(prm, n_obs, n_all)
+    assert out["sel"].shape == (A, Ko + Kn) and (Ko, Kn) == (min(3, n_obs), min(8, max(n_all - 1, 0)))
+    r = oracle.solve_batch12(oracle.params12(N, K_obs=3, K_nbr=8), *args)
+    assert (out["status"] == r["status"]).all(), (out["status"], r["status"])
+    np.testing.assert_allclose(out["x"][:, :12 * N], r["x"][:, :12 * N], atol=1e-6)
+    np.testing.assert_allclose(out["x"][:, 12 * N:], r["x"][:, 12 * N:], atol=1e-4)
+
+
 def test_srb12_abi_rejects_bad_arguments():
     """Parameter validation and the struct_size check run without a GPU (no context needed)."""
     import ctypes
