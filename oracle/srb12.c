@@ -202,8 +202,8 @@ static int reduced_pd(const p12_t *P, const double *Hf)
  * 1e-3 N from the optimum there; the active set's KKT point is exact. */
 #define ORC12_POL_RHO 1e9
 #define ORC12_POL_KAPPA 1e4
-#define ORC12_POL_IT 5
-#define ORC12_POL_PASSES 2
+#define ORC12_POL_IT 8
+#define ORC12_POL_PASSES 4
 #define ORC12_POL_PTOL 1e-9
 #define ORC12_POL_DXTOL 1e-7
 #define ORC12_POL_DYNTOL 1e-8        /* max |x_{k+1} - A_k x_k - B_k u_k - c_k| of an accepted point */
@@ -283,8 +283,6 @@ static int polish12(const p12_t *P, int nl, double *x, const double *s, const do
             pv = fmax(pv, v);
             if (act[r]) { cv = fmax(cv, fabs(v)); nzmin = fmax(nzmin, -za[r]); zm = fmax(zm, fabs(za[r])); }
         }
-        if (getenv("ORC12_TRACE"))
-            fprintf(stderr, "      polish pass %d: primal %.2e |c_A| %.2e -min z_A %.2e last dx %.2e\n", pass, pv, cv, nzmin, lastdx);
         /* and the dynamics: the rows alone would pass a point the Newton steps carried off them (the
          * kernel's SRB12_POL_DYNTOL test; the LU step keeps them to round-off here) */
         double dres = 0.0;
@@ -293,6 +291,8 @@ static int polish12(const p12_t *P, int nl, double *x, const double *s, const do
             for (int j = 0; j < n; j++) v += P->Aeq[(size_t)r * n + j] * xt[j];
             dres = fmax(dres, fabs(v));
         }
+        if (getenv("ORC12_TRACE"))
+            fprintf(stderr, "      polish pass %d: primal %.2e |c_A| %.2e -min z_A %.2e last dx %.2e dyn %.2e\n", pass, pv, cv, nzmin, lastdx, dres);
         if (pv <= ORC12_POL_PTOL && cv <= ORC12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= ORC12_POL_DXTOL &&
             dres <= ORC12_POL_DYNTOL) {
             memcpy(x, xt, sizeof(double) * n);
@@ -315,7 +315,8 @@ static int polish12(const p12_t *P, int nl, double *x, const double *s, const do
     return accepted;
 }
 
-/* one interior-point stage; z (n), lam (p) in/out; returns 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL */
+/* one interior-point stage; z (n), lam (p) in/out; returns 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL, and for the
+ * polished last stage 4 ACCEPTABLE (met tol_final, polish rejected) */
 static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
 {
     const orc12_params *prm = P->prm;
@@ -474,6 +475,9 @@ static int ipm(const p12_t *P, int nl, double *z, double *lam, int *iters)
     if (flag == 0 && (nl || !prm->use_nlp) && prm->polish) {         /* the last stage: exact active-set point */
         int steps = 0;
         const int acc = polish12(P, nl, z, s, zd, &steps);
+        /* a rejected polish leaves the interior-point point, up to ~1e-3 N from the optimum along the legs'
+         * internal-force directions: ACCEPTABLE (4), never OPTIMAL (the kernel, same rule) */
+        if (!acc) flag = 4;
         __atomic_fetch_add(&orc12_polish_stats[acc], 1, __ATOMIC_RELAXED);
         __atomic_fetch_add(&orc12_polish_stats[2], steps, __ATOMIC_RELAXED);
         int old = orc12_polish_stats[3];

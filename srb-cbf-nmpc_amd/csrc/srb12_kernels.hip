@@ -716,8 +716,13 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         return wmax(r);
     };
 #define S12CK(slot, expr) do { const double v_ = (expr); if (dchk && tid == 0) prm.dbg[SRB12_DBG_CHECK + (slot)] = v_; } while (0)
+// per Newton step (the first 5 steps of the first 2 passes) and per pass (the first 2)
+#define S12CKP(k, expr) do { if (pass < 2 && pit < 5) S12CK((k) + 40 * pass + 8 * pit, expr); } while (0)
+#define S12CKA(k, expr) do { if (pass < 2) S12CK((k) + 8 * pass, expr); } while (0)
 #else
 #define S12CK(slot, expr) do { } while (0)
+#define S12CKP(k, expr) do { } while (0)
+#define S12CKA(k, expr) do { } while (0)
 #endif
     // right-hand side of pass (0 predictor, 1 corrector) into column 0:
     // rhs = grad f + sum_rows J'(z + r3 / s + W r_p), r3 = -s z (+ sigma mu - ds_a dz_a)
@@ -1195,11 +1200,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 }
                 SYNC();
                 if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
-                S12CK(8 + 40 * pass + 8 * pit, schur);
+                S12CKP(8, schur);
                 sph = 9;
                 riccati_solve(1, false);                                    // d = -H^-1 grad (column 1)
-                S12CK(9 + 40 * pass + 8 * pit, sol_res()); S12CK(10 + 40 * pass + 8 * pit, L.dX[0]);
-                S12CK(11 + 40 * pass + 8 * pit, L.dU[2]); S12CK(12 + 40 * pass + 8 * pit, lds_sum(L.xsv, nv));
+                S12CKP(9, sol_res()); S12CKP(10, L.dX[0]);
+                S12CKP(11, L.dU[2]); S12CKP(12, lds_sum(L.xsv, nv));
                 // multipliers z_A += RHO (c_A + J_A d) at the linearisation point; then x += d
 #pragma unroll
                 for (int t = 0; t < TL; t++) {
@@ -1234,11 +1239,11 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 if (tid == 0) { L.Z[24 * N] += dsv; mdx = fmax(mdx, fabs(dsv)); }
                 lastdx = wmax(mdx);
                 SYNC();
-                S12CK(13 + 40 * pass + 8 * pit, lastdx); S12CK(14 + 40 * pass + 8 * pit, dyn_res());
-                S12CK(15 + 40 * pass + 8 * pit, X[0]);
+                S12CKP(13, lastdx); S12CKP(14, dyn_res());
+                S12CKP(15, X[0]);
                 if (lastdx <= SRB12_POL_DXTOL) break;
             }
-            S12CK(100 + pass, bad ? 1.0 : 0.0);
+            S12CKA(100 - 8 * pass + pass, bad ? 1.0 : 0.0);
             if (bad) break;
             SYNC();
             // acceptance at the polished point
@@ -1272,8 +1277,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             // the dynamics too: the rows alone would pass a point the Newton steps carried off them
             const double dres = dyn_res();
-            S12CK(102 + 8 * pass, pv); S12CK(103 + 8 * pass, cv); S12CK(104 + 8 * pass, nzmin); S12CK(105 + 8 * pass, zm);
-            S12CK(106 + 8 * pass, dres); S12CK(107 + 8 * pass, lds_sum(L.xsv, nv)); S12CK(108 + 8 * pass, X[0]);
+            S12CKA(102, pv); S12CKA(103, cv); S12CKA(104, nzmin); S12CKA(105, zm);
+            S12CKA(106, dres); S12CKA(107, lds_sum(L.xsv, nv)); S12CKA(108, X[0]);
             if (pv <= SRB12_POL_PTOL && cv <= SRB12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB12_POL_DXTOL &&
                 dres <= SRB12_POL_DYNTOL) {
                 accepted = true;
@@ -1312,8 +1317,12 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             if (!__builtin_amdgcn_ballot_w64(changed)) break;
         }
         SYNC();
-        if (!accepted)
+        if (!accepted) {
             for (int v = tid; v < nv; v += 64) L.Z[v] = L.xsv[v];
+            // the interior-point point stands, up to ~1e-3 N from the optimum along the legs' internal-force
+            // directions: ACCEPTABLE (4), never OPTIMAL (oracle/srb12.c, same rule)
+            if (prm.use_nlp) nlp_flag = 4; else qp_flag = 4;
+        }
         SYNC();
         S12CK(120, accepted ? 1.0 : 0.0); S12CK(121, lds_sum(L.Z, nv)); S12CK(122, X[0]); S12CK(123, dyn_res());
         S12ST(9);

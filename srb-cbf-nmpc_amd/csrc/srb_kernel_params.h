@@ -186,8 +186,11 @@ struct Srb12KParams {
 // active-set polish of the last stage's result (oracle/srb12.c ORC12_POL_*, the same constants)
 #define SRB12_POL_RHO 1e9
 #define SRB12_POL_KAPPA 1e4
-#define SRB12_POL_IT 5
-#define SRB12_POL_PASSES 2
+// (round 5: 8 steps, 4 passes -- with 5 and 2, 1 of 1024 stand agents ended a pass still contracting
+// linearly under the pass's frozen factor, or needed a third active set; the oracle at 6 x 1024 agents:
+// 2 rejected -> 0, Newton steps +0.1 %)
+#define SRB12_POL_IT 8
+#define SRB12_POL_PASSES 4
 #define SRB12_POL_PTOL 1e-9
 #define SRB12_POL_DXTOL 1e-7
 #define SRB12_POL_DYNTOL 1e-8      // accepted only where max_k |x_{k+1} - A_k x_k - B_k u_k - c_k| <= this

@@ -50,6 +50,14 @@ def main():
               f"iters equal {float((out['iters'] == r['iters']).all(1).mean()):.2f}; "
               f"x_qp max err {eq.max():.2e}; x max err {ex.max():.2e}, agents > 1e-6: {int((ex > 1e-6).sum())}")
         print("   agent errors:", " ".join(f"{e:.1e}" for e in ex[:16]))
+        if pol and ex[a.agent] > 1e-6:
+            np.set_printoptions(linewidth=180, precision=6, suppress=False)
+            g, o = out["x"][a.agent], r["x"][a.agent]
+            print("   agent x (gpu / oracle), entries off by > 1e-6:", int((np.abs(g - o) > 1e-6).sum()), "of", g.size,
+                  " exact zeros in gpu:", np.where(g == 0.0)[0].tolist()[:64])
+            for k in range(0, g.size, 12):
+                print(f"   [{k:4d}] gpu ", g[k:k + 12])
+                print(f"          orc ", o[k:k + 12])
         if pol:
             print("   agent0 X[0:3] gpu", out["x"][a.agent, :3], "oracle", r["x"][a.agent, :3])
             names = {0: "fin_flag", 1: "dyn_res(ipm)", 2: "sum|Z| start", 3: "X0 start", 4: "sum|xsv| saved"}

@@ -1,6 +1,7 @@
 """Diagnostic: per-iteration trace of chosen agents of an SRB-12 batch, GPU kernel
 (srb12_debug_trace) next to the oracle (ORC12_TRACE=1 on stderr).
-    python tools/srb12_trace.py gait seed A agent [agent ...]"""
+    python tools/srb12_trace.py [--lib libsrbnmpc_<tag>.so] gait seed A agent [agent ...]
+    (agent "auto": the first five agents the GPU does not report OPTIMAL)"""
 import ctypes
 import os
 import sys
@@ -12,7 +13,12 @@ import numpy as np  # noqa: E402
 import oracle  # noqa: E402
 from srbnmpc import srb12, workload  # noqa: E402
 
-gait, seed, A = sys.argv[1], int(sys.argv[2]), int(sys.argv[3])
+import srbnmpc  # noqa: E402
+argv = sys.argv[1:]
+if argv[0] == "--lib":
+    srbnmpc.use_library(argv[1])
+    argv = argv[2:]
+gait, seed, A = argv[0], int(argv[1]), int(argv[2])
 N = 10
 b = workload.make_batch12(A, N, gait, seed=seed)
 s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
@@ -20,7 +26,13 @@ L = srb12._lib()
 L.srb12_debug_trace.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
 buf = np.zeros(2 * 64 * 8 + 16)
 p = oracle.params12(N, K_obs=3, K_nbr=8)
-for ag in map(int, sys.argv[4:]):
+agents = argv[3:]
+if agents == ["auto"]:
+    out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    bad = np.where((out["status"] != 0).any(1))[0]
+    print("not OPTIMAL:", [(int(a), out["status"][a].tolist(), out["iters"][a].tolist()) for a in bad], flush=True)
+    agents = bad[:5]
+for ag in map(int, agents):
     L.srb12_debug_trace(s._h, ag, None)
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     L.srb12_debug_trace(s._h, -1, buf.ctypes.data_as(ctypes.POINTER(ctypes.c_double)))
