@@ -331,8 +331,9 @@ typedef struct srb12_params {
     int qp_maxit, nlp_maxit, use_nlp;
     double z0;                    /* NLP initial duals z0 / max(s, 1) */
     double tol_final;             /* complementarity s'z/m < tol_final ends the LAST stage (the NLP, or the QP when
-                                     use_nlp = 0; default 1e-9): with tol = 1e-6 there the forces stop up to 3e-2 N
-                                     from the exact optimum, with 1e-9 within 1e-5 N */
+                                     use_nlp = 0; default 1e-8): far enough for the polish to identify the active
+                                     set (without the polish 1e-8 leaves the forces up to 1e-3 N from
+                                     the exact optimum, 1e-6 up to 3e-2 N) */
     int polish;                   /* 1 (default): the last stage's result is polished to the exact KKT point of
                                      its active set (forces within 1e-4 N of the optimum); 0 off */
     double tol_qp;                /* the QP stage's tolerance when the NLP stage follows it (default 1e-3; 0: tol):

@@ -76,7 +76,7 @@ extern "C" void srb12_params_default(srb12_params *p, int N)
     p->eps_obs = (double)1.9f; p->eps_nbr = (double)2.2f;
     p->tol = 1e-6; p->qp_maxit = 25; p->nlp_maxit = 50; p->use_nlp = 1;
     p->z0 = 100.0;
-    p->tol_final = 1e-9;
+    p->tol_final = 1e-8;
     p->polish = 1;
     p->tol_qp = 1e-3;
 }

@@ -65,6 +65,7 @@ struct Srb12Lds {
     double *Wl, *cs, *ct, *Kst, *Hst, *T, *Q3, *Rh, *Z, *xr;
     double *rX, *rU, *gX, *gU, *dX, *dU, *kff, *vv, *sc, *obs, *eps, *xsv;
     double *wq, *wqN, *wr;                                  // the weights q, qN, r (lane-indexed reads)
+    double *x0l;                                            // x_0 in LDS (selected by LDS pointers only: no flat access)
     int *sel;
 };
 
@@ -84,6 +85,7 @@ __device__ __forceinline__ Srb12Lds carve12(double *p, int N, int K)
     L.dX = p; p += 13 * N; L.dU = p; p += 12 * N; L.kff = p; p += 12 * N;
     L.vv = p; p += 16; L.sc = p; p += 16;
     L.wq = p; L.wqN = p + 12; L.wr = p + 24; p += 28;
+    L.x0l = p; p += 16;
     L.obs = p; p += 2 * N * K; L.eps = p; p += K;
     L.sel = (int *)p;
     return L;
@@ -223,10 +225,14 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
     if (tid < 12) { L.wq[tid] = prm.q[tid]; L.wqN[tid] = prm.qN[tid]; }
     if (tid < 3) L.wr[tid] = prm.r[tid];
     if (prm.use_nlp && tid < K) L.sel[tid] = sel_g[(size_t)agent * K + tid];
+    if (tid < 12) L.x0l[tid] = x0[tid];
     SYNC();
     for (int e = tid; e < 4 * N; e += 64) {              // one (grid, leg) per lane: W_l = Ts Iw^-1 [r]x
         const int k = e >> 2, l = e & 3;
-        const double *ph = (k == 0) ? x0 : L.xr + 12 * (k - 1);
+        // (the linearisation point: x0 for grid 0, else the reference -- both in LDS: a pointer selecting between
+        // global memory and LDS compiles to flat accesses, which this kernel avoids)
+        const double *ph = (k == 0) ? L.x0l : L.xr + 12 * (k - 1);
+        const double ph0 = ph[0], ph1 = ph[1], ph2 = ph[2];
         const double psi = ph[5], c = cos(psi), s = sin(psi);
         double R[9], T[9], Iw[9], Iwi[9];
         for (int a = 0; a < 3; a++) for (int b = 0; b < 3; b++) R[3 * a + b] = rzab(a, b, c, s);
@@ -243,7 +249,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             Iwi[6] = C0 * r; Iwi[7] = -(a * h - b * g) * r; Iwi[8] = (a * ee - b * d) * r;
         }
         const double *fp = footg + (size_t)agent * 12 * N + 12 * k + 3 * l;
-        const double r0 = fp[0] - ph[0], r1 = fp[1] - ph[1], r2 = fp[2] - ph[2];
+        const double r0 = fp[0] - ph0, r1 = fp[1] - ph1, r2 = fp[2] - ph2;
         const double S[9] = {0, -r2, r1, r2, 0, -r0, -r1, r0, 0};
         const double on = L.ct[4 * k + l];
         for (int i = 0; i < 3; i++)
@@ -689,7 +695,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         double r = 0.0;
         for (int e = tid; e < 12 * N; e += 64) {
             const int k = e / 12, i = e - 12 * k;
-            const double *xp = (k == 0) ? x0 : X + 12 * (k - 1);
+            const double *xp = (k == 0) ? L.x0l : X + 12 * (k - 1);        // LDS only (no flat access)
             double v = a_mul(i, xp, Ts, L.cs[2 * k], L.cs[2 * k + 1]) + b_mul(i, U + 12 * k, L.Wl + 36 * k, L.ct + 4 * k, tsm);
             if (i == 8) v -= Ts * prm.grav;
             r = fmax(r, fabs(X[e] - v));
@@ -716,9 +722,9 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         return wmax(r);
     };
 #define S12CK(slot, expr) do { const double v_ = (expr); if (dchk && tid == 0) prm.dbg[SRB12_DBG_CHECK + (slot)] = v_; } while (0)
-// per Newton step (the first 5 steps of the first 2 passes) and per pass (the first 2)
+// per Newton step (the first 5 steps of the first 2 passes: slots 8..87) and per pass (the first 4: 88..119)
 #define S12CKP(k, expr) do { if (pass < 2 && pit < 5) S12CK((k) + 40 * pass + 8 * pit, expr); } while (0)
-#define S12CKA(k, expr) do { if (pass < 2) S12CK((k) + 8 * pass, expr); } while (0)
+#define S12CKA(k, expr) do { if (pass < 4) S12CK(88 + 8 * pass + (k), expr); } while (0)
 #else
 #define S12CK(slot, expr) do { } while (0)
 #define S12CKP(k, expr) do { } while (0)
@@ -1198,6 +1204,18 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                         __hip_atomic_fetch_add(&q3[5], om, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);
                     }
                 }
+                // converged: a last step <= DXTOL that left the active rows within PTOL (oracle/srb12.c, same
+                // rule; under the pass's frozen factor a small step can leave |c_A| above PTOL: one more step)
+                if (pit > 0 && lastdx <= SRB12_POL_DXTOL) {
+                    double cm = 0.0;
+#pragma unroll
+                    for (int t = 0; t < TL; t++)
+#pragma unroll
+                        for (int q = 0; q < 6; q++) cm = fmax(cm, lact[t][q] ? fabs(lcr[t][q]) : 0.0);
+#pragma unroll
+                    for (int t = 0; t < TO; t++) cm = fmax(cm, oact[t] ? fabs(ocr[t]) : 0.0);
+                    if (wmax(cm) <= SRB12_POL_PTOL) break;
+                }
                 SYNC();
                 if (pit == 0 && !factor(0.0)) { bad = true; break; }      // not definite: reject
                 S12CKP(8, schur);
@@ -1241,9 +1259,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 SYNC();
                 S12CKP(13, lastdx); S12CKP(14, dyn_res());
                 S12CKP(15, X[0]);
-                if (lastdx <= SRB12_POL_DXTOL) break;
             }
-            S12CKA(100 - 8 * pass + pass, bad ? 1.0 : 0.0);
+            S12CKA(5, bad ? 1.0 : 0.0);
             if (bad) break;
             SYNC();
             // acceptance at the polished point
@@ -1277,8 +1294,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             }
             // the dynamics too: the rows alone would pass a point the Newton steps carried off them
             const double dres = dyn_res();
-            S12CKA(102, pv); S12CKA(103, cv); S12CKA(104, nzmin); S12CKA(105, zm);
-            S12CKA(106, dres); S12CKA(107, lds_sum(L.xsv, nv)); S12CKA(108, X[0]);
+            S12CKA(0, pv); S12CKA(1, cv); S12CKA(2, nzmin); S12CKA(3, zm);
+            S12CKA(4, dres); S12CKA(6, lastdx); S12CKA(7, X[0]);
             if (pv <= SRB12_POL_PTOL && cv <= SRB12_POL_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB12_POL_DXTOL &&
                 dres <= SRB12_POL_DYNTOL) {
                 accepted = true;

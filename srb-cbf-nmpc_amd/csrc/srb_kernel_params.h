@@ -58,7 +58,12 @@
 #define SRB_POLISH_PTOL 1e-9
 #define SRB_POLISH_DXTOL 1e-7
 // and only where the equality rows (LIP dynamics, CoP, sum lambda) hold to this (lip_eq_res, srb_kernels.hip)
+#ifndef SRB_POLISH_EQTOL
 #define SRB_POLISH_EQTOL 1e-8
+#endif
+#ifndef SRB_POLISH_EQCHECK        // 0: diagnostic builds without the equality test
+#define SRB_POLISH_EQCHECK 1
+#endif
 // a Newton step <= DX1 after which every active row holds to CTOL (its quadratic remainder) ends the
 // pass as converged without the verifying step (oracle ORC_POLISH_DX1 / ORC_POLISH_CTOL)
 #define SRB_POLISH_DX1 1e-4
@@ -213,7 +218,7 @@ static inline int srb12_lds_doubles(int N, int K)
            + (24 * N + 4) + 12 * N                      // iterate (X | U | s), reference
            + 50 * N                                     // rhs columns 0 and 1 (the polish's saved iterate in column 0)
            + 13 * N + 12 * N + 12 * N                   // solution, feed-forward -Hu^-1 gu
-           + 16 + 16 + 28                               // vector, scalars, the weights q, qN, r
+           + 16 + 16 + 28 + 16                          // vector, scalars, the weights q, qN, r, x_0
            + 2 * N * K + K + K + 2                      // obstacle positions, eps, sel (as ints)
            + 16;                                        // stamp accumulators (diagnostic build make s12st)
 }

@@ -645,14 +645,20 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
 __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double *x0, const double *xs, const double *foot,
                                              int N, int C, int tid, int NTH)
 {
+    // (x0 and the LDS iterate are read through their own address spaces -- no generic pointer selecting
+    // between them: a flat access in this kernel changed its code generation enough to break the polish
+    // of the run-time instance)
+    const double g0x = x0[0], g1x = x0[1], g2x = x0[2], g3x = x0[3];
     double r = 0.0;
     for (int k = tid; k < N; k += NTH) {
-        const double *xp = k ? xs + 4 * (k - 1) : x0;
+        const int kp = k ? k - 1 : 0;
+        const double p0 = k ? xs[4 * kp] : g0x, p1 = k ? xs[4 * kp + 1] : g1x;
+        const double p2 = k ? xs[4 * kp + 2] : g2x, p3 = k ? xs[4 * kp + 3] : g3x;
         const double u0 = xs[4 * N + 2 * k], u1 = xs[4 * N + 2 * k + 1];
 #pragma unroll
         for (int d = 0; d < 4; d++) {
-            const double v = prm.Ad[4 * d] * xp[0] + prm.Ad[4 * d + 1] * xp[1] + prm.Ad[4 * d + 2] * xp[2] +
-                             prm.Ad[4 * d + 3] * xp[3] + prm.Bd[2 * d] * u0 + prm.Bd[2 * d + 1] * u1;
+            const double v = prm.Ad[4 * d] * p0 + prm.Ad[4 * d + 1] * p1 + prm.Ad[4 * d + 2] * p2 +
+                             prm.Ad[4 * d + 3] * p3 + prm.Bd[2 * d] * u0 + prm.Bd[2 * d + 1] * u1;
             r = fmax(r, fabs(xs[4 * k + d] - v));
         }
         double g0 = 0.0, g1 = 0.0, sl = 0.0;
@@ -929,12 +935,12 @@ _Pragma("unroll")                                                               
                         else if (q.m[r] != 0.0) vi = fmax(vi, v);                                                                             \
                     }                                                                                                                         \
                 }                                                                                                                             \
-            double rv[6] = {pv, cv, nzmin, zm, vi, lip_eq_res(prm, x0, xs, foot, N, C, tid, NTH)};                                            \
+            double rv[6] = {pv, cv, nzmin, zm, vi, SRB_POLISH_EQCHECK ? lip_eq_res(prm, x0, xs, foot, N, C, tid, NTH) : 0.0};                \
             wred_x<6, 0x3Fu, NW>(rv, red + 7 * 8 * NW, tid);                                                                                  \
             pv = rv[0]; cv = rv[1]; nzmin = rv[2]; zm = rv[3]; vi = rv[4]; eqr = rv[5];                                                       \
         }                                                                                                                                     \
         POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);                           \
-        POLDBG(pass, 5, lastdx);                                                                                                              \
+        POLDBG(pass, 5, lastdx); POLDBG(pass, 7, eqr);                                                                                        \
         if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&                             \
             eqr <= SRB_POLISH_EQTOL) {                                                                                                        \
             POLDBG(pass, 6, 1.0);                                                                                                             \

@@ -176,6 +176,13 @@ def _exact_active_set_optimum(p, b, a, x_start, act_tol=1e-6, iters=30):
     Pd, c, Aeq, beq, gJ, hh = _problem(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a], obs, eps)
     n, neq, K = Pd.size, Aeq.shape[0], obs.shape[1]
     nlin = len(hh) - p.N * K
+    def certified(x):
+        # |f - f*| <= stat / r (the force weights make the reduced problem strongly convex along the forces):
+        # stat < 1e-9 bounds the start point's force error by 1e-7 N
+        cert = certify(Pd, c, Aeq, beq, gJ, hh, x, act_tol=1e-7, comp_tol=1e-9)
+        return cert["prim"] < 1e-9 and cert["eq"] < 1e-9 and (cert["stat"] < 1e-9 or cert["stat_rel"] < 1e-12)
+    if certified(x_start):           # degenerate active sets (rows at zero force, multipliers 0) stop here
+        return x_start.copy()
     g, _ = gJ(x_start)
     act = np.where(hh - g < act_tol)[0]
     x = x_start.copy()
@@ -200,8 +207,7 @@ def _exact_active_set_optimum(p, b, a, x_start, act_tol=1e-6, iters=30):
             z = z + d[n + neq:]
             if np.abs(d[:n]).max() < 1e-12:
                 break
-        cert = certify(Pd, c, Aeq, beq, gJ, hh, x, act_tol=1e-7, comp_tol=1e-9)
-        if cert["prim"] < 1e-9 and cert["eq"] < 1e-9 and cert["stat_rel"] < 1e-10:
+        if certified(x):
             return x
         g, _ = gJ(x)
         viol = np.where(hh - g < -1e-9)[0]

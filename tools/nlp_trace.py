@@ -16,7 +16,7 @@ import bench  # noqa: E402
 import srbnmpc  # noqa: E402
 from srbnmpc import workload  # noqa: E402
 
-srbnmpc.LIB_PATH = os.path.join(os.path.dirname(srbnmpc.__file__), "libsrbnmpc_nlpdbg.so")
+srbnmpc.use_library("libsrbnmpc_nlpdbg.so")
 if sys.argv[1] == "custom":     # NLPTRACE_SPEC="N C K_obs K_nbr agents seed" (workload.make_batch)
     N, C, Ko, Kn, A, seed = map(int, os.environ["NLPTRACE_SPEC"].split())
     cfg = dict(N=N, C=C, K_obs=Ko, K_nbr=Kn, agents=A)
@@ -28,6 +28,7 @@ else:
     A, b, _, _ = bench.rank_batch(c, A, 1, 0)
 p = srbnmpc.default_params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"], use_nlp=1)
 s = srbnmpc.BatchSolver(p, A)
+p_n = p.nv
 s.set_waves(int(os.environ.get("NLPTRACE_WAVES", "0")))
 L = srbnmpc.lib()
 L.srb_debug_nlp_trace.argtypes = [ctypes.c_int, ctypes.POINTER(ctypes.c_double)]
@@ -41,12 +42,27 @@ for ag in map(int, sys.argv[2:]):
     for i in range(min(int(out["iters"][ag, 1]) + 1, 56)):
         r = buf[8 * i:8 * i + 8]
         print(f"  {i:2d} " + " ".join(f"{v:10.3e}" for v in r), flush=True)
-    print("  polish pass: primal     |c_A|     -min z_A   max|z_A|   inact.viol  last|dx|   accepted")
+    print("  polish pass: primal     |c_A|     -min z_A   max|z_A|   inact.viol  last|dx|   accepted   eq.resid")
     for p in range(4):
         r = buf[8 * (56 + p):8 * (56 + p) + 8]
         if r.any():
-            print(f"  {p:2d}          " + " ".join(f"{v:10.3e}" for v in r[:7]), flush=True)
+            print(f"  {p:2d}          " + " ".join(f"{v:10.3e}" for v in r[:8]), flush=True)
             print("      Newton |dx|: " + " ".join(f"{v:10.3e}" for v in buf[8 * (60 + p):8 * (60 + p) + 8] if v), flush=True)
+    import oracle
+    op = oracle.params(N, C, K_obs=cfg["K_obs"], K_nbr=cfg["K_nbr"])
+    Ad, Bd = oracle.lip(op)
+    for it in range(3):
+        xs = buf[2848 + 256 * it:2848 + 256 * it + p_n]
+        if not xs.any():
+            continue
+        X = xs[:4 * N].reshape(N, 4); U = xs[4 * N:6 * N].reshape(N, 2); Lm = xs[6 * N:6 * N + C * N].reshape(N, C)
+        F = b["foot"][ag].reshape(N, 2, C)
+        prev, res = b["x0"][ag], []
+        for k in range(N):
+            res.append(max(np.abs(X[k] - Ad @ prev - Bd @ U[k]).max(), np.abs(U[k] - F[k] @ Lm[k]).max(), abs(Lm[k].sum() - 1)))
+            prev = X[k]
+        print(f"  pass 0 Newton step {it}: host equality residual of x {max(res):.3e} (per grid " +
+              " ".join(f"{v:.1e}" for v in res) + ")", flush=True)
     nzr = int((np.abs(buf[512 + 32 * np.arange(32) + np.arange(32)]) > 0).sum())
     if nzr:
         Hm = buf[512:512 + 1024].reshape(32, 32)[:nzr, :nzr]

@@ -71,9 +71,11 @@ def main():
                         continue
                     print(f"   pass {pas} step {pit}: schur {v[0]: .3e} sol_res {v[1]: .2e} dX0 {v[2]: .3e} dU2 {v[3]: .3e} "
                           f"sum|xsv| {v[4]: .6e} lastdx {v[5]: .2e} dyn_res {v[6]: .2e} X0 {v[7]: .6e}")
-                v = chk[102 + 8 * pas:110 + 8 * pas]
-                print(f"   pass {pas} bad {chk[100 + pas]:.0f} accept-test: pv {v[0]: .2e} cv {v[1]: .2e} nzmin {v[2]: .2e} "
-                      f"zm {v[3]: .2e} dyn {v[4]: .2e} sum|xsv| {v[5]: .6e} X0 {v[6]: .6e}")
+            for pas in range(4):
+                v = chk[88 + 8 * pas:96 + 8 * pas]
+                if v.any():
+                    print(f"   pass {pas} bad {v[5]:.0f} accept-test: pv {v[0]: .2e} cv {v[1]: .2e} nzmin {v[2]: .2e} "
+                          f"zm {v[3]: .2e} dyn {v[4]: .2e} lastdx {v[6]: .2e} X0 {v[7]: .6e}")
             print(f"   end: accepted {chk[120]:.0f} sum|Z| {chk[121]: .6e} X0 {chk[122]: .6e} dyn_res {chk[123]: .2e}")
 
 
