@@ -256,6 +256,10 @@ private:
         srb_ctx *c = nullptr;
         if (srb_ctx_create(&p, 1, device_, &c) != SRB_OK)
             throw std::runtime_error(std::string("srb_ctx_create: ") + srb_last_error());
+        /* the per-agent surface keeps the reference's QP solution (qp_solution_eventbased_, iSWIFT's
+         * tolerance): the QP stage is not shortened here */
+        if (srb_ctx_set_option(c, SRB_OPT_QP_WARM_TOL, 0.0) != SRB_OK)
+            throw std::runtime_error(std::string("srb_ctx_set_option: ") + srb_last_error());
         ctx_[key] = c;
         return c;
     }

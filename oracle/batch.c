@@ -23,7 +23,10 @@ int orc_solve_agent(const orc_params *p_in, const double x0[4], const double *re
     double *G = malloc(sizeof(double) * (size_t)mq * nv), *h = malloc(sizeof(double) * mq);
     double *xq = malloc(sizeof(double) * nv);
     orc_build_qp(p, x0, ref, foot, Pd, c, A, b, G, h);
-    status[0] = orc_qp_solve_init(nv, mq, neq, Pd, c, A, b, G, h, p->qp_maxit, p->tol, p->qp_init, xq, NULL, &iters[0]);
+    /* the QP stage that the NLP follows runs to tol_qp: its point only warm-starts the NLP (the kernel's
+     * SRB_OPT_QP_WARM_TOL; the reference runs iSWIFT to 1e-6 there -- a documented deviation) */
+    const double tq = (p->use_nlp && p->tol_qp > 0.0) ? p->tol_qp : p->tol;
+    status[0] = orc_qp_solve_init(nv, mq, neq, Pd, c, A, b, G, h, p->qp_maxit, tq, p->qp_init, xq, NULL, &iters[0]);
     if (x_qp) memcpy(x_qp, xq, sizeof(double) * nv);
     status[1] = 0; iters[1] = 0;
     if (p->use_nlp) {

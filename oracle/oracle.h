@@ -40,6 +40,8 @@ typedef struct orc_params {
     int qp_maxit, nlp_maxit;            /* 25 (GlobalOptions.h:23), 50                        */
     int use_nlp;                        /* MPC_dist::use_snopt                                */
     int qp_init;                        /* QP starting point: 1 scaled (the kernel's default), 0 iSWIFT's kkt_initialize */
+    double tol_qp;                      /* the QP stage's tolerance when the NLP follows (the kernel's SRB_OPT_QP_WARM_TOL,
+                                           default 1e-2; 0: tol) */
 } orc_params;
 
 void orc_params_default(orc_params *p, int N, int C);

@@ -123,6 +123,7 @@ struct srb_ctx {
     int last_polish;               // how the last launch polished: 0 no, 1 polish kernel, 2 fused
     int timing;                    // 1: HIP events around the kernels (srb_last_kernel_ms); 0: none
     double polish_rho;
+    double qp_warm_tol;            // SRB_OPT_QP_WARM_TOL
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
     float polish_ms;
@@ -311,7 +312,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
-    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->qp_warm_tol = SRB_QP_WARM_TOL; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -419,6 +420,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     SrbKParams k = make_kparams(p, use_nlp);
     k.qp_init = c->qp_init;
     k.polish_rho = c->polish_rho;
+    k.qp_warm_tol = c->qp_warm_tol;
     // "up to K nearest": clamp to what exists (batch-uniform), so no row is ever a dummy
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
@@ -501,6 +503,9 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
         c->polish_fused = (int)v; return SRB_OK;
     case SRB_OPT_LAST_POLISH:
         return fail(SRB_ERR_ARG, "SRB_OPT_LAST_POLISH is read only");
+    case SRB_OPT_QP_WARM_TOL:
+        if (!(v >= 0.0 && v <= 1e3)) return fail(SRB_ERR_ARG, "SRB_OPT_QP_WARM_TOL: 0 (the full tolerance) .. 1e3");
+        c->qp_warm_tol = v; return SRB_OK;
     case SRB_OPT_TIMING:
         if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_TIMING: 0 or 1");
         c->timing = (int)v; return SRB_OK;
@@ -526,6 +531,7 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_POLISH_FUSED: *v = c->polish_fused; return SRB_OK;
     case SRB_OPT_LAST_POLISH: *v = c->last_polish; return SRB_OK;
     case SRB_OPT_TIMING: *v = c->timing; return SRB_OK;
+    case SRB_OPT_QP_WARM_TOL: *v = c->qp_warm_tol; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }

@@ -1025,6 +1025,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
 #pragma clang loop unroll(disable)
     for (int stage = 0; stage < nstage; stage++) {
         const bool nl = stage == 1;
+        // the QP stage that the NLP follows runs to qp_warm_tol (its point is only the NLP's warm start)
+        const double tolS = (!nl && prm.use_nlp && prm.qp_warm_tol > 0.0) ? prm.qp_warm_tol : tol, thS = tolS / sqrt(3.0);
         STAMP_STAGE(stage);
         const int nts = ((nl ? S : sV) + NTH - 1) / NTH;      // active slot trips
         const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
@@ -1283,10 +1285,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 break;
             }
             // NLP: dual residual scaled by max(1, ||Q x + f||_inf) (QP: iSWIFT's absolute test)
-            const double thx = nl ? SRB_NLP_EXITF * th * gm : th;
-            const double mtol = nl ? SRB_NLP_EXITF * tol : tol;
+            const double thx = nl ? SRB_NLP_EXITF * th * gm : thS;
+            const double mtol = nl ? SRB_NLP_EXITF * tol : tolS;
             NLPDBG(iter, 0, nrx); NLPDBG(iter, 1, thx); NLPDBG(iter, 2, nrz); NLPDBG(iter, 3, sz * inv_m);
-            const bool pass = nrx < thx && nrz < th && sz * inv_m < mtol;
+            const bool pass = nrx < thx && nrz < thS && sz * inv_m < mtol;
             if (pass && (!nl || dxm < SRB_NLP_DXTOL)) {
                 // NLP: met only by the loosened tests (SRB_NLP_EXITF, which rely on the polish), the result
                 // is provisional -- ACCEPTABLE (4) unless the polish kernel accepts its polish (oracle, same rule)

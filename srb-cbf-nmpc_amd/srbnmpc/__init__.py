@@ -29,7 +29,7 @@ _ip = ctypes.POINTER(ctypes.c_int)
 OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
 # srb_ctx_set_option codes (SRB_OPT_* of include/srbnmpc.h)
 OPTIONS = {"polish": 1, "polish_rho": 2, "polish_waves": 3, "grid_min_rows": 4, "grid_min_rows_static": 5,
-           "polish_fused": 6, "last_polish": 7, "timing": 8}
+           "polish_fused": 6, "last_polish": 7, "timing": 8, "qp_warm_tol": 9}
 ABI_VERSION = 5                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 

@@ -140,6 +140,9 @@ class MPCDist:
         if key not in MPCDist._solvers:
             p = default_params(self.N, C, K_obs=1, K_nbr=0, use_nlp=int(use_nlp))
             MPCDist._solvers[key] = BatchSolver(p, 1, self.device)
+            # the per-agent surface keeps the reference's QP solution (qp_solution_eventbased_, iSWIFT's
+            # tolerance): the QP stage is not shortened here (SRB_OPT_QP_WARM_TOL = 0)
+            MPCDist._solvers[key].set_option("qp_warm_tol", 0.0)
         return MPCDist._solvers[key]
 
     def run_NMPC(self):

@@ -104,7 +104,7 @@ def test_shim_horizon_10_trot_vs_oracle(tmp_path):
     X, xq, alpha = nums[:4 * N], nums[4 * N:4 * N + nv], nums[4 * N + nv:4 * N + nv + 20].reshape(4, 5)
     F = INIT_FOOTPRINT[[0, 3]].T                     # FR, RL stance around Pstart = 0 (gaitDomain 0)
     foot = np.repeat(F[None], N, 0)
-    o = oracle.solve_batch(oracle.params(N, C, K_obs=1, use_nlp=1), x0[None], ref[None], foot[None], obst)
+    o = oracle.solve_batch(oracle.params(N, C, K_obs=1, use_nlp=1, tol_qp=0.0), x0[None], ref[None], foot[None], obst)
     assert [int(v[0]), int(v[1])] == o["status"][0].tolist() == [0, 0]
     np.testing.assert_allclose(X, o["x"][0, :4 * N], atol=1e-4, rtol=0)
     np.testing.assert_allclose(xq[:6 * N], o["x_qp"][0, :6 * N], atol=1e-6, rtol=0)

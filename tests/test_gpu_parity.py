@@ -11,6 +11,7 @@ import numpy as np
 import pytest
 from conftest import load_golden
 
+import bench
 import oracle
 from kkt import certify, nlp_rows
 
@@ -36,12 +37,14 @@ def conv(st):
 _solvers = {}
 
 
-def solver(N, C, K_obs=1, K_nbr=0, use_nlp=1, max_agents=2048, qp_init=1):
-    key = (N, C, K_obs, K_nbr, use_nlp, max_agents, qp_init)
+def solver(N, C, K_obs=1, K_nbr=0, use_nlp=1, max_agents=2048, qp_init=1, qp_warm_tol=None):
+    key = (N, C, K_obs, K_nbr, use_nlp, max_agents, qp_init, qp_warm_tol)
     if key not in _solvers:
         p = srbnmpc.default_params(N, C, K_obs=K_obs, K_nbr=K_nbr, use_nlp=use_nlp)
         _solvers[key] = srbnmpc.BatchSolver(p, max_agents)
         _solvers[key].set_qp_init(qp_init)
+        if qp_warm_tol is not None:
+            _solvers[key].set_option("qp_warm_tol", qp_warm_tol)
     return _solvers[key]
 
 
@@ -57,7 +60,7 @@ def test_kat2_reference_instance(kat2, qp_init):
     genuine iSWIFT; NLP stage == KKT-certified optimum.  qp_init 0 (iSWIFT's start) follows the
     genuine iSWIFT step for step (same iteration count); the default scaled start ends at the same
     point to the log's precision in fewer iterations."""
-    s = solver(4, 4, K_obs=1, qp_init=qp_init)
+    s = solver(4, 4, K_obs=1, qp_init=qp_init, qp_warm_tol=0.0)      # the QP stage to iSWIFT's tolerance
     foot = np.repeat(kat2["F"][None], 4, 0)
     out = s.solve(kat2["x0"][None], kat2["ref"][None], foot[None], np.asarray(kat2["obstacle"])[None])
     assert out["status"][0].tolist() == [0, 0]
@@ -558,12 +561,35 @@ def test_sharded_solve_matches_full_batch(shards, nw):
 
 
 def test_qp_only_equals_qp_stage():
+    """srb_solve_qp (use_nlp = 0) runs the QP to the full tolerance: bit-identical to the QP stage of a full
+    solve with SRB_OPT_QP_WARM_TOL = 0."""
     N, C = 10, 2
     b = workload.make_batch(32, N, C, seed=21)
-    full = solver(N, C, 3, 0, 1).solve(b["x0"], b["ref"], b["foot"], b["obstacles"])
+    full = solver(N, C, 3, 0, 1, qp_warm_tol=0.0).solve(b["x0"], b["ref"], b["foot"], b["obstacles"])
     qp = solver(N, C, 3, 0, 0).solve(b["x0"], b["ref"], b["foot"], b["obstacles"], qp_only=True)
     np.testing.assert_array_equal(qp["x"], full["x_qp"])
     assert (qp["iters"][:, 1] == 0).all()
+
+
+def test_qp_warm_tolerance_leaves_the_nlp_result():
+    """SRB_OPT_QP_WARM_TOL (default 1e-2): the QP stage only warm-starts the NLP, so stopping it early changes
+    neither the NLP's statuses nor its result (to 1e-9) while the QP stage takes fewer iterations -- the
+    configs[2] batch against the full-tolerance QP stage (0), and against the oracle, which does the same."""
+    A, b, _, _ = bench.rank_batch(3, 1024, 1, 0)
+    cfg = bench.CONFIGS[3]
+    N, C, Ko, Kn = cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"]
+    args = (b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
+    s = solver(N, C, Ko, Kn)
+    assert s.get_option("qp_warm_tol") == 1e-2
+    warm = s.solve(*args)
+    full = solver(N, C, Ko, Kn, qp_warm_tol=0.0).solve(*args)
+    np.testing.assert_array_equal(warm["status"], full["status"])
+    np.testing.assert_allclose(xus(N, warm["x"]), xus(N, full["x"]), atol=1e-9, rtol=0)
+    assert warm["iters"][:, 0].mean() < full["iters"][:, 0].mean() - 1.0 and warm["iters"][:, 0].max() < full["iters"][:, 0].max()
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), *args, nthreads=16)
+    np.testing.assert_array_equal(conv(warm["status"]), conv(r["status"]))
+    assert (warm["iters"][:, 0] == r["iters"][:, 0]).mean() > 0.95
+    np.testing.assert_allclose(xus(N, warm["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
 def test_device_api_matches_host():
@@ -648,7 +674,7 @@ def test_mpcdist_horizon_10_trot_cycles_vs_oracle():
     Pr[0] = 0.27 * 0.043 * (c + 1); Prd[0] = 0.27
     m.setReferenceTrajectory(Pr, Prd)
     m.use_snopt = True
-    p = oracle.params(N, C, K_obs=1, use_nlp=1)
+    p = oracle.params(N, C, K_obs=1, use_nlp=1, tol_qp=0.0)          # MPCDist keeps the full QP tolerance
     q = np.zeros(18); dq = np.zeros(18)
     # moving start (test_cpp_shim's): from rest at the origin the agent sits inside the first
     # obstacle's eps radius and the NLP ends FATAL (dual divergence) there, on the GPU and in the oracle alike
@@ -784,7 +810,7 @@ def test_closed_loop_hl_to_solve_through_mpcdist():
     np.testing.assert_array_equal(m.Pr_refined_, R)
     np.testing.assert_array_equal(m.Prd_refined_, Rd)
     m.use_snopt = True
-    p = oracle.params(4, 4, K_obs=1, use_nlp=1)
+    p = oracle.params(4, 4, K_obs=1, use_nlp=1, tol_qp=0.0)          # MPCDist keeps the full QP tolerance
     q = np.zeros(18); dq = np.zeros(18)
     q[:2] = Ps[2:4]
     from srbnmpc.mpc_dist import INIT_FOOTPRINT
