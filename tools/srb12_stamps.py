@@ -1,6 +1,6 @@
 """Diagnostic: per-phase cycle stamps of chosen agents of an SRB-12 batch (configs[2] swarm, 1024
 agents), from the -DSRB12_STAMPS build:
-    SRBNMPC_LIB=libsrbnmpc_s12st.so python tools/srb12_stamps.py agent [agent ...]"""
+    python tools/srb12_stamps.py agent [agent ...]     (loads libsrbnmpc_s12st.so, make s12st)"""
 import ctypes
 import os
 import sys
@@ -9,6 +9,8 @@ ROOT = os.path.abspath(os.path.join(os.path.dirname(__file__), ".."))
 sys.path[:0] = [ROOT, os.path.join(ROOT, "srb-cbf-nmpc_amd")]
 import numpy as np  # noqa: E402
 
+import srbnmpc  # noqa: E402
+srbnmpc.use_library("libsrbnmpc_s12st.so")
 from srbnmpc import srb12, workload  # noqa: E402
 
 PHASES = ["inputs/model/rollout", "costates+norms+exit", "Riccati factor", "gradient (+factor->pred)",

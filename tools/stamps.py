@@ -6,7 +6,7 @@ import ctypes, os, sys
 sys.path.insert(0, os.path.join(os.path.dirname(__file__), '..', 'srb-cbf-nmpc_amd'))
 import numpy as np
 import srbnmpc
-srbnmpc.LIB_PATH = os.path.join(os.path.dirname(srbnmpc.__file__), os.environ.get('SRB_STAMPS_LIB', 'libsrbnmpc_stamps.so'))
+srbnmpc.use_library('libsrbnmpc_stamps.so')
 from srbnmpc import workload
 N, C, Ko, Kn, A = [int(v) for v in (sys.argv[1:6] if len(sys.argv) > 5 else (10, 2, 3, 0, 64))]
 p = srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn)
