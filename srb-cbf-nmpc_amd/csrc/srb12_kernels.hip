@@ -1376,7 +1376,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
         int *__restrict__ iters_out)                                                                          \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
-        const int agent = blockIdx.x;                                                                          \
+        const int agent = xcd_agent(blockIdx.x, gridDim.x);                                                   \
         if (agent >= n_agents) return;                                                                         \
         srb12_agent<TL, TO, NC, K1>(prm, agent, x0g, xrefg, footg, contactg, obstacles, nbr_state, sel_g, x_qp_out,     \
                             x_out, obj_out, status_out, iters_out, lds);                                       \

@@ -1681,7 +1681,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride)                               \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
-        const int agent = blockIdx.x;                                                                          \
+        const int agent = xcd_agent(blockIdx.x, gridDim.x);                                                   \
         if (agent >= n_agents) return;                                                                         \
         nmpc_agent<NZL, TS, NW, NC, CC, KC>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
                                 x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, sel_g, \
@@ -1696,7 +1696,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
         const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride)                         \
     {                                                                                                          \
         extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
-        const int agent = blockIdx.x;                                                                          \
+        const int agent = xcd_agent(blockIdx.x, gridDim.x);                                                   \
         if (agent >= n_agents) return;                                                                         \
         polish_agent<NZL, TS, NW, NC, CC, KC>(prm, agent, x0g, refg, footg, obstacles, nbr_state, x_out, obj_out,          \
                                   status_out, alpha_buf, alpha_out, sel_g, zpol_g, zstride, lds);             \
@@ -1734,7 +1734,7 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
 {
     __shared__ double wd_lds[SRB_KNN_WAVES];
     __shared__ int wi_lds[SRB_KNN_WAVES];
-    const int agent = blockIdx.x, tid = threadIdx.x;
+    const int agent = xcd_agent(blockIdx.x, gridDim.x), tid = threadIdx.x;
     if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
     const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
     int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);

@@ -13,6 +13,19 @@
 
 typedef double d4 __attribute__((ext_vector_type(4)));
 
+// Agent of workgroup b in a grid of n one-agent workgroups, XCD-aware: the dispatcher deals
+// workgroups round-robin over the 8 XCDs (MI355X_MICROARCH.md, "Workgroup dispatch"; observed, not
+// promised -- only the traffic depends on it), so b and b + 8 share an L2.  Workgroups b = 8 j + x take
+// the x-th contiguous block of agents: neighbouring agents' inputs share 128-B lines, which a
+// round-robin assignment fetched once into each of up to four L2s (configs[2]: x0, ref, foot and the
+// selection rows 1.09 -> 0.73 MB per launch, tools/ubench/kernarg_fetch.hip).
+// A bijection of [0, n) for every n.
+__device__ __forceinline__ int xcd_agent(int b, int n)
+{
+    const int q = n >> 3, r = n & 7, x = b & 7;
+    return x * q + min(x, r) + (b >> 3);
+}
+
 // --------------------------------------------------------------------------- wave helpers
 // Cross-lane traffic stays in the VALU: DPP row permutations for the 16-lane rows and
 // gfx950's v_permlane16/32_swap across rows.  Every lane ends with the bit-identical
