@@ -443,7 +443,7 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     }
     if (c->timing) HIPCHK(hipEventRecord(c->ev[2], s));
     // the solve kernel, then (NLP stage) the active-set polish of its result: fused into the solve
-    // kernel's end (SRB_OPT_POLISH_FUSED, instances up to NZL 16), else srb_polish_kernel (same instance
+    // kernel's end (SRB_OPT_POLISH_FUSED, instances up to SRB_FUSED_POLISH_MAX = NZL 24), else srb_polish_kernel (same instance
     // geometry; it rewrites x / obj / alpha / status only where the polish is accepted)
     const bool fused = use_nlp && c->polish && c->polish_fused && SRB_FUSED_POLISH_OK(in->nzl);
     const bool polish = use_nlp && c->polish && !fused;

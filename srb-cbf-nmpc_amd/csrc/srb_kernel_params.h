@@ -48,8 +48,13 @@
 #define SRB_POLISH_ON 1
 #endif
 // instances whose solve kernel carries the fused polish (srb_kernels.hip; srb_capi.cpp launches the
-// polish kernel for the others)
-#define SRB_FUSED_POLISH_OK(NZL) ((NZL) <= 16)
+// polish kernel for the others).  Round 5: up to NZL 24 -- with the obstacle positions moved into the
+// Z'Z buffer (SRB_OBS_IN_ZZ) two N = 20 agents with the fused polish's buffer fit one CU's LDS, and
+// config 5 went 2.49 -> 2.33 ms (2.12 with the horizon compiled in, SRB_N20_NC)
+#ifndef SRB_FUSED_POLISH_MAX
+#define SRB_FUSED_POLISH_MAX 24
+#endif
+#define SRB_FUSED_POLISH_OK(NZL) ((NZL) <= SRB_FUSED_POLISH_MAX)
 
 // diagnostic trace buffer of the nlpdbg build (srb_kernels.hip, srb_capi.cpp)
 #define SRB_NLP_DBG_LEN (8 * 64 + 32 * 32 + 32 + 1024 + 256 + 3 * 256)
@@ -98,8 +103,9 @@ struct SrbKParams {
 // threads, see srb_kernels.hip), and the problem shape (N, C, K = K_obs + K_nbr) the instance is
 // compiled for -- 0: read at run time.  A compiled shape makes every LDS offset and loop bound of
 // the agent a constant (the bench shapes configs[1] and configs[2] / [3]: 12 % and 7 % faster steps;
-// the N = 20 shape compiled whole spilled to scratch and ran 16 % slower, with a different polish
-// outcome on a quarter of the agents, so its instance fixes C and K only: 1.7 % faster).  The
+// the N = 20 shape, configs[4] / config 5: compiled whole since round 5 -- the round-4 build of it
+// returned wrong polishes on a quarter of the agents, the code-generation hazard of DESIGN.md 11 that
+// tests/test_isa_hazard.py now scans every shipped kernel for; this one is clean and 9 % faster).  The
 // host launches the first fitting instance of this list (an exact shape first, then the run-time
 // ones) with NW = 4 for small batches (one agent per CU, all four SIMDs) and NW = 1 otherwise
 // (srb_capi.cpp).
@@ -110,8 +116,11 @@ struct SrbKParams {
 #define SRB_KERNEL_INSTANCES(X) SRB_DEV_INSTANCES(X)
 #else
 // the host picks the first fitting instance of this list (srb_capi.cpp), so its order matters
+#ifndef SRB_N20_NC               // horizon compiled into the configs[4]-shape instance (0: read at run time)
+#define SRB_N20_NC 20
+#endif
 #define SRB_KERNEL_INSTANCES(X) \
-    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) X(24, 4, 2, 0, 2, 11) \
+    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) X(24, 4, 2, SRB_N20_NC, 2, 11) \
     X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) X(12, 3, 1, 0, 0, 0) X(12, 4, 1, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(32, 4, 1, 0, 0, 0) X(32, 8, 1, 0, 0, 0) \
     X(8, 1, 4, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 1, 4, 0, 0, 0) X(16, 2, 4, 0, 0, 0) X(32, 2, 4, 0, 0, 0) \
@@ -120,7 +129,7 @@ struct SrbKParams {
 // srb_kernels.hip once per part (-DSRB_PART=0..3, in parallel)
 #define SRB_KI_PART0(X) X(12, 4, 1, 10, 2, 11) X(12, 4, 1, 0, 0, 0) X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) \
     X(12, 3, 1, 0, 0, 0) X(8, 1, 4, 0, 0, 0)
-#define SRB_KI_PART1(X) X(24, 4, 2, 0, 2, 11) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
+#define SRB_KI_PART1(X) X(24, 4, 2, SRB_N20_NC, 2, 11) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(12, 2, 2, 0, 0, 0)
 #define SRB_KI_PART2(X) X(12, 1, 4, 10, 2, 3) X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(16, 1, 4, 0, 0, 0) \
     X(16, 2, 4, 0, 0, 0) X(16, 2, 2, 0, 0, 0)
@@ -142,6 +151,10 @@ static inline int srb_r4(int x) { return (x + 3) & ~3; }
 #endif
 #define SRB_OBS_STORED(NZL) ((NZL) <= SRB_OBS_STORED_MAX)
 
+// the obstacle positions (2 N K + 2 doubles, read by the slots' setup only) share the Z'Z buffer when they
+// fit there: Z'Z is first written by the NLP setup's Gram, after every slot has read its position
+#define SRB_OBS_IN_ZZ(NZL, NK) (2 * (NK) + 2 <= (NZL) * ((NZL) + 1))
+
 static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
 {
     const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZL + 1;
@@ -151,7 +164,8 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N + (2 * NK + 2) +
+    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N +
+           (SRB_OBS_IN_ZZ(NZL, NK) ? 0 : 2 * NK + 2) +
            (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + (SRB_FUSED_POLISH_OK(NZL) ? srb_r4(srb_slots(N, C, K)) : 0)
 #ifdef SRB_STAMPS
            + 64

@@ -715,7 +715,7 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     double *xprev = p; p += n4;                   /* the iterate before the last update (non-finite fallback) */ \
     double *ref = p; p += 4 * N; \
     double *foot = p; p += 2 * C * N; \
-    double *obs = p; p += 2 * NK + 2; \
+    double *obs = SRB_OBS_IN_ZZ(NZL, NK) ? ZZ : p; p += SRB_OBS_IN_ZZ(NZL, NK) ? 0 : 2 * NK + 2;   /* obstacle positions (setup) */ \
     double *eps = p; p += K + 1; \
     double *zo = p; p += NK4;                     /* obstacle duals (per-grid sums) */ \
     double *dpos = p; p += 2 * N + 1;             /* Z_x dxi, Z_y dxi per grid, dxi_s (obstacle J dx) */ \
@@ -1549,7 +1549,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     // passes on the LDS state the NLP stage left (term rows, iterate) with the interior-point slots
     // reused as the polish's (their state is dead here), so an agent that finishes early polishes on
     // its own SIMD while slower agents still iterate, and nothing goes through HBM.  Compiled for the
-    // instances up to NZL 16 only: in the N = 20 ones (NZL 24) it raised the loop's spills 71 -> 123
+    // instances up to SRB_FUSED_POLISH_MAX (NZL 24 since round 5: N = 20 included, 28 B of scratch per lane
+    // in 24_4_2_20_2_11, config 5 2.49 -> 2.12 ms with the compiled horizon; NZL 32 keeps the kernel)
     if constexpr (SRB_FUSED_POLISH_OK(NZL))
     if (prm.polish_fused && prm.use_nlp && nlp_flag != 1 && nlp_flag != 3) {
         const int nts = (S + NTH - 1) / NTH;
