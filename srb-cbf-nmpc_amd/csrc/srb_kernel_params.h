@@ -119,8 +119,9 @@ struct SrbKParams {
 #ifndef SRB_N20_NC               // horizon compiled into the configs[4]-shape instance (0: read at run time)
 #define SRB_N20_NC 20
 #endif
+#define SRB_XE(X, ...) X(__VA_ARGS__)   // expands SRB_N20_NC before X pastes it into the kernel name
 #define SRB_KERNEL_INSTANCES(X) \
-    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) X(24, 4, 2, SRB_N20_NC, 2, 11) \
+    X(12, 4, 1, 10, 2, 11) X(12, 1, 4, 10, 2, 3) SRB_XE(X, 24, 4, 2, SRB_N20_NC, 2, 11) \
     X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) X(12, 3, 1, 0, 0, 0) X(12, 4, 1, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(32, 4, 1, 0, 0, 0) X(32, 8, 1, 0, 0, 0) \
     X(8, 1, 4, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 1, 4, 0, 0, 0) X(16, 2, 4, 0, 0, 0) X(32, 2, 4, 0, 0, 0) \
@@ -129,7 +130,7 @@ struct SrbKParams {
 // srb_kernels.hip once per part (-DSRB_PART=0..3, in parallel)
 #define SRB_KI_PART0(X) X(12, 4, 1, 10, 2, 11) X(12, 4, 1, 0, 0, 0) X(8, 1, 1, 0, 0, 0) X(16, 1, 1, 0, 0, 0) \
     X(12, 3, 1, 0, 0, 0) X(8, 1, 4, 0, 0, 0)
-#define SRB_KI_PART1(X) X(24, 4, 2, SRB_N20_NC, 2, 11) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
+#define SRB_KI_PART1(X) SRB_XE(X, 24, 4, 2, SRB_N20_NC, 2, 11) X(24, 4, 2, 0, 0, 0) X(12, 1, 4, 0, 0, 0) X(16, 4, 1, 0, 0, 0) \
     X(12, 2, 2, 0, 0, 0)
 #define SRB_KI_PART2(X) X(12, 1, 4, 10, 2, 3) X(24, 5, 1, 0, 0, 0) X(24, 8, 1, 0, 0, 0) X(16, 1, 4, 0, 0, 0) \
     X(16, 2, 4, 0, 0, 0) X(16, 2, 2, 0, 0, 0)

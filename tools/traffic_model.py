@@ -10,7 +10,9 @@ What the model counts, each term measured on its own by a microbenchmark (DESIGN
     rows) and the gathered table rows (obstacles 16 B, neighbour snapshot 32 B), with workgroups dealt
     round-robin over the 8 XCDs and each XCD given a contiguous block of agents (csrc/srb_wave.h xcd_agent);
   - outputs: bytes rounded to 32-B sectors per XCD block (kernarg_fetch.hip: 8-B stores cost 32 B each,
-    partially written lines are not filled from HBM).
+    partially written lines are not filled from HBM);
+  - spilled registers: the kernel's scratch bytes per lane x 64 x the resident waves (one per SIMD), written
+    back once.
 
     python tools/traffic_model.py [--config 3|5] [--round-robin]
 """
@@ -40,6 +42,9 @@ def code_sizes(lib):
                                  text=True, check=True).stdout
             for m in re.finditer(r"^\s*\d+:\s+[0-9a-f]+\s+(\d+)\s+FUNC\s+\w+\s+\w+\s+\d+\s+(\S+)$", txt, re.M):
                 out[m.group(2)] = int(m.group(1))
+            for m in re.finditer(r"^\s*\d+:\s+([0-9a-f]+)\s+0\s+NOTYPE\s+\w+\s+\w+\s+ABS\s+(\S+)\.private_seg_size$",
+                                 txt, re.M):
+                out[m.group(2) + ".scratch"] = int(m.group(1), 16)
     return out
 
 
@@ -86,13 +91,7 @@ def model(config, rr=False, lib=None):
         write[arr] = sum(SECTOR * len({o // SECTOR for a in ags for o in range(a * sz, a * sz + sz, 8)})
                          for ags in blocks(A, rr))
     code = code_sizes(lib or os.path.join(ROOT, "srb-cbf-nmpc_amd", "srbnmpc", "libsrbnmpc.so"))
-    zpol = 8 * ((srb_slots(N, C, K) + 3) // 4 * 4)      # the split polish's hand-off: 2 floats a row slot
-    return dict(A=A, N=N, C=C, K=K, nv=nv, fetch=fetch, write=write, code=code, zpol=zpol)
-
-
-def srb_slots(N, C, K):
-    """row slots of one agent (csrc/srb_kernel_params.h srb_slots)"""
-    return (6 + C) * N + 1 + 2 * (N - 1) + 2 * N + N * K
+    return dict(A=A, N=N, C=C, K=K, nv=nv, fetch=fetch, write=write, code=code)
 
 
 def main():
@@ -102,29 +101,22 @@ def main():
     ap.add_argument("--kernel", default=None, help="solve kernel symbol (default: the config's compiled instance)")
     a = ap.parse_args()
     m = model(a.config, a.round_robin)
-    inst = {3: "12_4_1_10_2_11", 5: "24_4_2_0_2_11"}.get(a.config)
+    inst = {3: "12_4_1_10_2_11", 5: "24_4_2_20_2_11"}.get(a.config)
     kern = a.kernel or "srb_nmpc_kernel_" + inst
-    split = a.config == 5                               # N = 20: the separate polish kernel (zpol hand-off)
     meas = {}
-    mp = os.path.join(ROOT, "profiles", f"r05x_pmc_traffic_c{a.config}.json")
-    if os.path.exists(mp) and not a.round_robin:
+    mp = os.path.join(ROOT, "profiles", {3: "r05x_pmc_traffic_c3.json", 5: "r05f_pmc_traffic_c5.json"}.get(a.config, ""))
+    if os.path.isfile(mp) and not a.round_robin:
         import json
         meas = json.load(open(mp))["kernels"]
-    A = m["A"]
-    inputs = sum(m["fetch"].values())
     rows = []                                           # (kernel, direction, [(term, bytes)], measured)
     fs = [(f"code {m['code'][kern]} B x {CODE_FACTOR}", m["code"][kern] * CODE_FACTOR)] + list(m["fetch"].items())
-    ws = list(m["write"].items()) + ([("zpol hand-off", A * m["zpol"])] if split else [])
     rows.append(("srb_nmpc_kernel", "fetch", fs, meas.get("srb_nmpc_kernel", {}).get("fetch_bytes")))
+    # spilled registers: each resident wave's scratch lines are written back once (one wave per SIMD)
+    nw = {3: 1, 5: 2}.get(a.config, 1)
+    scr = m["code"].get(kern + ".scratch", 0) * 64 * min(m["A"] * nw, 4 * 256)
+    ws = list(m["write"].items()) + ([(f"scratch {m['code'][kern + '.scratch']} B/lane, resident waves", scr)] if scr else [])
     rows.append(("srb_nmpc_kernel", "write", ws, meas.get("srb_nmpc_kernel", {}).get("write_bytes")))
-    if split:
-        pk = "srb_polish_kernel_" + inst
-        pf = [(f"code {m['code'][pk]} B x {CODE_FACTOR}", m["code"][pk] * CODE_FACTOR), ("inputs + table rows", inputs),
-              ("x (solve result)", m["write"]["x"]), ("zpol", A * m["zpol"])]
-        rows.append(("srb_polish_kernel", "fetch", pf, meas.get("srb_polish_kernel", {}).get("fetch_bytes")))
-        rows.append(("srb_polish_kernel", "write", list(m["write"].items()),
-                     meas.get("srb_polish_kernel", {}).get("write_bytes")))
-    print(f"config {a.config}: {A} agents, N = {m['N']}, C = {m['C']}, K = {m['K']}, "
+    print(f"config {a.config}: {m['A']} agents, N = {m['N']}, C = {m['C']}, K = {m['K']}, "
           f"{'round-robin' if a.round_robin else 'XCD-blocked'} agents")
     for k, d, terms, mv in rows:
         tot = sum(v for _, v in terms)
