@@ -39,6 +39,7 @@
 // Inputs/outputs are agent-major fp64 arrays in HBM, read once / written once.
 #include <hip/hip_runtime.h>
 #include <stdint.h>
+#include <type_traits>
 #include "srb_kernel_params.h"
 
 #define WAVE 64
@@ -148,7 +149,7 @@ __device__ __forceinline__ double term_elem(const double *R, const double *OJ, i
     const int o = r - rO;
     const double jx = OJ[2 * o], jy = OJ[2 * o + 1];
     const int xr = min(4 * (int)(((float)o + 0.5f) * invK), rO - 4);   // padding terms (jx = jy = 0) stay in R
-    return (col < NZL) ? fma(jx, R[xr * LDR + col], fma(jy, R[(xr + 2) * LDR + col], (col == nz - 1) ? -1.0 : 0.0)) : 0.0;
+    return (col < NZL) ? fma(jx, R[xr * LDR + col], fma(jy, R[(xr + 2) * LDR + col], (col == 0) ? -1.0 : 0.0)) : 0.0;
 }
 
 // Re-linearisation of obstacle row o at x: J_o = (jx, jy, -1) on (p_x(k), p_y(k), slack).  Stored-row
@@ -162,15 +163,54 @@ __device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, 
         double *dst = R + (rO + o) * LDR;
         const double *zx = R + i0 * LDR, *zy = R + i1 * LDR;
 #pragma unroll
-        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == nz - 1) ? -1.0 : 0.0));
+        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == 0) ? -1.0 : 0.0));
     } else {
         OJ[2 * o] = jx; OJ[2 * o + 1] = jy;
     }
 }
 
+// Highest reduced column term row t touches (columns: 0 the slack, 1 + j (C - 1) + i the i-th contact-weight
+// dof of grid j): X rows of grid k reach grid k, a CoM-CoP row of grid i grid i + 1, U / lambda rows their
+// own grid, obstacle rows of grid k grid k and the slack.  With NZM = 32 a batch of 16 terms whose rows all
+// stop below column 16 needs the (0,0) tile only (gram_rhs, rhs_only; `bmask` bit b = batch b needs all three).
+__device__ __forceinline__ int term_maxcol(int t, int N, int C, int n, int rC, int NE, int rU, int rO, int NK, int K)
+{
+    const int c1 = C - 1;
+    if (t < rC) return (t / 4 + 1) * c1;
+    if (t < rC + NE) return ((t - rC) / 2 + 2) * c1;
+    if (t < rU) return 0;
+    const int v = 4 * N + (t - rU);
+    if (v < 6 * N) return ((v - 4 * N) / 2 + 1) * c1;
+    if (v < n - 1) return ((v - 6 * N) / C + 1) * c1;
+    if (t < rO) return 0;
+    const int o = t - rO;
+    return (o < NK) ? (o / K + 1) * c1 : 0;
+}
+
+template <int NZM>
+__device__ __forceinline__ uint64_t full_batches(int TT, int N, int C, int n, int rC, int NE, int rU, int rO, int NK, int K,
+                                                 int lane)
+{
+    if constexpr (NZM == 16) return ~0ull;
+    int f = 0;
+    if (16 * lane < TT) {
+        int mx = 0;
+        for (int u = 0; u < 16; u++) mx = max(mx, term_maxcol(16 * lane + u, N, C, n, rC, NE, rU, rO, NK, K));
+        f = mx >= 16;
+    }
+    return __ballot(f) | ((TT > 16 * 64) ? (1ull << 63) : 0ull);   /* (more than 64 batches: the last bit covers the rest) */
+}
+
+__device__ __forceinline__ bool batch_full(uint64_t bmask, int t0)
+{
+    const int b = t0 >> 4;
+    return (bmask >> (b < 63 ? b : 63)) & 1ull;
+}
+
 template <int NZL, bool RHS, int NW>
 __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt, const double *OJ,
-                                         int rO, int nko, int K, double *H, double *g, int nz, int tid, double *part)
+                                         int rO, int nko, int K, double *H, double *g, int nz, int tid, double *part,
+                                         uint64_t bmask)
 {
     const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
@@ -184,13 +224,16 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     for (int t = 0; t < NT; t++) acc[t] = d4{0.0, 0.0, 0.0, 0.0};
 #pragma unroll
     for (int t = 0; t < NTC; t++) ps[t] = 0.0;
-    auto batch = [&](int t0, bool gen) {
+    // FULL: all NTC column blocks; otherwise block 0 only (every row of the batch is zero beyond column 15)
+    auto body = [&](int t0, bool gen, auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
+        constexpr int NB = FULL ? NTC : 1;
         double a[4][NTC], w[4], c[4];
 #pragma unroll
         for (int u = 0; u < 4; u++) {
             const int r = t0 + 4 * u + kq;
 #pragma unroll
-            for (int tc = 0; tc < NTC; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
+            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
             w[u] = W[r];
             c[u] = RHS ? CF[r] : 0.0;
         }
@@ -199,8 +242,8 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
         for (int u = 0; u < 4; u++) {
             if (RHS)
 #pragma unroll
-                for (int tc = 0; tc < NTC; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
-            if constexpr (NZM == 16) {
+                for (int tc = 0; tc < NB; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
+            if constexpr (NZM == 16 || !FULL) {
                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
             } else {
                 acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], w[u] * a[u][0], acc[0], 0, 0, 0);
@@ -208,6 +251,10 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
                 acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][NTC - 1], w[u] * a[u][NTC - 1], acc[2], 0, 0, 0);
             }
         }
+    };
+    auto batch = [&](int t0, bool gen) {
+        if (NZM == 16 || batch_full(bmask, t0)) body(t0, gen, std::integral_constant<bool, true>{});
+        else body(t0, gen, std::integral_constant<bool, false>{});
     };
     {
         const int chunk = cnt / NW, tb = wv * chunk;
@@ -281,7 +328,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 // eight term groups per batch so that 16 loads are in flight before the FMAs need them.
 template <int NZL, int NW>
 __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, const double *OJ, int rO, int nko,
-                                         int K, double *g, int nz, int tid, double *part)
+                                         int K, double *g, int nz, int tid, double *part, uint64_t bmask)
 {
     const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
@@ -291,23 +338,30 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
     double ps[2][NTC];
 #pragma unroll
     for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
+    auto chunk32 = [&](int t0, bool gen, auto fullc) {
+        constexpr int NB = decltype(fullc)::value ? NTC : 1;
+        double a[8][NTC], c[8];
+#pragma unroll
+        for (int u = 0; u < 8; u++) {
+            const int r = t0 + 4 * u + kq;
+            c[u] = CF[r];
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 8; u++)
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
+    };
     auto range = [&](int tb, int te, bool gen) {
         int t0 = tb;
 #pragma clang loop unroll(disable)
         for (; t0 + 32 <= te; t0 += 32) {
-            double a[8][NTC], c[8];
-#pragma unroll
-            for (int u = 0; u < 8; u++) {
-                const int r = t0 + 4 * u + kq;
-                c[u] = CF[r];
-#pragma unroll
-                for (int tc = 0; tc < NTC; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
-            }
-            __builtin_amdgcn_sched_barrier(0);
-#pragma unroll
-            for (int u = 0; u < 8; u++)
-#pragma unroll
-                for (int tc = 0; tc < NTC; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
+            if (NZM == 16 || batch_full(bmask, t0) || batch_full(bmask, t0 + 16))
+                chunk32(t0, gen, std::integral_constant<bool, true>{});
+            else
+                chunk32(t0, gen, std::integral_constant<bool, false>{});
         }
 #pragma clang loop unroll(disable)
         for (; t0 < te; t0 += 4) {
@@ -697,6 +751,7 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     const int rC = 4 * N, rU = rC + E4, rO = (rU + UL4 + 16 * NW - 1) / (16 * NW) * (16 * NW); \
     const int NKP = (NK + 16 * NW - 1) / (16 * NW) * (16 * NW), TT = rO + NKP; \
     const TermLayout TL{N, C, n, nz, E4}; \
+    const uint64_t bmask = full_batches<NZM>(TT, N, C, n, rC, NE, rU, rO, NK, K, lane);   /* batches needing every column block */ \
     const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK; \
     const double tol = prm.tol, th = tol / sqrt(3.0); \
     STAMP_DECL; \
@@ -749,8 +804,8 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
         } \
         xb[n - 1] = 0.0; \
     } \
-    for (int col = tid; col < nz - 1; col += NTH) { \
-        const int j = col / (C - 1), t = col % (C - 1); \
+    for (int cg = tid; cg < nz - 1; cg += NTH) {   /* column 1 + cg: dof t of grid j (column 0: the slack) */ \
+        const int j = cg / (C - 1), t = cg % (C - 1), col = cg + 1; \
         double lam[4]; \
         const int is_null = lambda_basis(foot + j * 2 * C, C, t, lam); \
         double g0 = 0.0, g1 = 0.0; \
@@ -769,7 +824,7 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
             for (int d = 0; d < 4; d++) v[d] = tt[d]; \
         } \
     } \
-    if (tid == 0) R[TL.zr(n - 1) * LDR + nz - 1] = 1.0; \
+    if (tid == 0) R[TL.zr(n - 1) * LDR] = 1.0; \
     SYNC(); \
     /* CoM-CoP term rows M_e = Z_p - Z_u (p: CoM of grid i, u: CoP of grid i+1); xs = xbar */ \
     if (tid < NE) { \
@@ -884,7 +939,7 @@ _Pragma("unroll")                                                               
                     __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);                                   \
                 }                                                                                                                             \
             SYNC();                                                                                                                           \
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);                                                    \
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);                                                    \
             SYNC();                                                                                                                           \
             if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);                                                                           \
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
@@ -1058,7 +1113,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
             if (gj_reduced<NZL>(Mi, nz, lane, 1) != 0) {
@@ -1187,7 +1242,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     __hip_atomic_fetch_add(&CF[Q[t].r], Q[t].m[0] * Q[t].z[0] - Q[t].m[1] * Q[t].z[1], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, ZZ, vg, nz, tid, part);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, ZZ, vg, nz, tid, part, bmask);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_reduced<NZL>(Mi, nz, lane, 0);
@@ -1376,7 +1431,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 set_rhs(0);
                 SYNC();
                 STAMP_END(17);
-                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part);
+                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);
                 SYNC();
                 STAMP_END(4);
                 double dstart = 0.0;
@@ -1404,7 +1459,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     set_rhs(pass);
                     SYNC();
                     STAMP_END(6 + 4 * pass);
-                    rhs_only<NZL, NW>(R, CF, cnt, OJ, rO, nko, K, vg, nz, tid, part);
+                    rhs_only<NZL, NW>(R, CF, cnt, OJ, rO, nko, K, vg, nz, tid, part, bmask);
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }

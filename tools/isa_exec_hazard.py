@@ -101,6 +101,7 @@ def region_open(body, i):
 def scan(body):
     """(line index, copy line, register) for every hazardous copy in one kernel body."""
     execz_targets = set(re.findall(r"s_cbranch_execz\s+(\.LBB\w+)", "\n".join(body)))
+    labels = {m.group(1): k for k, ln in enumerate(body) for m in [re.match(r"^(\.LBB\w+):", ln)] if m}
     found = []
     for i, ln in enumerate(body):
         if not re.match(r"^\s*s_or_b64\s+exec,\s*exec,", ln):
@@ -184,23 +185,50 @@ def scan(body):
                 wop, wdst, _ = split_operands(w)
                 if wop and not wop.startswith((";", "global_store", "ds_write", "scratch_store", "buffer_store")):
                     dregs -= regs(wdst)
-            # ... and read after the restore before a redefinition (linear scan to the next exec change)
-            live = set(dregs)
-            for u in body[i + 1:i + 400]:
-                uop, udst, usrc = split_operands(u)
-                if not uop or uop.startswith(";"):
-                    continue
-                used = regs(usrc) | (regs(udst) if uop.startswith(("global_store", "ds_write", "scratch_store",
-                                                                     "buffer_store", "v_cmp", "s_")) else set())
-                if live & used:
-                    found.append((k, t.strip(), sorted(live & used)))
-                    break
-                if uop.startswith(("global_store", "ds_write", "scratch_store", "buffer_store")):
-                    continue
-                live -= regs(udst)
-                if not live or re.match(r"^\s*s_\w+\s+exec", u) or "s_endpgm" in u:
-                    break
+            # ... and read after the restore before a redefinition: every path from the restore (branches
+            # followed: s_branch jumps, s_cbranch forks), each ending at a redefinition, the next exec change
+            # or the end of the program
+            used_regs = read_before_redefined(body, i + 1, set(dregs), labels)
+            if used_regs:
+                found.append((k, t.strip(), sorted(used_regs)))
     return found
+
+
+STORES = ("global_store", "ds_write", "scratch_store", "buffer_store")
+
+
+def read_before_redefined(body, start, live0, labels, budget=6000):
+    """Registers of live0 read on some path from body[start] before that path redefines them."""
+    hits, seen, work, steps = set(), set(), [(start, frozenset(live0))], 0
+    while work and steps < budget:
+        pos, live = work.pop()
+        while pos < len(body) and live and steps < budget:
+            if (pos, live) in seen:
+                break
+            seen.add((pos, live))
+            steps += 1
+            u = body[pos]
+            uop, udst, usrc = split_operands(u)
+            if not uop or uop.startswith((";", ".")) or uop.endswith(":"):
+                pos += 1
+                continue
+            used = regs(usrc) | (regs(udst) if uop.startswith(STORES + ("v_cmp", "s_")) else set())
+            if live & used:
+                hits |= live & used
+                break
+            if not uop.startswith(STORES):
+                live = live - regs(udst)
+            if re.match(r"^\s*s_\w+\s+exec", u) or "s_endpgm" in u or "s_setpc" in u:
+                break
+            m = re.match(r"^\s*s_branch\s+(\.LBB\w+)", u)
+            if m:
+                pos = labels.get(m.group(1), len(body))
+                continue
+            m = re.match(r"^\s*s_cbranch_\w+\s+(\.LBB\w+)", u)
+            if m and m.group(1) in labels:
+                work.append((labels[m.group(1)], live))
+            pos += 1
+    return hits
 
 
 def main():
