@@ -143,10 +143,10 @@ static inline int srb_r4(int x) { return (x + 3) & ~3; }
 
 // doubles of dynamic LDS one agent needs for instance bound NZL; must match the carve in
 // nmpc_agent (srb_kernels.hip)
-// Obstacle term rows: materialised in LDS at each re-linearisation for the small instances
-// (NZL <= SRB_OBS_STORED_MAX: the rows fit and a stored row is one LDS load per Gram element),
-// generated inside the Gram from the grid's CoM rows and (jx, jy) for the large ones, where the
-// N K stored rows would fill the LDS (N = 20: 1 agent per CU instead of 2)
+// Obstacle rows: materialised as term rows in LDS at each re-linearisation for the small instances
+// (NZL <= SRB_OBS_STORED_MAX: a stored row is one LDS load per Gram element), folded per grid into three
+// terms built from the grid's CoM rows for the large ones (srb_kernels.hip ObsFold: at N = 20 the Gram's
+// obstacle part 14 -> 4 batches; at configs[1] / [2] the fold measured 7 % / 1.6 % slower than stored rows)
 #ifndef SRB_OBS_STORED_MAX
 #define SRB_OBS_STORED_MAX 16
 #endif
@@ -162,10 +162,11 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
     const int q = 16 * NW;
     const int rO = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + q - 1) / q * q;   // stored term rows
-    const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;                                     // + obstacle terms
+    const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;          // + the obstacle rows' W / CF / (jx, jy) entries
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;
-    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP) + 2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N +
+    return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP + 9 * (N + 1)) +
+           2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N +
            (SRB_OBS_IN_ZZ(NZL, NK) ? 0 : 2 * NK + 2) +
            (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + (SRB_FUSED_POLISH_OK(NZL) ? srb_r4(srb_slots(N, C, K)) : 0)
 #ifdef SRB_STAMPS

@@ -115,65 +115,55 @@ __device__ int srb_nlp_dbg_agent = -1;
 #endif
 
 // --------------------------------------------------------------------------- term rows
-// Term row t (Z row of a variable, M_e, M_o) at R + t * LDR; LDR = NZL + 1 (odd: lane-
-// parallel row reads stay conflict-free).  Rows are zero beyond nz and beyond the count.
-// Row order: X rows (4N) | CoM-CoP rows | U, lambda, slack rows | obstacle rows.
+// Term row t (Z row of a variable, M_e) at R + t * LDR; LDR = NZL + 1 (odd: lane-parallel row reads stay
+// conflict-free).  Rows are zero beyond nz and beyond the count.  Row order: X rows (4N) | CoM-CoP rows |
+// U, lambda, slack rows.  Reduced columns: 0 the slack, 1 + j (C - 1) + i the i-th contact-weight dof of
+// grid j.
 struct TermLayout {
     int N, C, n, nz, E4;
     __device__ __forceinline__ int zr(int v) const { return v < 4 * N ? v : v + E4; }
 };
 
-// GRAM: H = sum_t W_t r_t r_t' over the stored term rows [0, cnt) and the generated obstacle
-//   term rows [rO, rO + nko): v_mfma_f64_16x16x4f64 with A[a][k] = r_{t0+k}[a],
-//   B[k][b] = W_{t0+k} r_{t0+k}[b]; lane l supplies term t0 + (l >> 4), column l & 15; D layout
-//   row (l >> 4) + 4 q, column l & 15; NZM = 32: tiles (0,0), (0,1), (1,1).  Four term groups per
-//   batch: every operand load of the batch issues before the first MFMA waits on one.
-// Obstacle rows are not stored: M_o = J_o Z = jx Z_x + jy Z_y - e_s (Z_x, Z_y: the stored Z rows of
-//   the grid's CoM position; OJ[2 o] = jx, OJ[2 o + 1] = jy; grid k = o / K), built in
-//   registers from two row loads -- the re-linearisation each iteration is two numbers per row
-//   instead of a stored row, and at N = 20 the rows no longer fill the LDS (2 agents per CU).
-// RHS: g[a] = sum_t CF_t r_t[a]: the very element lane l forms for the MFMA is the one its
-//   (column, term) pair needs, so the right-hand side costs one FMA per element; the four term
-//   chunks combine by permlane swaps.
-// cnt and nko are multiples of 16 NW; W / CF / OJ are zero beyond every real row.
-// NW > 1: wave w takes the w-th NW-th of both ranges; the per-wave partial tiles / right-hand
-// sides are summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
-// (obstacle term o belongs to grid k = o / K, whose CoM-position Z rows are 4k and 4k + 2: the row
-// index is formed in registers -- from a loaded index the row loads would wait on that load)
-template <int NZL>
-__device__ __forceinline__ double term_elem(const double *R, const double *OJ, int r, int rO, int col, int nz, bool gen,
-                                            float invK)
-{
-    constexpr int LDR = NZL + 1;
-    if (!gen) return (col < NZL) ? R[r * LDR + col] : 0.0;
-    const int o = r - rO;
-    const double jx = OJ[2 * o], jy = OJ[2 * o + 1];
-    const int xr = min(4 * (int)(((float)o + 0.5f) * invK), rO - 4);   // padding terms (jx = jy = 0) stay in R
-    return (col < NZL) ? fma(jx, R[xr * LDR + col], fma(jy, R[(xr + 2) * LDR + col], (col == 0) ? -1.0 : 0.0)) : 0.0;
-}
+// Obstacle rows, folded per grid (round 5).  Row o = k K + j of grid k is M_o = J_o Z = jx Z_x + jy Z_y - e_s
+// (Z_x, Z_y: the stored Z rows 4k, 4k + 2 of the grid's CoM position; OJ[2 o] = jx, OJ[2 o + 1] = jy, set
+// by the re-linearisation).  With V_k = [Z_x, Z_y, e_s] and v_o = (jx, jy, -1), the K rows of a grid add
+//   sum_j W_o M_o M_o' = V_k S_k V_k',  S_k = sum_j W_o v_o v_o'   and   sum_j CF_o M_o = V_k c_k,  c_k = sum_j CF_o v_o
+// to the Gram and the right-hand side: 3 terms a grid instead of K rows (obs_fold forms S_k, c_k; the
+// Gram's term (k, u) has A = column u of V_k, B = V_k S_k e_u).  FO holds S_k (00 01 02 11 12 22) and c_k per
+// grid, 9 doubles, and a zero entry at grid N for the padding terms.
+struct ObsFold {
+    const double *OJ;
+    double *FO;
+    int rO, N, K, NOP;                 // obstacle rows' W / CF offset, grids, rows per grid, 3N padded to 16 NW
+    uint64_t mask;                     // NZM = 32: grid-term batches that reach column 16 (all three tiles)
+};
 
-// Re-linearisation of obstacle row o at x: J_o = (jx, jy, -1) on (p_x(k), p_y(k), slack).  Stored-row
-// instances (SRB_OBS_STORED(NZL)) materialise its term row in R, M_o = jx Z_x(k) + jy Z_y(k) - e_s
-// (i0 = 4k, i1 = 4k + 2: the grid's CoM rows); the others keep (jx, jy) in OJ for gram_rhs
-template <int NZL>
-__device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, int i0, int i1, double jx, double jy, int nz)
+// S_k and c_k (GRAM) or c_k alone into FO: one lane per grid, the K rows in index order
+template <bool GRAM>
+__device__ __forceinline__ void obs_fold(const double *W, const double *CF, const ObsFold &F, int tid, int NTH)
 {
-    if constexpr (SRB_OBS_STORED(NZL)) {
-        constexpr int LDR = NZL + 1;
-        double *dst = R + (rO + o) * LDR;
-        const double *zx = R + i0 * LDR, *zy = R + i1 * LDR;
-#pragma unroll
-        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == 0) ? -1.0 : 0.0));
-    } else {
-        OJ[2 * o] = jx; OJ[2 * o + 1] = jy;
+    for (int k = tid; k < F.N; k += NTH) {
+        double s00 = 0.0, s01 = 0.0, s02 = 0.0, s11 = 0.0, s12 = 0.0, s22 = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
+        for (int j = 0; j < F.K; j++) {
+            const int o = k * F.K + j;
+            const double cf = CF[F.rO + o], jx = F.OJ[2 * o], jy = F.OJ[2 * o + 1];
+            c0 = fma(cf, jx, c0); c1 = fma(cf, jy, c1); c2 -= cf;
+            if (GRAM) {
+                const double w = W[F.rO + o], wx = w * jx, wy = w * jy;
+                s00 = fma(wx, jx, s00); s01 = fma(wx, jy, s01); s02 -= wx; s11 = fma(wy, jy, s11); s12 -= wy; s22 += w;
+            }
+        }
+        double *f = F.FO + 9 * k;
+        if (GRAM) { f[0] = s00; f[1] = s01; f[2] = s02; f[3] = s11; f[4] = s12; f[5] = s22; }
+        f[6] = c0; f[7] = c1; f[8] = c2;
     }
 }
 
-// Highest reduced column term row t touches (columns: 0 the slack, 1 + j (C - 1) + i the i-th contact-weight
-// dof of grid j): X rows of grid k reach grid k, a CoM-CoP row of grid i grid i + 1, U / lambda rows their
-// own grid, obstacle rows of grid k grid k and the slack.  With NZM = 32 a batch of 16 terms whose rows all
-// stop below column 16 needs the (0,0) tile only (gram_rhs, rhs_only; `bmask` bit b = batch b needs all three).
-__device__ __forceinline__ int term_maxcol(int t, int N, int C, int n, int rC, int NE, int rU, int rO, int NK, int K)
+// Highest reduced column term row t (t < rO) touches: X rows of grid k reach grid k, a CoM-CoP row of grid i
+// grid i + 1, U / lambda rows their own grid.  With NZM = 32 a batch of 16 terms whose rows all stop below
+// column 16 needs the (0,0) tile only (gram_rhs, rhs_only; `bmask` bit b = batch b needs all three; the
+// obstacle grid terms likewise in ObsFold::mask).
+__device__ __forceinline__ int term_maxcol(int t, int N, int C, int n, int rC, int NE, int rU)
 {
     const int c1 = C - 1;
     if (t < rC) return (t / 4 + 1) * c1;
@@ -182,23 +172,28 @@ __device__ __forceinline__ int term_maxcol(int t, int N, int C, int n, int rC, i
     const int v = 4 * N + (t - rU);
     if (v < 6 * N) return ((v - 4 * N) / 2 + 1) * c1;
     if (v < n - 1) return ((v - 6 * N) / C + 1) * c1;
-    if (t < rO) return 0;
-    const int o = t - rO;
-    return (o < NK) ? (o / K + 1) * c1 : 0;
+    return 0;                                                    // slack row (column 0), padding
 }
 
 template <int NZM>
-__device__ __forceinline__ uint64_t full_batches(int TT, int N, int C, int n, int rC, int NE, int rU, int rO, int NK, int K,
-                                                 int lane)
+__device__ __forceinline__ uint64_t full_batches(int rO, int N, int C, int n, int rC, int NE, int rU, int lane)
 {
     if constexpr (NZM == 16) return ~0ull;
     int f = 0;
-    if (16 * lane < TT) {
+    if (16 * lane < rO) {
         int mx = 0;
-        for (int u = 0; u < 16; u++) mx = max(mx, term_maxcol(16 * lane + u, N, C, n, rC, NE, rU, rO, NK, K));
+        for (int u = 0; u < 16; u++) mx = max(mx, term_maxcol(16 * lane + u, N, C, n, rC, NE, rU));
         f = mx >= 16;
     }
-    return __ballot(f) | ((TT > 16 * 64) ? (1ull << 63) : 0ull);   /* (more than 64 batches: the last bit covers the rest) */
+    return __ballot(f) | ((rO > 16 * 64) ? (1ull << 63) : 0ull);   /* (more than 64 batches: the last bit covers the rest) */
+}
+
+template <int NZM>
+__device__ __forceinline__ uint64_t full_obs_batches(int N, int C, int NOP, int lane)
+{
+    if constexpr (NZM == 16) return ~0ull;
+    const int kmax = min((16 * lane + 15) / 3, N - 1);
+    return __ballot(16 * lane < NOP && (kmax + 1) * (C - 1) >= 16) | ((NOP > 16 * 64) ? (1ull << 63) : 0ull);
 }
 
 __device__ __forceinline__ bool batch_full(uint64_t bmask, int t0)
@@ -207,17 +202,52 @@ __device__ __forceinline__ bool batch_full(uint64_t bmask, int t0)
     return (bmask >> (b < 63 ? b : 63)) & 1ull;
 }
 
-template <int NZL, bool RHS, int NW>
-__device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt, const double *OJ,
-                                         int rO, int nko, int K, double *H, double *g, int nz, int tid, double *part,
-                                         uint64_t bmask)
+// element `col` of stored term row r
+template <int NZL>
+__device__ __forceinline__ double term_elem(const double *R, int r, int col)
 {
-    const float invK = 1.0f / (float)(K > 0 ? K : 1);
+    constexpr int LDR = NZL + 1;
+    return (col < NZL) ? R[r * LDR + col] : 0.0;
+}
+
+// obstacle grid term t = 3 k + u: A element (column u of V_k) for column col, and the row of S_k / entry of
+// c_k it pairs with (padding terms: grid N, all zero)
+template <int NZL>
+__device__ __forceinline__ double obs_term_a(const double *R, const ObsFold &F, int t, int col, double &zx, double &zy)
+{
+    constexpr int LDR = NZL + 1;
+    const int k = t / 3, u = t - 3 * k, xr = 4 * min(k, F.N - 1);
+    zx = (col < NZL) ? R[xr * LDR + col] : 0.0;
+    zy = (col < NZL) ? R[(xr + 2) * LDR + col] : 0.0;
+    const double es = (col == 0) ? 1.0 : 0.0;
+    return (u == 0) ? zx : (u == 1) ? zy : es;
+}
+
+// GRAM: H = sum_t W_t r_t r_t' over the stored term rows [0, cnt) plus the folded obstacle grid terms
+//   [0, NOP) (when nko > 0, the NLP stage): v_mfma_f64_16x16x4f64 with A[a][k] = r_{t0+k}[a],
+//   B[k][b] = W_{t0+k} r_{t0+k}[b] (grid terms: B = V_k S_k e_u); lane l supplies term t0 + (l >> 4),
+//   column l & 15; D layout row (l >> 4) + 4 q, column l & 15; NZM = 32: tiles (0,0), (0,1), (1,1).  Four
+//   term groups per batch: every operand load of the batch issues before the first MFMA waits on one.
+// RHS: g[a] = sum_t CF_t r_t[a]: the very element lane l forms for the MFMA is the one its (column, term)
+//   pair needs, so the right-hand side costs one FMA per element; the four term chunks combine by permlane
+//   swaps.
+// cnt and NOP are multiples of 16 NW; W / CF are zero beyond every real row.
+// NW > 1: wave w takes the w-th NW-th of both ranges; the per-wave partial tiles / right-hand sides are
+// summed through LDS (`part`: NW x NT x 256 + NW x NZM doubles).
+template <int NZL, bool RHS, int NW>
+__device__ __forceinline__ void gram_rhs(const double *R, const double *W, const double *CF, int cnt, const ObsFold &F,
+                                         int nko, double *H, double *g, int nz, int tid, double *part, uint64_t bmask)
+{
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int LDH = NZL + 1;            // H holds rows / columns < NZL only (the rest of the tiles are 0)
     constexpr int NT = (NZM == 16) ? 1 : 3, NTC = NZM / 16;
     const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
+    constexpr bool FOLD = !SRB_OBS_STORED(NZL);
+    if (FOLD && nko > 0) {
+        obs_fold<true>(W, CF, F, tid, 64 * NW);
+        srb_sync<NW>();
+    }
     d4 acc[NT];
     double ps[NTC];
 #pragma unroll
@@ -225,7 +255,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 #pragma unroll
     for (int t = 0; t < NTC; t++) ps[t] = 0.0;
     // FULL: all NTC column blocks; otherwise block 0 only (every row of the batch is zero beyond column 15)
-    auto body = [&](int t0, bool gen, auto fullc) {
+    auto body = [&](int t0, auto fullc) {
         constexpr bool FULL = decltype(fullc)::value;
         constexpr int NB = FULL ? NTC : 1;
         double a[4][NTC], w[4], c[4];
@@ -233,7 +263,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
         for (int u = 0; u < 4; u++) {
             const int r = t0 + 4 * u + kq;
 #pragma unroll
-            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
+            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, r, 16 * tc + li);
             w[u] = W[r];
             c[u] = RHS ? CF[r] : 0.0;
         }
@@ -252,17 +282,59 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
             }
         }
     };
-    auto batch = [&](int t0, bool gen) {
-        if (NZM == 16 || batch_full(bmask, t0)) body(t0, gen, std::integral_constant<bool, true>{});
-        else body(t0, gen, std::integral_constant<bool, false>{});
+    // folded obstacle grid terms t0 .. t0 + 15
+    auto obody = [&](int t0, auto fullc) {
+        constexpr bool FULL = decltype(fullc)::value;
+        constexpr int NB = FULL ? NTC : 1;
+        double a[4][NTC], b[4][NTC], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + 4 * u + kq, k = t / 3, uu = t - 3 * k;
+            const double *f = F.FO + 9 * min(k, F.N);
+            const int i1 = (uu == 0) ? 1 : (uu == 1) ? 3 : 4, i2 = (uu == 0) ? 2 : (uu == 1) ? 4 : 5;
+            const double s0 = f[uu], s1 = f[i1], s2 = f[i2];
+            c[u] = RHS ? f[6 + uu] : 0.0;
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) {
+                double zx, zy;
+                a[u][tc] = obs_term_a<NZL>(R, F, t, 16 * tc + li, zx, zy);
+                b[u][tc] = fma(s0, zx, fma(s1, zy, (16 * tc + li == 0) ? s2 : 0.0));
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            if (RHS)
+#pragma unroll
+                for (int tc = 0; tc < NB; tc++) ps[tc] = fma(c[u], a[u][tc], ps[tc]);
+            if constexpr (NZM == 16 || !FULL) {
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], b[u][0], acc[0], 0, 0, 0);
+            } else {
+                acc[0] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], b[u][0], acc[0], 0, 0, 0);
+                acc[1] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][0], b[u][NTC - 1], acc[1], 0, 0, 0);
+                acc[2] = __builtin_amdgcn_mfma_f64_16x16x4f64(a[u][NTC - 1], b[u][NTC - 1], acc[2], 0, 0, 0);
+            }
+        }
     };
     {
         const int chunk = cnt / NW, tb = wv * chunk;
 #pragma clang loop unroll(disable)
-        for (int t0 = tb; t0 < tb + chunk; t0 += 16) batch(t0, false);
-        const int och = nko / NW, ob = rO + wv * och;
+        for (int t0 = tb; t0 < tb + chunk; t0 += 16) {
+            if (NZM == 16 || batch_full(bmask, t0)) body(t0, std::integral_constant<bool, true>{});
+            else body(t0, std::integral_constant<bool, false>{});
+        }
+        if (FOLD && nko > 0) {
+            const int och = F.NOP / NW, ob = wv * och;
 #pragma clang loop unroll(disable)
-        for (int t0 = ob; t0 < ob + och; t0 += 16) batch(t0, !SRB_OBS_STORED(NZL));
+            for (int t0 = ob; t0 < ob + och; t0 += 16) {
+                if (NZM == 16 || batch_full(F.mask, t0)) obody(t0, std::integral_constant<bool, true>{});
+                else obody(t0, std::integral_constant<bool, false>{});
+            }
+        } else if (nko > 0) {                       // stored obstacle rows [rO, rO + nko)
+            const int och = nko / NW, ob = F.rO + wv * och;
+#pragma clang loop unroll(disable)
+            for (int t0 = ob; t0 < ob + och; t0 += 16) body(t0, std::integral_constant<bool, true>{});
+        }
     }
     double gs[NTC];
     if (RHS)
@@ -324,21 +396,25 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
     }
 }
 
-// g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping and term ranges as gram_rhs,
-// eight term groups per batch so that 16 loads are in flight before the FMAs need them.
+// g[a] = sum_t CF_t r_t[a] alone (corrector): same lane mapping and term ranges as gram_rhs (c_k refolded,
+// S_k kept), eight term groups per batch so that 16 loads are in flight before the FMAs need them.
 template <int NZL, int NW>
-__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, const double *OJ, int rO, int nko,
-                                         int K, double *g, int nz, int tid, double *part, uint64_t bmask)
+__device__ __forceinline__ void rhs_only(const double *R, const double *CF, int cnt, const ObsFold &F, int nko, double *g,
+                                         int nz, int tid, double *part, uint64_t bmask)
 {
-    const float invK = 1.0f / (float)(K > 0 ? K : 1);
     constexpr int NZM = ((NZL + 15) / 16) * 16;
     constexpr int NTC = NZM / 16;
     const int lane = tid & 63, wv = tid >> 6;
     const int li = lane & 15, kq = lane >> 4;
+    constexpr bool FOLD = !SRB_OBS_STORED(NZL);
+    if (FOLD && nko > 0) {
+        obs_fold<false>(nullptr, CF, F, tid, 64 * NW);
+        srb_sync<NW>();
+    }
     double ps[2][NTC];
 #pragma unroll
     for (int t = 0; t < NTC; t++) { ps[0][t] = 0.0; ps[1][t] = 0.0; }
-    auto chunk32 = [&](int t0, bool gen, auto fullc) {
+    auto chunk32 = [&](int t0, auto fullc) {
         constexpr int NB = decltype(fullc)::value ? NTC : 1;
         double a[8][NTC], c[8];
 #pragma unroll
@@ -346,7 +422,7 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
             const int r = t0 + 4 * u + kq;
             c[u] = CF[r];
 #pragma unroll
-            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK);
+            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, r, 16 * tc + li);
         }
         __builtin_amdgcn_sched_barrier(0);
 #pragma unroll
@@ -354,28 +430,57 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
             for (int tc = 0; tc < NB; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
     };
-    auto range = [&](int tb, int te, bool gen) {
+    auto ochunk16 = [&](int t0, auto fullc) {
+        constexpr int NB = decltype(fullc)::value ? NTC : 1;
+        double a[4][NTC], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int t = t0 + 4 * u + kq, k = t / 3, uu = t - 3 * k;
+            c[u] = F.FO[9 * min(k, F.N) + 6 + uu];
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) {
+                double zx, zy;
+                a[u][tc] = obs_term_a<NZL>(R, F, t, 16 * tc + li, zx, zy);
+            }
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
+    };
+    auto range = [&](int tb, int te, bool st) {     // stored rows [tb, te) (st: the stored obstacle rows)
         int t0 = tb;
 #pragma clang loop unroll(disable)
         for (; t0 + 32 <= te; t0 += 32) {
-            if (NZM == 16 || batch_full(bmask, t0) || batch_full(bmask, t0 + 16))
-                chunk32(t0, gen, std::integral_constant<bool, true>{});
+            if (NZM == 16 || st || batch_full(bmask, t0) || batch_full(bmask, t0 + 16))
+                chunk32(t0, std::integral_constant<bool, true>{});
             else
-                chunk32(t0, gen, std::integral_constant<bool, false>{});
+                chunk32(t0, std::integral_constant<bool, false>{});
         }
 #pragma clang loop unroll(disable)
         for (; t0 < te; t0 += 4) {
             const int r = t0 + kq;
             const double cc = CF[r];
 #pragma unroll
-            for (int tc = 0; tc < NTC; tc++) ps[0][tc] = fma(cc, term_elem<NZL>(R, OJ, r, rO, 16 * tc + li, nz, gen, invK), ps[0][tc]);
+            for (int tc = 0; tc < NTC; tc++) ps[0][tc] = fma(cc, term_elem<NZL>(R, r, 16 * tc + li), ps[0][tc]);
         }
     };
     {
         const int chunk = cnt / NW, tb = wv * chunk;
         range(tb, tb + chunk, false);
-        const int och = nko / NW, ob = rO + wv * och;
-        range(ob, ob + och, !SRB_OBS_STORED(NZL));
+        if (!FOLD && nko > 0) {
+            const int och = nko / NW, ob = F.rO + wv * och;
+            range(ob, ob + och, true);
+        }
+        if (FOLD && nko > 0) {
+            const int och = F.NOP / NW, ob = wv * och;
+#pragma clang loop unroll(disable)
+            for (int o0 = ob; o0 < ob + och; o0 += 16) {
+                if (NZM == 16 || batch_full(F.mask, o0)) ochunk16(o0, std::integral_constant<bool, true>{});
+                else ochunk16(o0, std::integral_constant<bool, false>{});
+            }
+        }
     }
     double sv[NTC];
 #pragma unroll
@@ -400,6 +505,23 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
             for (int w2 = 0; w2 < NW; w2++) v += part[w2 * NZM + tid];
             g[tid] = v;
         }
+    }
+}
+
+// Re-linearisation of obstacle row o at x: J_o = (jx, jy, -1) on (p_x(k), p_y(k), slack).  Stored-row
+// instances (SRB_OBS_STORED(NZL)) materialise its term row in R, M_o = jx Z_x(k) + jy Z_y(k) - e_s
+// (i0 = 4k, i1 = 4k + 2: the grid's CoM rows); the others keep (jx, jy) in OJ for the fold (ObsFold)
+template <int NZL>
+__device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, int i0, int i1, double jx, double jy)
+{
+    if constexpr (SRB_OBS_STORED(NZL)) {
+        constexpr int LDR = NZL + 1;
+        double *dst = R + (rO + o) * LDR;
+        const double *zx = R + i0 * LDR, *zy = R + i1 * LDR;
+#pragma unroll
+        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == 0) ? -1.0 : 0.0));
+    } else {
+        OJ[2 * o] = jx; OJ[2 * o + 1] = jy;
     }
 }
 
@@ -686,7 +808,7 @@ __device__ __forceinline__ void polish_rows(Slot (&Q)[TS], int nts, const double
             q.jd = slot_f(q, xs, s_var);
             if (kind_of(q) == K_OBS) {
                 const int o = q.r - rO;
-                obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
+                obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1));
                 zo[o] = q.ds[0] * q.dz[0];
             }
         }
@@ -751,16 +873,19 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     const int rC = 4 * N, rU = rC + E4, rO = (rU + UL4 + 16 * NW - 1) / (16 * NW) * (16 * NW); \
     const int NKP = (NK + 16 * NW - 1) / (16 * NW) * (16 * NW), TT = rO + NKP; \
     const TermLayout TL{N, C, n, nz, E4}; \
-    const uint64_t bmask = full_batches<NZM>(TT, N, C, n, rC, NE, rU, rO, NK, K, lane);   /* batches needing every column block */ \
+    const uint64_t bmask = full_batches<NZM>(rO, N, C, n, rC, NE, rU, lane);   /* stored-row batches needing every column block */ \
+    const int NOP = (3 * N + 16 * NW - 1) / (16 * NW) * (16 * NW);   /* folded obstacle grid terms (3 a grid), padded */ \
     const int sE = n, sV = n + NE, sO = sV + 2 * N, S = sO + NK; \
     const double tol = prm.tol, th = tol / sqrt(3.0); \
     STAMP_DECL; \
     /* LDS carve (must match srb_lds_doubles) */ \
     double *p = lds; \
-    double *R = p; p += (SRB_OBS_STORED(NZL) ? TT : rO) * LDR;   /* stored term rows (Z rows first) */ \
+    double *R = p; p += (SRB_OBS_STORED(NZL) ? TT : rO) * LDR;   /* stored term rows (Z rows first; + obstacle rows) */ \
     double *W = p; p += TT + 1;                   /* gram weights (+ one scratch entry) */ \
     double *CF = p; p += TT + 1;                  /* rhs coefficients (+ one scratch entry) */ \
-    double *OJ = p; p += SRB_OBS_STORED(NZL) ? 0 : 2 * NKP;   /* generated obstacle terms: jx, jy (gram_rhs) */ \
+    double *OJ = p; p += SRB_OBS_STORED(NZL) ? 0 : 2 * NKP;       /* folded instances: obstacle rows' jx, jy */ \
+    double *FO = p; p += SRB_OBS_STORED(NZL) ? 0 : 9 * (N + 1);   /* per-grid obstacle fold S_k, c_k (+ a zero grid) */ \
+    const ObsFold OF{OJ, FO, rO, N, K, NOP, full_obs_batches<NZM>(N, C, NOP, lane)}; \
     double *H0 = p; p += NZL * LDH;               /* assembled Z'HZ (unshifted; + delta Z'Z on the fly) */ \
     double *ZZ = p; p += NZL * LDH;               /* Z'Z (NLP) */ \
     double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM; \
@@ -939,7 +1064,7 @@ _Pragma("unroll")                                                               
                     __hip_atomic_fetch_add(&CF[q.r], -cfa, __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP);                                   \
                 }                                                                                                                             \
             SYNC();                                                                                                                           \
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);                                                    \
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, H0, vg, nz, tid, part, bmask);                                                    \
             SYNC();                                                                                                                           \
             if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);                                                                           \
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
@@ -950,7 +1075,7 @@ _Pragma("unroll")                                                               
             for (int t = 0; t < TS; t++)                                                                                                      \
                 if (t < nts) {                                                                                                                \
                     Slot &q = PS[t];                                                                                                          \
-                    const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) /* J_o Z dxi, M_o generated (gram_rhs) */                 \
+                    const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) /* J_o Z dxi, folded instances (OJ) */                \
                         ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),                                                          \
                               fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))     \
                         : row_dot<NZL>(R + q.r * LDR, dxi);                                                                                   \
@@ -1113,7 +1238,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     if (q.kind == K_VAR || q.kind == K_COP) { W[q.r] = wgt; CF[q.r] = cfv; }
                 }
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, H0, vg, nz, tid, part, bmask);
             SYNC();
             gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
             if (gj_reduced<NZL>(Mi, nz, lane, 1) != 0) {
@@ -1127,7 +1252,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    const double f = slot_f(q, xs, 0.0) + row_dot<NZL>(R + q.r * LDR, dxi);
+                    const double f = slot_f(q, xs, 0.0) +
+                        ((!SRB_OBS_STORED(NZL) && q.kind == K_OBS) ? 0.0 : row_dot<NZL>(R + q.r * LDR, dxi));   /* (OBS: masked here) */
                     q.jd = f;                                 // f(x) for the shift below
                     const double z0 = q.h[0] - f, z1 = q.h[1] + f;
                     if (q.m[0] != 0.0) { mn = fmin(mn, z0); mx = fmax(mx, z0); }
@@ -1226,7 +1352,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     q.z[1] = SRB_NLP_Z0 * rcp_d(fmax(q.s[1], 1.0));
                     if (q.kind == K_OBS) {                     // M_o = J_o Z at the current x (gram_rhs)
                         const int o = q.r - rO;
-                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
+                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1));
                     }
                     // Z'Z (delta shifts) and rx0 = -Z (Z'Z)^-1 Z'(P x + c + J'z): each row's J'z on its
                     // term row (the velocity rows' below, onto their variables' rows)
@@ -1242,7 +1368,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     __hip_atomic_fetch_add(&CF[Q[t].r], Q[t].m[0] * Q[t].z[0] - Q[t].m[1] * Q[t].z[1], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
             SYNC();
-            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, ZZ, vg, nz, tid, part, bmask);
+            gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, ZZ, vg, nz, tid, part, bmask);
             SYNC();
             gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
             gj_reduced<NZL>(Mi, nz, lane, 0);
@@ -1311,7 +1437,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         for (int r = 0; r < 2; r++) { q.iz[r] = rcp_d(q.z[r]); q.is[r] = rcp_d(q.s[r]); }
                     if (nl && kind_of(q) == K_OBS) {              // re-linearise: M_o = J_o(x) Z (gram_rhs)
                         const int o = q.r - rO;
-                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1), nz);
+                        obs_relin<NZL>(R, OJ, rO, o, q.i0, q.i1, -2.0 * (xs[q.i0] - q.a0), -2.0 * (xs[q.i1] - q.a1));
                         zo[o] = q.z[0];
                     }
                 }
@@ -1431,7 +1557,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 set_rhs(0);
                 SYNC();
                 STAMP_END(17);
-                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OJ, rO, nko, K, H0, vg, nz, tid, part, bmask);
+                gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, H0, vg, nz, tid, part, bmask);
                 SYNC();
                 STAMP_END(4);
                 double dstart = 0.0;
@@ -1459,7 +1585,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     set_rhs(pass);
                     SYNC();
                     STAMP_END(6 + 4 * pass);
-                    rhs_only<NZL, NW>(R, CF, cnt, OJ, rO, nko, K, vg, nz, tid, part, bmask);
+                    rhs_only<NZL, NW>(R, CF, cnt, OF, nko, vg, nz, tid, part, bmask);
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
@@ -1479,9 +1605,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        if (!SRB_OBS_STORED(NZL) && nl && kind_of(q) == K_OBS) {
+                        if (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) {   /* (QP stage: masked rows, 0) */
                             const int o = q.r - rO;
-                            q.jd = fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N]));
+                            q.jd = nl ? fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N])) : 0.0;
                         } else {
                             q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
                         }
