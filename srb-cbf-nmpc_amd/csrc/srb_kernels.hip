@@ -526,13 +526,13 @@ __device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, 
 }
 
 // dot of LDS term row (lane-parallel rows) with a wave-uniform vector held in registers
-template <int NZL>
+template <int NZL, int NZE = NZL>
 __device__ __forceinline__ double row_dot(const double *row, const double (&v)[NZL])
 {
     double s0 = 0.0, s1 = 0.0;
 #pragma unroll
-    for (int j = 0; j + 1 < NZL; j += 2) { s0 = fma(row[j], v[j], s0); s1 = fma(row[j + 1], v[j + 1], s1); }
-    if (NZL & 1) s0 = fma(row[NZL - 1], v[NZL - 1], s0);
+    for (int j = 0; j + 1 < NZE; j += 2) { s0 = fma(row[j], v[j], s0); s1 = fma(row[j + 1], v[j + 1], s1); }
+    if (NZE & 1) s0 = fma(row[NZE - 1], v[NZE - 1], s0);
     return s0 + s1;
 }
 
@@ -542,7 +542,7 @@ template <int NZL>
 __device__ __forceinline__ int mrow(int lane) { return (NZL <= 16 && SRB_USE_DPP) ? (lane & 15) : lane; }
 
 // lane i (< NZL) loads row i of H (+ delta * Z'Z) with identity padding
-template <int NZL>
+template <int NZL, int NZE = NZL>
 __device__ __forceinline__ void gj_load(double (&A)[NZL], const double *H, const double *ZtZ, double delta, int nz, int lane)
 {
     constexpr int LDH = NZL + 1;
@@ -550,6 +550,7 @@ __device__ __forceinline__ void gj_load(double (&A)[NZL], const double *H, const
     const int i = (lane < NZL) ? lane : 0;
 #pragma unroll
     for (int j = 0; j < NZL; j++) {
+        if (j >= NZE) { A[j] = (lane == j) ? 1.0 : 0.0; continue; }
         double v = H[i * LDH + j];
         if (delta != 0.0) v = fma(delta, ZtZ[i * LDH + j], v);
         A[j] = (lane < nz && j < nz) ? v : ((lane == j) ? 1.0 : 0.0);
@@ -565,13 +566,13 @@ __device__ __forceinline__ void gj_load(double (&A)[NZL], const double *H, const
 #define SRB_GJ_SPLIT 0
 #endif
 #if SRB_GJ_SPLIT
-template <int NZL>
+template <int NZL, int NZE = NZL>
 __device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, int regularise)
 {
     if constexpr (NZL <= 16 && NZL % 4 == 0 && SRB_USE_DPP && !SRB_KKT_FP32)
         return gj_invert_split<NZL>(A, lane, regularise);
     else
-        return gj_invert<NZL>(A, nz, lane, regularise);
+        return gj_invert<NZL, NZE>(A, nz, lane, regularise);
 }
 #else
 #define gj_reduced gj_invert
@@ -581,7 +582,7 @@ __device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, in
 // (y = M g; y += M (g - Hs y)): the explicit inverse alone is not backward stable, and near
 // the end of an interior-point solve Hs carries barrier weights of 1e8..1e12.
 // g, y, r, out: LDS vectors (zero beyond nz).  Returns out in registers (uniform).
-template <int NZL, int NW>
+template <int NZL, int NW, int NZE = NZL>
 __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *Hs, const double *Zs, double dl, const double *g,
                                          double *y, double *r, double *out, double (&res)[NZL], int nz, int lane)
 {
@@ -593,7 +594,7 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         const double gi = (i < nz) ? g[i] : 0.0;         // g is zero beyond nz
         double y0 = 0.0;
 #pragma unroll
-        for (int j = 0; j < NZL; j++) y0 = fma(M[j], bc16(gi, j), y0);
+        for (int j = 0; j < NZE; j++) y0 = fma(M[j], bc16(gi, j), y0);
         // SRB_REFINE steps of iterative refinement with fp64 residuals (1 in the product build;
         // the fp32-factor diagnostic build uses more)
         double y1 = y0;
@@ -602,26 +603,26 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
             double rr = gi;
             if (dl != 0.0) {                 // the NLP's inertia shift, applied on the fly (H stays unshifted)
 #pragma unroll
-                for (int j = 0; j < NZL; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), bc16(y1, j), rr);
+                for (int j = 0; j < NZE; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), bc16(y1, j), rr);
             } else {
 #pragma unroll
-                for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], bc16(y1, j), rr);
+                for (int j = 0; j < NZE; j++) rr = fma(-Hs[i * LDH + j], bc16(y1, j), rr);
             }
             if (i >= nz) rr = 0.0;
 #pragma unroll
-            for (int j = 0; j < NZL; j++) y1 = fma(M[j], bc16(rr, j), y1);
+            for (int j = 0; j < NZE; j++) y1 = fma(M[j], bc16(rr, j), y1);
         }
 #pragma unroll
-        for (int j = 0; j < NZL; j++) res[j] = bc16(y1, j);
+        for (int j = 0; j < NZL; j++) res[j] = (j < NZE) ? bc16(y1, j) : 0.0;
         return;
     }
     const int i = (lane < NZL) ? lane : 0;
     double gv[NZL];
 #pragma unroll
-    for (int j = 0; j < NZL; j++) gv[j] = g[j];
+    for (int j = 0; j < NZE; j++) gv[j] = g[j];
     double y0 = 0.0;
 #pragma unroll
-    for (int j = 0; j < NZL; j++) y0 = fma(M[j], gv[j], y0);
+    for (int j = 0; j < NZE; j++) y0 = fma(M[j], gv[j], y0);
     double y1 = y0;
     for (int it = 0; it < SRB_REFINE; it++) {
         if (it > 0) SYNC();                      // every lane has read the previous r
@@ -630,20 +631,20 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         double rr = (lane < nz) ? g[lane] : 0.0;
         if (dl != 0.0) {
 #pragma unroll
-            for (int j = 0; j < NZL; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), y[j], rr);
+            for (int j = 0; j < NZE; j++) rr = fma(-fma(dl, Zs[i * LDH + j], Hs[i * LDH + j]), y[j], rr);
         } else {
 #pragma unroll
-            for (int j = 0; j < NZL; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
+            for (int j = 0; j < NZE; j++) rr = fma(-Hs[i * LDH + j], y[j], rr);
         }
         if (lane < nz) r[lane] = rr;
         SYNC();
 #pragma unroll
-        for (int j = 0; j < NZL; j++) y1 = fma(M[j], r[j], y1);
+        for (int j = 0; j < NZE; j++) y1 = fma(M[j], r[j], y1);
     }
     if (lane < nz) out[lane] = y1;
     SYNC();
 #pragma unroll
-    for (int j = 0; j < NZL; j++) res[j] = out[j];
+    for (int j = 0; j < NZL; j++) res[j] = (j < NZE) ? out[j] : 0.0;
 }
 
 // --------------------------------------------------------------------------- null space
@@ -862,6 +863,7 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     constexpr int NZM = ((NZL + 15) / 16) * 16; \
     constexpr int LDR = NZL + 1, LDH = NZL + 1; \
     constexpr int NTH = 64 * NW; \
+    constexpr int NZE = (NC > 0 && CC > 0) ? NC * (CC - 1) + 1 : NZL;   /* reduced size when the shape is compiled */ \
     const int tid = threadIdx.x, lane = tid & 63, wv = tid >> 6; \
     /* the compiled shape (NC, CC, KC > 0) or the run-time one; n = (6 + C) N + 1, nz = N (C - 1) + 1 */ \
     const int N = NC > 0 ? NC : prm.N, C = CC > 0 ? CC : prm.C, K = KC > 0 ? KC : prm.K_obs + prm.K_nbr; \
@@ -1067,18 +1069,18 @@ _Pragma("unroll")                                                               
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, H0, vg, nz, tid, part, bmask);                                                    \
             SYNC();                                                                                                                           \
             if (pass == 0 && pit == 0) POLDBG_MAT(H0, LDH, vg, nz);                                                                           \
-            gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
-            if (gj_reduced<NZL>(Mi, nz, lane, 0) != 0) { bad = true; break; } /* not PD: reject */                                            \
-            la_solve<NZL, NW>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);                                                                    \
+            gj_load<NZL, NZE>(Mi, H0, ZZ, 0.0, nz, lane);                                                                                          \
+            if (gj_reduced<NZL, NZE>(Mi, nz, lane, 0) != 0) { bad = true; break; } /* not PD: reject */                                            \
+            la_solve<NZL, NW, NZE>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);                                                                    \
             double mdx = 0.0;                                                                                                                 \
 _Pragma("unroll")                                                                                                                             \
             for (int t = 0; t < TS; t++)                                                                                                      \
                 if (t < nts) {                                                                                                                \
                     Slot &q = PS[t];                                                                                                          \
                     const double jd = (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) /* J_o Z dxi, folded instances (OJ) */                \
-                        ? fma(OJ[2 * (q.r - rO)], row_dot<NZL>(R + q.i0 * LDR, dxi),                                                          \
-                              fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL>(R + q.i1 * LDR, dxi), -row_dot<NZL>(R + TL.zr(n - 1) * LDR, dxi)))     \
-                        : row_dot<NZL>(R + q.r * LDR, dxi);                                                                                   \
+                        ? fma(OJ[2 * (q.r - rO)], row_dot<NZL, NZE>(R + q.i0 * LDR, dxi),                                                          \
+                              fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL, NZE>(R + q.i1 * LDR, dxi), -row_dot<NZL, NZE>(R + TL.zr(n - 1) * LDR, dxi)))     \
+                        : row_dot<NZL, NZE>(R + q.r * LDR, dxi);                                                                                   \
                     q.dz[0] = fma(q.ds[0] * prm.polish_rho, q.r3[0] + jd, q.dz[0]);                                                           \
                     q.dz[1] = fma(q.ds[1] * prm.polish_rho, q.r3[1] - jd, q.dz[1]);                                                           \
                     if (kind_of(q) == K_VAR) {                                                                                                \
@@ -1240,12 +1242,12 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             SYNC();
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, H0, vg, nz, tid, part, bmask);
             SYNC();
-            gj_load<NZL>(Mi, H0, ZZ, 0.0, nz, lane);
-            if (gj_reduced<NZL>(Mi, nz, lane, 1) != 0) {
+            gj_load<NZL, NZE>(Mi, H0, ZZ, 0.0, nz, lane);
+            if (gj_reduced<NZL, NZE>(Mi, nz, lane, 1) != 0) {
                 qp_flag = 1;                                  // x stays xbar (last iterate is returned)
                 continue;
             }
-            la_solve<NZL, NW>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
+            la_solve<NZL, NW, NZE>(Mi, H0, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
             // x = xbar + Z xi ; zi = h - G x ; s, z shifted (Auxilary.c:716-746)
             double mn = 1e300, mx = -1e300;
 #pragma unroll
@@ -1253,7 +1255,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 if (t < nts) {
                     Slot &q = Q[t];
                     const double f = slot_f(q, xs, 0.0) +
-                        ((!SRB_OBS_STORED(NZL) && q.kind == K_OBS) ? 0.0 : row_dot<NZL>(R + q.r * LDR, dxi));   /* (OBS: masked here) */
+                        ((!SRB_OBS_STORED(NZL) && q.kind == K_OBS) ? 0.0 : row_dot<NZL, NZE>(R + q.r * LDR, dxi));   /* (OBS: masked here) */
                     q.jd = f;                                 // f(x) for the shift below
                     const double z0 = q.h[0] - f, z1 = q.h[1] + f;
                     if (q.m[0] != 0.0) { mn = fmin(mn, z0); mx = fmax(mx, z0); }
@@ -1370,14 +1372,14 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             SYNC();
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, ZZ, vg, nz, tid, part, bmask);
             SYNC();
-            gj_load<NZL>(Mi, ZZ, ZZ, 0.0, nz, lane);
-            gj_reduced<NZL>(Mi, nz, lane, 0);
-            la_solve<NZL, NW>(Mi, ZZ, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
+            gj_load<NZL, NZE>(Mi, ZZ, ZZ, 0.0, nz, lane);
+            gj_reduced<NZL, NZE>(Mi, nz, lane, 0);
+            la_solve<NZL, NW, NZE>(Mi, ZZ, ZZ, 0.0, vg, vy, vr, vd, dxi, nz, lane);
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts) {
                     Slot &q = Q[t];
-                    q.rx = (q.kind == K_VAR) ? -row_dot<NZL>(R + q.r * LDR, dxi) : 0.0;
+                    q.rx = (q.kind == K_VAR) ? -row_dot<NZL, NZE>(R + q.r * LDR, dxi) : 0.0;
                 }
             SYNC();
             STAMP_END(2);
@@ -1567,8 +1569,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         const double dm = (lane < nz) ? H0[lane * LDH + lane] : 1.0;
                         dstart = 1e-10 * fmax(1.0, wmax(dm));
                     }
-                    gj_load<NZL>(Mi, H0, ZZ, delta, nz, lane);    // H0 + delta Z'Z (the solves shift on the fly too)
-                    const int cf = gj_reduced<NZL>(Mi, nz, lane, !nl);
+                    gj_load<NZL, NZE>(Mi, H0, ZZ, delta, nz, lane);    // H0 + delta Z'Z (the solves shift on the fly too)
+                    const int cf = gj_reduced<NZL, NZE>(Mi, nz, lane, !nl);
                     if (cf == 0) { ok = 1; break; }
                     delta = (delta == 0.0) ? dstart : delta * 10.0;
                 }
@@ -1589,7 +1591,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
-                la_solve<NZL, NW>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
+                la_solve<NZL, NW, NZE>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
@@ -1598,7 +1600,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 // (stored-row instances: every slot dots its own row)
                 if (nl && !SRB_OBS_STORED(NZL)) {
                     if (tid <= 2 * N)
-                        dpos[tid] = row_dot<NZL>(R + (tid < 2 * N ? 4 * (tid >> 1) + 2 * (tid & 1) : TL.zr(n - 1)) * LDR, dxi);
+                        dpos[tid] = row_dot<NZL, NZE>(R + (tid < 2 * N ? 4 * (tid >> 1) + 2 * (tid & 1) : TL.zr(n - 1)) * LDR, dxi);
                     SYNC();
                 }
 #pragma unroll
@@ -1609,7 +1611,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                             const int o = q.r - rO;
                             q.jd = nl ? fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N])) : 0.0;
                         } else {
-                            q.jd = row_dot<NZL>(R + q.r * LDR, dxi);
+                            q.jd = row_dot<NZL, NZE>(R + q.r * LDR, dxi);
                         }
 #pragma unroll
                         for (int r = 0; r < 2; r++) {

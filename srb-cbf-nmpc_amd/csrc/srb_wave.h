@@ -212,30 +212,32 @@ __device__ __forceinline__ int gj_invert_f32(double (&Ad)[NZL], int lane, int re
     return fail;
 }
 
-template <int NZL>
+template <int NZL, int NZE = NZL>
 __device__ __forceinline__ int gj_invert(double (&A)[NZL], int nz, int lane, int regularise)
 {
     if constexpr (NZL <= 16 && SRB_USE_DPP) lane &= 15;
     if constexpr (SRB_KKT_FP32) return gj_invert_f32<NZL>(A, lane, regularise);
-    // All NZL steps run (the identity padding makes steps >= nz exact no-ops), so the whole
+    // All NZE steps run (the identity padding makes steps >= nz exact no-ops), so the whole
     // elimination is one basic block: the scheduler overlaps step k's row updates with the
-    // broadcast of row k+1, whose entries are updated first.
+    // broadcast of row k+1, whose entries are updated first.  NZE: the instance's nz when its shape
+    // is compiled in (columns >= NZE are identity padding, never touched), else NZL.
+    static_assert(NZE <= NZL, "NZE");
     int fail = 0;
     double cs = 1.0;
 #pragma unroll
-    for (int k = 0; k < NZL; k++) {
+    for (int k = 0; k < NZE; k++) {
         double piv = readlane_d(A[k], k);
         if (regularise && piv <= 1e-14 && piv == piv) piv = 1e-7;
         fail |= !(piv > 0.0);
         const double inv = rcp_d(piv);
         double rk[NZL];
 #pragma unroll
-        for (int j = 0; j < NZL; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
+        for (int j = 0; j < NZE; j++) rk[j] = (j == k) ? 0.0 : readlane_d(A[j], k);
         const bool me = lane == k;
         const double f = me ? 0.0 : A[k] * inv;
 #pragma unroll
-        for (int jj = 0; jj < NZL; jj++) {
-            const int j = (k + 1 + jj) % NZL;           // next pivot row's entries first
+        for (int jj = 0; jj < NZE; jj++) {
+            const int j = (k + 1 + jj) % NZE;           // next pivot row's entries first
             if (j != k) A[j] = fma(-f, rk[j], A[j]);
         }
         A[k] = me ? 1.0 : -f;
