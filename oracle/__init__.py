@@ -34,7 +34,7 @@ class OrcParams(ctypes.Structure):
                 ("box", ctypes.c_double), ("eps_obs", ctypes.c_double), ("eps_nbr", ctypes.c_double),
                 ("vsat", ctypes.c_double), ("tol", ctypes.c_double),
                 ("qp_maxit", ctypes.c_int), ("nlp_maxit", ctypes.c_int), ("use_nlp", ctypes.c_int),
-                ("qp_init", ctypes.c_int), ("tol_qp", ctypes.c_double)]
+                ("qp_init", ctypes.c_int), ("tol_qp", ctypes.c_double), ("polish", ctypes.c_int)]
 
 
 def build(force: bool = False) -> None:

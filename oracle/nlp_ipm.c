@@ -149,9 +149,6 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
  * iteration has converged, the equality rows hold to ORC_POLISH_EQTOL and the reduced stationarity Z'(grad f + J_A' z_A) is at round-off
  * level; the solve then ends OPTIMAL.  Otherwise the interior-point result stands.
  */
-#ifndef ORC_POLISH_ON
-#define ORC_POLISH_ON 1           /* the kernel's SRB_POLISH_ON */
-#endif
 #define ORC_POLISH_RHO 1e9
 #define ORC_POLISH_IT 5           /* at most this many Newton steps per active-set pass */
 #define ORC_POLISH_PASSES 4       /* active-set passes (the most negative z_A leaves, violated rows join) */
@@ -560,7 +557,7 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     if (getenv("ORC_POLISH_IT")) g_polish_it = atoi(getenv("ORC_POLISH_IT"));
     if (getenv("ORC_POLISH_PASSES")) g_polish_passes = atoi(getenv("ORC_POLISH_PASSES"));
     if (getenv("ORC_POLISH_OMCAP")) g_polish_omcap = atof(getenv("ORC_POLISH_OMCAP"));
-    const int do_polish = ORC_POLISH_ON ? getenv("ORC_NO_POLISH") == NULL : getenv("ORC_POLISH") != NULL;
+    const int do_polish = pp->polish;   /* orc_params.polish (a parameter, not the environment: ADVICE r04) */
     if (do_polish && !early_done && (flag == 0 || flag == 4 || flag == 2) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
     free(xe); free(ze);
     memcpy(x_out, x, sizeof(double) * n);

@@ -42,6 +42,7 @@ typedef struct orc_params {
     int qp_init;                        /* QP starting point: 1 scaled (the kernel's default), 0 iSWIFT's kkt_initialize */
     double tol_qp;                      /* the QP stage's tolerance when the NLP follows (the kernel's SRB_OPT_QP_WARM_TOL,
                                            default 1e-2; 0: tol) */
+    int polish;                         /* 1: active-set polish of the NLP result (the kernel's SRB_OPT_POLISH, default 1) */
 } orc_params;
 
 void orc_params_default(orc_params *p, int N, int C);

@@ -7,6 +7,10 @@
 #include <float.h>
 #include "oracle.h"
 
+#ifndef ORC_POLISH_DEFAULT
+#define ORC_POLISH_DEFAULT 1           /* the kernel's SRB_POLISH_ON */
+#endif
+
 void orc_params_default(orc_params *p, int N, int C)
 {
     memset(p, 0, sizeof(*p));
@@ -24,6 +28,7 @@ void orc_params_default(orc_params *p, int N, int C)
     p->nlp_maxit = 50;
     p->use_nlp = 1;
     p->qp_init = 1;                      /* scaled QP start (qp_ipm.c); 0 = iSWIFT's kkt_initialize */
+    p->polish = ORC_POLISH_DEFAULT;
     p->tol_qp = 1e-2;                    /* QP stage before the NLP: its point only warm-starts the NLP */
 }
 

@@ -265,9 +265,8 @@ def test_unpolished_loosened_exit_is_acceptable_not_optimal():
     """the NLP stage exits on dual-residual / complementarity tests 10x looser than the
     QP's (SRB_NLP_EXITF) because the polish makes the result exact.  A result that met only those
     loosened tests is provisional: with the polish off (SRB_OPT_POLISH = 0) it must read ACCEPTABLE
-    (4), never OPTIMAL, exactly as the oracle (ORC_NO_POLISH) says; with the polish on every such
+    (4), never OPTIMAL, exactly as the oracle with orc_params.polish = 0 says; with the polish on every such
     solve is promoted to OPTIMAL at the exact KKT point."""
-    import os
     N, C, Ko, Kn, A = 10, 2, 3, 8, 256
     b = workload.make_batch(A, N, C, seed=11)
     p = srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn)
@@ -280,12 +279,8 @@ def test_unpolished_loosened_exit_is_acceptable_not_optimal():
         on = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
     finally:
         s.close()
-    os.environ["ORC_NO_POLISH"] = "1"
-    try:
-        r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), b["x0"], b["ref"], b["foot"],
-                               b["obstacles"], b["nbr_state"], nthreads=8)
-    finally:
-        del os.environ["ORC_NO_POLISH"]
+    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn, polish=0), b["x0"], b["ref"], b["foot"],
+                           b["obstacles"], b["nbr_state"], nthreads=8)
     prov = off["status"][:, 1] == 4
     assert prov.sum() >= A // 10, prov.sum()                    # the loosened exit is the common case
     assert ((off["status"] == r["status"]).all(1)).mean() >= 0.99
