@@ -161,7 +161,8 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     const int NZM = ((NZL + 15) / 16) * 16, LDR = NZL + 1, LDH = NZL + 1;
     const int N = p.N, C = p.C, K = p.K_obs + p.K_nbr, n4 = srb_r4(p.n), NK = N * K;
     const int q = 16 * NW;
-    const int rO = (4 * N + srb_r4(2 * (N - 1)) + srb_r4(p.n - 4 * N) + q - 1) / q * q;   // stored term rows
+    const int rU = (4 * N + 2 * (N - 1) + q - 1) / q * q;                                  // X, CoM-CoP rows
+    const int rO = (rU + srb_r4(p.n - 4 * N) + q - 1) / q * q;                              // stored term rows
     const int NKP = (NK + q - 1) / q * q, TT = rO + NKP;          // + the obstacle rows' W / CF / (jx, jy) entries
     const int red = (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;
     const int part = (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;

@@ -136,7 +136,41 @@ struct ObsFold {
     double *FO;
     int rO, N, K, NOP;                 // obstacle rows' W / CF offset, grids, rows per grid, 3N padded to 16 NW
     uint64_t mask;                     // NZM = 32: grid-term batches that reach column 16 (all three tiles)
+    int rU, C, n;                      // the U, lambda, slack rows (ul_add): first row, contacts, variables
 };
+
+// The U, lambda and slack rows [rU, rU + n - 4N) touch only their own grid's C - 1 columns (the slack row
+// column 0), so their part of the Gram is block diagonal: H[a][b] += sum_r W_r R[r][a] R[r][b] over the
+// 2 + C rows of grid j for a, b in grid j's columns (and W_s at [0][0]), g[a] += sum_r CF_r R[r][a] --
+// added directly instead of as MFMA batches of single-entry rows (configs[2] Gram 14 -> 11 batches,
+// N = 20 14 + 4 -> 8 + 4).  Lanes tid0, tid0 + step, .. of the caller; after its tile stores.
+template <int NZL, bool GRAM, bool RHS>
+__device__ __forceinline__ void ul_add(const double *R, const double *W, const double *CF, const ObsFold &F, double *H,
+                                       double *g, int nz, int tid0, int step)
+{
+    constexpr int LDR = NZL + 1, LDH = NZL + 1;
+    const int c1 = F.C - 1, np = F.N * c1 * c1, rl = F.rU + 2 * F.N, rs = F.rU + F.n - 1 - 4 * F.N;
+    if (GRAM) {
+        for (int e = tid0; e <= np; e += step) {
+            if (e == np) { H[0] += W[rs]; continue; }             // slack row: Z = e_0
+            const int j = e / (c1 * c1), rem = e - j * c1 * c1, a = 1 + j * c1 + rem / c1, b = 1 + j * c1 + rem % c1;
+            double v = 0.0;
+            for (int d = 0; d < 2; d++) { const int r = F.rU + 2 * j + d; v = fma(W[r] * R[r * LDR + a], R[r * LDR + b], v); }
+            for (int i = 0; i < F.C; i++) { const int r = rl + F.C * j + i; v = fma(W[r] * R[r * LDR + a], R[r * LDR + b], v); }
+            H[a * LDH + b] += v;
+        }
+    }
+    if (RHS) {
+        for (int a = tid0; a < nz; a += step) {
+            if (a == 0) { g[0] += CF[rs]; continue; }
+            const int j = (a - 1) / c1;
+            double v = 0.0;
+            for (int d = 0; d < 2; d++) { const int r = F.rU + 2 * j + d; v = fma(CF[r], R[r * LDR + a], v); }
+            for (int i = 0; i < F.C; i++) { const int r = rl + F.C * j + i; v = fma(CF[r], R[r * LDR + a], v); }
+            g[a] += v;
+        }
+    }
+}
 
 // S_k and c_k (GRAM) or c_k alone into FO: one lane per grid, the K rows in index order
 template <bool GRAM>
@@ -364,6 +398,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
                         put(16 + r, 16 + li, acc[2][q], ph > 0);
                     }
                 }
+                if (ph == NW - 1) ul_add<NZL, true, RHS>(R, W, CF, F, H, g, nz, lane, 64);   /* (same wave, after its stores) */
             }
         }
     } else {
@@ -393,6 +428,8 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
             for (int w2 = 0; w2 < NW; w2++) v += pg[w2 * NZM + tid];
             g[tid] = v;
         }
+        __syncthreads();
+        ul_add<NZL, true, RHS>(R, W, CF, F, H, g, nz, tid, 64 * NW);
     }
 }
 
@@ -489,10 +526,12 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
         for (int ph = 0; ph < NW; ph++) {       // wave 0 stores, wave 1 adds (as gram_rhs)
             if (ph > 0) __syncthreads();
-            if (wv == ph)
+            if (wv == ph) {
 #pragma unroll
                 for (int tc = 0; tc < NTC; tc++)
                     if (kq == 0 && 16 * tc + li < nz) g[16 * tc + li] = ph ? g[16 * tc + li] + sv[tc] : sv[tc];
+                if (ph == NW - 1) ul_add<NZL, false, true>(R, nullptr, CF, F, nullptr, g, nz, lane, 64);
+            }
         }
     } else {
 #pragma unroll
@@ -505,6 +544,8 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
             for (int w2 = 0; w2 < NW; w2++) v += part[w2 * NZM + tid];
             g[tid] = v;
         }
+        __syncthreads();
+        ul_add<NZL, false, true>(R, nullptr, CF, F, nullptr, g, nz, tid, 64 * NW);
     }
 }
 
@@ -869,7 +910,8 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     const int N = NC > 0 ? NC : prm.N, C = CC > 0 ? CC : prm.C, K = KC > 0 ? KC : prm.K_obs + prm.K_nbr; \
     const int n = (NC > 0 && CC > 0) ? (6 + CC) * NC + 1 : prm.n, nz = (NC > 0 && CC > 0) ? NC * (CC - 1) + 1 : prm.nz; \
     const int NK = N * K, NE = 2 * (N - 1); \
-    const int n4 = rnd4(n), E4 = rnd4(NE), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N); \
+    const int n4 = rnd4(n), NK4 = rnd4(NK), UL4 = rnd4(n - 4 * N); \
+    const int E4 = (4 * N + NE + 16 * NW - 1) / (16 * NW) * (16 * NW) - 4 * N;   /* CoM-CoP block: rU a multiple of 16 NW */ \
     /* stored term rows: X (4N) | CoM-CoP (E4) | U, lambda, slack (UL4) | zero rows up to rO, a */ \
     /* multiple of 16 NW; then the NKP (NK padded likewise) generated obstacle terms: TT terms */ \
     const int rC = 4 * N, rU = rC + E4, rO = (rU + UL4 + 16 * NW - 1) / (16 * NW) * (16 * NW); \
@@ -887,7 +929,7 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     double *CF = p; p += TT + 1;                  /* rhs coefficients (+ one scratch entry) */ \
     double *OJ = p; p += SRB_OBS_STORED(NZL) ? 0 : 2 * NKP;       /* folded instances: obstacle rows' jx, jy */ \
     double *FO = p; p += SRB_OBS_STORED(NZL) ? 0 : 9 * (N + 1);   /* per-grid obstacle fold S_k, c_k (+ a zero grid) */ \
-    const ObsFold OF{OJ, FO, rO, N, K, NOP, full_obs_batches<NZM>(N, C, NOP, lane)}; \
+    const ObsFold OF{OJ, FO, rO, N, K, NOP, full_obs_batches<NZM>(N, C, NOP, lane), rU, C, n}; \
     double *H0 = p; p += NZL * LDH;               /* assembled Z'HZ (unshifted; + delta Z'Z on the fly) */ \
     double *ZZ = p; p += NZL * LDH;               /* Z'Z (NLP) */ \
     double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM; \
@@ -1212,7 +1254,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         STAMP_STAGE(stage);
         const int nts = ((nl ? S : sV) + NTH - 1) / NTH;      // active slot trips
         const int mrows = nl ? (4 * (N - 1) + 12 * N + 2 * C * N + NK + 4 * N) : (4 * (N - 1) + 12 * N + 2 * C * N);
-        const int cnt = rO, nko = nl ? NKP : 0;            // stored term rows, generated obstacle terms
+        const int cnt = rU, nko = nl ? NKP : 0;            // MFMA term rows (X, CoM-CoP), obstacle terms
         STAMP_BEGIN();
         // stage activity of each row
         // (written out here rather than through slot_stage: the call form measurably changes the
@@ -1737,7 +1779,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     if constexpr (SRB_FUSED_POLISH_OK(NZL))
     if (prm.polish_fused && prm.use_nlp && nlp_flag != 1 && nlp_flag != 3) {
         const int nts = (S + NTH - 1) / NTH;
-        const int cnt = rO, nko = NKP;
+        const int cnt = rU, nko = NKP;
         for (int v = tid; v < n; v += NTH) xsv[v] = xs[v];
 #pragma unroll
         for (int t = 0; t < TS; t++) {
@@ -1826,7 +1868,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
     // stays definite along directions no active row pins, lambda with four contacts).
     {
         const int nts = (S + NTH - 1) / NTH;
-        const int cnt = rO, nko = NKP;
+        const int cnt = rU, nko = NKP;
         Slot P[TS];
 #pragma unroll
         for (int t = 0; t < TS; t++) {
