@@ -48,7 +48,14 @@
 
 // one wave per SIMD is the design point (four agents per CU by LDS): the scheduler may spend every
 // register on latency hiding instead of trimming live ranges for an occupancy the LDS rules out
-#ifndef SRB12_WPE
+// (Overriding it is for diagnostic builds only, make s12var, which define SRB_DIAG_BUILD: the round-4
+// build without it returned wrong OPTIMAL answers -- the compiler hazard of DESIGN.md 11, which
+// tests/test_isa_hazard.py now scans every shipped kernel for.)
+#ifdef SRB12_WPE
+#ifndef SRB_DIAG_BUILD
+#error "SRB12_WPE overrides the product SRB-12 instances' attribute: diagnostic builds only (make s12var)"
+#endif
+#else
 #define SRB12_WPE __attribute__((amdgpu_waves_per_eu(1, 1)))
 #endif
 
@@ -56,6 +63,13 @@
 // barrier needs no hardware wait -- a wavefront-scope fence (no s_waitcnt) and a wave barrier keep the
 // compiler from moving memory accesses across it.  (__syncthreads would add an lgkmcnt(0) wait for the
 // stores before every barrier.)
+// What this relies on: (1) LLVM IR -- a fence, whatever its scope, orders the thread's memory
+// operations: no load or store is moved across it (an acq_rel fence is a read-write of all memory for
+// alias analysis), so the ISA keeps the source order of the LDS accesses around SYNC; the wave barrier
+// is IntrNoMem (a convergence point only) and is not what orders them.  (2) The AMDGPU memory model
+// (LLVM AMDGPUUsage, memory model for GFX942 / GFX950): the LDS operations of one wavefront are performed
+// in issue order, so a ds_read by any lane observes an earlier ds_write of the same wave without an
+// s_waitcnt; the compiler still waits (lgkmcnt) before a loaded value is used.
 #define SYNC() do { __builtin_amdgcn_fence(__ATOMIC_ACQ_REL, "wavefront"); __builtin_amdgcn_wave_barrier(); } while (0)
 #include "srb_wave.h"
 
@@ -430,6 +444,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
                 rs = fma(0.5 * rs, fma(-piv * rs, rs, 1.0), rs);
                 dinv[kk] = rs;
             }
+            // (Two pivots a step -- every broadcast of the step reading values from before it, the same fma
+            // forms, bit-identical -- measured slower: SRB-12 step 0.756 -> 0.793 ms, round 5.)
             S12ST(12);  // factor: elimination
             // Y = D^-1/2 L^-1 Hux (lanes 12..24), Z = D^-1/2 L^-1 (lanes 25..36), back to T column-major
             {

@@ -169,7 +169,7 @@ static inline int srb_lds_doubles(const SrbKParams &p, int NZL, int NW)
     return (SRB_OBS_STORED(NZL) ? TT : rO) * LDR + 2 * (TT + 1) + (SRB_OBS_STORED(NZL) ? 0 : 2 * NKP + 9 * (N + 1)) +
            2 * NZL * LDH + 4 * NZM + 4 * n4 + 4 * N + 2 * C * N +
            (SRB_OBS_IN_ZZ(NZL, NK) ? 0 : 2 * NK + 2) +
-           (K + 1) + srb_r4(NK) + (2 * N + 1) + (K + 1) + red + part + (SRB_FUSED_POLISH_OK(NZL) ? srb_r4(srb_slots(N, C, K)) : 0)
+           (K + 1) + srb_r4(NK) + (K + 1) + red + part + (SRB_FUSED_POLISH_OK(NZL) ? srb_r4(srb_slots(N, C, K)) : 0)
 #ifdef SRB_STAMPS
            + 64
 #endif

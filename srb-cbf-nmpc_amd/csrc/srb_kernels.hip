@@ -47,6 +47,13 @@
 // accesses of one wavefront execute in issue order, so a wavefront-scope fence (no s_waitcnt) and a wave
 // barrier suffice -- __syncthreads would wait for every outstanding LDS store first.  (Every SYNC site
 // sits in a function templated on NW.)
+// What this relies on: (1) LLVM IR -- a fence, whatever its scope, orders the thread's memory
+// operations: no load or store is moved across it (an acq_rel fence is a read-write of all memory for
+// alias analysis), so the ISA keeps the source order of the LDS accesses around SYNC; the wave barrier
+// is IntrNoMem (a convergence point only) and is not what orders them.  (2) The AMDGPU memory model
+// (LLVM AMDGPUUsage, memory model for GFX942 / GFX950): the LDS operations of one wavefront are performed
+// in issue order, so a ds_read by any lane observes an earlier ds_write of the same wave without an
+// s_waitcnt; the compiler still waits (lgkmcnt) before a loaded value is used.
 template <int NW>
 __device__ __forceinline__ void srb_sync()
 {
@@ -934,7 +941,8 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     double *ZZ = p; p += NZL * LDH;               /* Z'Z (NLP) */ \
     double *vg = p; p += NZM; double *vy = p; p += NZM; double *vr = p; p += NZM; double *vd = p; p += NZM; \
     double *xs = p; p += n4; \
-    double *xb = p; p += n4; \
+    double *xb = p; p += n4;                      /* xbar (setup); then dx = Z dxi of the Newton steps (dxv) */ \
+    double *dxv = xb; \
     double *xsv = p; p += n4;                     /* NLP: saved iterate (round-off floor / polish) */ \
     double *xprev = p; p += n4;                   /* the iterate before the last update (non-finite fallback) */ \
     double *ref = p; p += 4 * N; \
@@ -942,7 +950,6 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     double *obs = SRB_OBS_IN_ZZ(NZL, NK) ? ZZ : p; p += SRB_OBS_IN_ZZ(NZL, NK) ? 0 : 2 * NK + 2;   /* obstacle positions (setup) */ \
     double *eps = p; p += K + 1; \
     double *zo = p; p += NK4;                     /* obstacle duals (per-grid sums) */ \
-    double *dpos = p; p += 2 * N + 1;             /* Z_x dxi, Z_y dxi per grid, dxi_s (obstacle J dx) */ \
     int *sel = (int *)p; p += (K + 1); \
     double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
     double *part = p; p += (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs (NW = 4) */ \
@@ -1637,23 +1644,27 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
-                // obstacle rows: J_o Z dxi = jx (Z_x dxi) + jy (Z_y dxi) - dxi_s, the CoM-position steps
-                // of every grid formed once (dpos) instead of one generated row per obstacle
-                // (stored-row instances: every slot dots its own row)
-                if (nl && !SRB_OBS_STORED(NZL)) {
-                    if (tid <= 2 * N)
-                        dpos[tid] = row_dot<NZL, NZE>(R + (tid < 2 * N ? 4 * (tid >> 1) + 2 * (tid & 1) : TL.zr(n - 1)) * LDR, dxi);
+                // folded instances (N = 20): dx = Z dxi of every variable once (dxv; ceil(n / NTH) row dots a
+                // lane instead of one per slot), then each slot's J dx from it: VAR / VEL dx_v, CoM-CoP
+                // dx_p - dx_u, obstacle rows jx dx_px + jy dx_py - dx_s (config 5 1.81 -> 1.80 ms).  The
+                // stored-row instances dot each slot's own row inside the slot loop (the separate pass measured
+                // slower there: configs[2] 0.327 -> 0.340 ms)
+                if constexpr (!SRB_OBS_STORED(NZL)) {
+                    for (int v = tid; v < n; v += NTH) dxv[v] = row_dot<NZL, NZE>(R + TL.zr(v) * LDR, dxi);
                     SYNC();
                 }
 #pragma unroll
                 for (int t = 0; t < TS; t++)
                     if (t < nts) {
                         Slot &q = Q[t];
-                        if (!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS) {   /* (QP stage: masked rows, 0) */
-                            const int o = q.r - rO;
-                            q.jd = nl ? fma(OJ[2 * o], dpos[q.i0 >> 1], fma(OJ[2 * o + 1], dpos[q.i1 >> 1], -dpos[2 * N])) : 0.0;
-                        } else {
+                        const int kd = kind_of(q);
+                        if constexpr (SRB_OBS_STORED(NZL)) {
                             q.jd = row_dot<NZL, NZE>(R + q.r * LDR, dxi);
+                        } else if (kd == K_OBS) {                     /* (QP stage: masked rows, 0) */
+                            const int o = q.r - rO;
+                            q.jd = nl ? fma(OJ[2 * o], dxv[q.i0], fma(OJ[2 * o + 1], dxv[q.i1], -dxv[n - 1])) : 0.0;
+                        } else {
+                            q.jd = (kd == K_COP) ? dxv[q.i0] - dxv[q.i1] : dxv[q.i0];
                         }
 #pragma unroll
                         for (int r = 0; r < 2; r++) {
@@ -1830,7 +1841,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
 {
     SRB_AGENT_LAYOUT;
     double *Rt = R + rC * LDR;
-    (void)xb; (void)th; (void)tol; (void)wv;
+    (void)xb; (void)dxv; (void)th; (void)tol; (void)wv;
     const int st1 = status_out[2 * agent + 1];
     if (!prm.use_nlp || st1 == 1 || st1 == 3) return;          // the whole workgroup: no usable iterate to polish
     // the solve's outputs first (x into xsv, which the setup does not clear; the exported active set
