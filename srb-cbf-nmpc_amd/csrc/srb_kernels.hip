@@ -1451,15 +1451,22 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         // others -min(z/s, OMCAP), their barrier weight, as a proximal term
         // -- go to HBM, zpol_g[agent][2 slot + row], with the iterate the result is taken from
         // (the saved one on a restore)
+        // (LDS or global by a uniform branch, not a pointer select: a generic pointer would make these flat stores)
         auto export_zpol = [&]() {
-            float *zp = (SRB_FUSED_POLISH_OK(NZL) && prm.polish_fused) ? zpl : zpol_g + (size_t)agent * zstride;
+            const bool to_lds = SRB_FUSED_POLISH_OK(NZL) && prm.polish_fused;
+            // address-space-typed pointers: the two stores cannot be merged into one through a select
+            __attribute__((address_space(1))) float *zg = (__attribute__((address_space(1))) float *)(zpol_g + (size_t)agent * zstride);
+            __attribute__((address_space(3))) float *zl = (__attribute__((address_space(3))) float *)zpl;
 #pragma unroll
             for (int t = 0; t < TS; t++)
                 if (t < nts && tid + NTH * t < S)
 #pragma unroll
-                    for (int r = 0; r < 2; r++)
-                        zp[2 * (tid + NTH * t) + r] = Q[t].m[r] == 0.0 ? 0.0f
+                    for (int r = 0; r < 2; r++) {
+                        const float v = Q[t].m[r] == 0.0 ? 0.0f
                             : (float)(Q[t].s[r] * SRB_POLISH_KAPPA < Q[t].z[r] ? Q[t].z[r] : -fmin(Q[t].z[r] / Q[t].s[r], SRB_POLISH_OMCAP));
+                        if (to_lds) zl[2 * (tid + NTH * t) + r] = v;
+                        else zg[2 * (tid + NTH * t) + r] = v;
+                    }
         };
         for (int v = tid; v < n; v += NTH) xprev[v] = xs[v];
         for (int iter = 0; iter < maxit; iter++) {
@@ -1975,6 +1982,20 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
     if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
     const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
     int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);
+    if (SRB_KNN_WAVES == 2 && K_obs > 0 && K_nbr > 0) {
+        // the two tables on the two waves at once, each selection wave-local (DPP argmins, no barrier):
+        // configs[2] selection 23.5 -> 20.9 us a step (HIP events, round 5); the same rows.  (Selecting
+        // inside the solve kernel's setup instead measured no faster at configs[2] -- the solve kernel
+        // grew by what the launch saved -- and 4.6 % slower at N = 20, where four rounds of agents each
+        // wait for their selection; round 5)
+        const int lane = tid & 63;
+        if (tid < 64)
+            knn_select<1>(lane, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds, gob, oob, pob, iob);
+        else
+            knn_select<1>(lane, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, 0, sel + K_obs, wd_lds, wi_lds,
+                          gnb, onb, pnb, inb);
+        return;
+    }
     if (K_obs > 0)
         knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds, gob, oob, pob, iob);
     if (K_nbr > 0)
