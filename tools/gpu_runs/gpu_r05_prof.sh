@@ -30,7 +30,7 @@ python tools/pmc_traffic.py calib $O/cal_FETCH_SIZE $O/cal_WRITE_SIZE $O/r05_pmc
 C=$O/r05_pmc_calib.json
 pmc c3 --config 3 && python tools/pmc_traffic.py $O/pmc_c3_FETCH_SIZE $O/pmc_c3_WRITE_SIZE 3 1024 $O/r05_pmc_traffic_c3.json $C 1 || exit 1
 pmc c2 --config 2 && python tools/pmc_traffic.py $O/pmc_c2_FETCH_SIZE $O/pmc_c2_WRITE_SIZE 2 64 $O/r05_pmc_traffic_c2.json $C 1 || exit 1
-pmc c5 --config 5 && python tools/pmc_traffic.py $O/pmc_c5_FETCH_SIZE $O/pmc_c5_WRITE_SIZE 5 2048 $O/r05_pmc_traffic_c5.json $C 0 || exit 1
+pmc c5 --config 5 && python tools/pmc_traffic.py $O/pmc_c5_FETCH_SIZE $O/pmc_c5_WRITE_SIZE 5 2048 $O/r05_pmc_traffic_c5.json $C 1 || exit 1
 pmc s12 --path srb12 && python tools/pmc_traffic.py $O/pmc_s12_FETCH_SIZE $O/pmc_s12_WRITE_SIZE s12 1024 $O/r05_pmc_traffic_s12.json $C 0 || exit 1
 stats c3 --config 3 && stats c2 --config 2 && stats c5 --config 5 && stats s12 --path srb12 || exit 1
 cp $O/r05_pmc_traffic_*.json profiles/ 2>/dev/null
@@ -38,7 +38,7 @@ timeout -k 10 300 python bench.py > $O/r05_bench_c3.json 2> $O/bench_c3.err || {
 timeout -k 10 200 python bench.py --config 5 --no-cpu-baseline > $O/r05_bench_c5.json 2> $O/bench_c5.err || { tail $O/bench_c5.err; exit 1; }
 timeout -k 10 200 python bench.py --config 2 --no-cpu-baseline > $O/r05_bench_c2.json 2> $O/bench_c2.err || { tail $O/bench_c2.err; exit 1; }
 timeout -k 10 200 python bench.py --path srb12 > $O/r05_bench_srb12.json 2> $O/bench_s12.err || { tail $O/bench_s12.err; exit 1; }
-timeout -k 10 120 python tools/stamps.py 10 2 3 8 1024 > $O/r05_c3_stamps.txt 2>&1 || exit 1
+timeout -k 10 120 python tools/stamps.py 10 2 3 8 1024 > $O/r05_c3_stamps.txt 2>&1 && timeout -k 10 150 python tools/stamps.py 20 2 3 8 2048 > $O/r05_c5_stamps.txt 2>&1 || exit 1
 timeout -k 10 120 python tools/srb12_stamps.py 0 24 31 > $O/r05_s12_stamps.txt 2>&1 || exit 1
 cat $O/r05_bench_c3.json $O/r05_bench_c5.json $O/r05_bench_c2.json $O/r05_bench_srb12.json
 find $O -name "*kernel_stats.csv" | sort
