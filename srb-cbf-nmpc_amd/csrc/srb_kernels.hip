@@ -185,13 +185,26 @@ __device__ __forceinline__ void obs_fold(const double *W, const double *CF, cons
 {
     for (int k = tid; k < F.N; k += NTH) {
         double s00 = 0.0, s01 = 0.0, s02 = 0.0, s11 = 0.0, s12 = 0.0, s22 = 0.0, c0 = 0.0, c1 = 0.0, c2 = 0.0;
-        for (int j = 0; j < F.K; j++) {
-            const int o = k * F.K + j;
-            const double cf = CF[F.rO + o], jx = F.OJ[2 * o], jy = F.OJ[2 * o + 1];
-            c0 = fma(cf, jx, c0); c1 = fma(cf, jy, c1); c2 -= cf;
-            if (GRAM) {
-                const double w = W[F.rO + o], wx = w * jx, wy = w * jy;
-                s00 = fma(wx, jx, s00); s01 = fma(wx, jy, s01); s02 -= wx; s11 = fma(wy, jy, s11); s12 -= wy; s22 += w;
+        // the grid's rows in chunks of 8, every load of a chunk issued before the first use (predicated, as
+        // zo_sum): one LDS round trip a chunk instead of one a row; the sums keep the row order
+        for (int j0 = 0; j0 < F.K; j0 += 8) {
+            double cfv[8], jxv[8], jyv[8], wv[8];
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                const bool in = j0 + u < F.K;
+                const int o = k * F.K + (in ? j0 + u : 0);
+                cfv[u] = in ? CF[F.rO + o] : 0.0; jxv[u] = in ? F.OJ[2 * o] : 0.0; jyv[u] = in ? F.OJ[2 * o + 1] : 0.0;
+                wv[u] = (GRAM && in) ? W[F.rO + o] : 0.0;
+            }
+#pragma unroll
+            for (int u = 0; u < 8; u++) {
+                if (j0 + u >= F.K) break;
+                const double cf = cfv[u], jx = jxv[u], jy = jyv[u];
+                c0 = fma(cf, jx, c0); c1 = fma(cf, jy, c1); c2 -= cf;
+                if (GRAM) {
+                    const double w = wv[u], wx = w * jx, wy = w * jy;
+                    s00 = fma(wx, jx, s00); s01 = fma(wx, jy, s01); s02 -= wx; s11 = fma(wy, jy, s11); s12 -= wy; s22 += w;
+                }
             }
         }
         double *f = F.FO + 9 * k;
