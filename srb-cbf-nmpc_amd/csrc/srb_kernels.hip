@@ -371,16 +371,19 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
         }
     };
     {
-        const int chunk = cnt / NW, tb = wv * chunk;
+        // NZM = 32 with several waves: the batches dealt round-robin over the waves (the full-width ones
+        // cluster at high grids, so contiguous halves left one wave with most of them); else contiguous
+        constexpr bool ILV = NZM == 32 && NW > 1;
+        const int chunk = cnt / NW, tb = ILV ? 16 * wv : wv * chunk, te = ILV ? cnt : tb + chunk, ts = ILV ? 16 * NW : 16;
 #pragma clang loop unroll(disable)
-        for (int t0 = tb; t0 < tb + chunk; t0 += 16) {
+        for (int t0 = tb; t0 < te; t0 += ts) {
             if (NZM == 16 || batch_full(bmask, t0)) body(t0, std::integral_constant<bool, true>{});
             else body(t0, std::integral_constant<bool, false>{});
         }
         if (FOLD && nko > 0) {
-            const int och = F.NOP / NW, ob = wv * och;
+            const int och = F.NOP / NW, ob = ILV ? 16 * wv : wv * och, oe = ILV ? F.NOP : ob + och;
 #pragma clang loop unroll(disable)
-            for (int t0 = ob; t0 < ob + och; t0 += 16) {
+            for (int t0 = ob; t0 < oe; t0 += ts) {
                 if (NZM == 16 || batch_full(F.mask, t0)) obody(t0, std::integral_constant<bool, true>{});
                 else obody(t0, std::integral_constant<bool, false>{});
             }
@@ -487,6 +490,22 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
 #pragma unroll
             for (int tc = 0; tc < NB; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
     };
+    auto schunk16 = [&](int t0, auto fullc) {          // stored rows t0 .. t0 + 15
+        constexpr int NB = decltype(fullc)::value ? NTC : 1;
+        double a[4][NTC], c[4];
+#pragma unroll
+        for (int u = 0; u < 4; u++) {
+            const int r = t0 + 4 * u + kq;
+            c[u] = CF[r];
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) a[u][tc] = term_elem<NZL>(R, r, 16 * tc + li);
+        }
+        __builtin_amdgcn_sched_barrier(0);
+#pragma unroll
+        for (int u = 0; u < 4; u++)
+#pragma unroll
+            for (int tc = 0; tc < NB; tc++) ps[u & 1][tc] = fma(c[u], a[u][tc], ps[u & 1][tc]);
+    };
     auto ochunk16 = [&](int t0, auto fullc) {
         constexpr int NB = decltype(fullc)::value ? NTC : 1;
         double a[4][NTC], c[4];
@@ -524,16 +543,25 @@ __device__ __forceinline__ void rhs_only(const double *R, const double *CF, int 
         }
     };
     {
+        constexpr bool ILV = NZM == 32 && NW > 1;       // batches round-robin over the waves, as gram_rhs
         const int chunk = cnt / NW, tb = wv * chunk;
-        range(tb, tb + chunk, false);
+        if constexpr (ILV) {
+#pragma clang loop unroll(disable)
+            for (int t0 = 16 * wv; t0 < cnt; t0 += 16 * NW) {
+                if (batch_full(bmask, t0)) schunk16(t0, std::integral_constant<bool, true>{});
+                else schunk16(t0, std::integral_constant<bool, false>{});
+            }
+        } else {
+            range(tb, tb + chunk, false);
+        }
         if (!FOLD && nko > 0) {
             const int och = nko / NW, ob = F.rO + wv * och;
             range(ob, ob + och, true);
         }
         if (FOLD && nko > 0) {
-            const int och = F.NOP / NW, ob = wv * och;
+            const int och = F.NOP / NW, ob = ILV ? 16 * wv : wv * och, oe = ILV ? F.NOP : ob + och, os = ILV ? 16 * NW : 16;
 #pragma clang loop unroll(disable)
-            for (int o0 = ob; o0 < ob + och; o0 += 16) {
+            for (int o0 = ob; o0 < oe; o0 += os) {
                 if (NZM == 16 || batch_full(F.mask, o0)) ochunk16(o0, std::integral_constant<bool, true>{});
                 else ochunk16(o0, std::integral_constant<bool, false>{});
             }
