@@ -485,6 +485,8 @@ def main():
     ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
     ap.add_argument("--qp-init", type=int, default=1,
                     help="QP-stage start: 1 scaled (default), 0 iSWIFT's kkt_initialize (srb_ctx_set_qp_init)")
+    ap.add_argument("--qp-warm-tol", type=float, default=None,
+                    help="diagnostics: the QP stage's tolerance before the NLP (SRB_OPT_QP_WARM_TOL; default: the library's)")
     ap.add_argument("--polish-fused", type=int, default=1,
                     help="1 (default): the active-set polish runs at the end of the solve kernel where the instance "
                          "allows (NZL <= 16), 0: as srb_polish_kernel (SRB_OPT_POLISH_FUSED)")
@@ -550,6 +552,8 @@ def main():
     solver.set_waves(args.waves)
     solver.set_qp_init(args.qp_init)
     solver.set_option("polish_fused", args.polish_fused)
+    if args.qp_warm_tol is not None:
+        solver.set_option("qp_warm_tol", args.qp_warm_tol)
     # one explicit stream for the collective, both kernels and the timing events (the C ABI
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)

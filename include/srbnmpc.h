@@ -149,10 +149,11 @@ int srb_ctx_waves(srb_ctx *ctx);
  *   SRB_OPT_TIMING               1 (default): HIP events around the launch's kernels (srb_last_kernel_ms,
  *                                srb_last_polish_ms); 0: none (each event record is a marker the queue
  *                                drains to: a few us per call, measured in bench.py's timed loop)
- *   SRB_OPT_QP_WARM_TOL          the QP stage's tolerance when the NLP stage follows (default 1e-2; 0: the
+ *   SRB_OPT_QP_WARM_TOL          the QP stage's tolerance when the NLP stage follows (default 0.3; 0: the
  *                                full tolerance, 1e-6 as iSWIFT): that point only warm-starts the NLP, whose
- *                                result is unchanged (within 4e-11 on the bench batches) while the QP stage
- *                                takes 3.8 instead of 5.8 iterations; x_qp is then that rougher point.  The
+ *                                result is unchanged (the polish makes it exact; statuses and NLP iterations
+ *                                unchanged on the bench batches) while the QP stage takes 3.0 instead of 5.8
+ *                                iterations at configs[2]; x_qp is then that rougher point.  The
  *                                QP-only solve (srb_solve_qp, use_nlp = 0) always runs to the full tolerance */
 #define SRB_OPT_POLISH 1
 #define SRB_OPT_POLISH_RHO 2

@@ -41,7 +41,7 @@ typedef struct orc_params {
     int use_nlp;                        /* MPC_dist::use_snopt                                */
     int qp_init;                        /* QP starting point: 1 scaled (the kernel's default), 0 iSWIFT's kkt_initialize */
     double tol_qp;                      /* the QP stage's tolerance when the NLP follows (the kernel's SRB_OPT_QP_WARM_TOL,
-                                           default 1e-2; 0: tol) */
+                                           default 0.3; 0: tol) */
     int polish;                         /* 1: active-set polish of the NLP result (the kernel's SRB_OPT_POLISH, default 1) */
 } orc_params;
 

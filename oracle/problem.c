@@ -29,7 +29,7 @@ void orc_params_default(orc_params *p, int N, int C)
     p->use_nlp = 1;
     p->qp_init = 1;                      /* scaled QP start (qp_ipm.c); 0 = iSWIFT's kkt_initialize */
     p->polish = ORC_POLISH_DEFAULT;
-    p->tol_qp = 1e-2;                    /* QP stage before the NLP: its point only warm-starts the NLP */
+    p->tol_qp = 3e-1;                    /* QP stage before the NLP: its point only warm-starts the NLP */
 }
 
 int orc_nv(const orc_params *p) { return (6 + p->C) * p->N + 1; }

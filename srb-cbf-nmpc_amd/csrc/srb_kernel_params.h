@@ -29,10 +29,12 @@
 // near-optimal iterates without meeting both, the solve is at its round-off floor: ACCEPTABLE
 #define SRB_NLP_DXTOL 1e300     // round 3: off (the polish makes the result exact; oracle ORC_NLP_DXTOL)
 // QP stage followed by the NLP stage: its point only warm-starts the NLP (the duals restart), so it runs to
-// this tolerance (srb_ctx_set_option SRB_OPT_QP_WARM_TOL; 0: the reference's 1e-6).  Oracle at configs[2]:
-// QP iterations 5.8 -> 3.8 on average, 9 -> 5 at most, NLP iterations and statuses unchanged, the result
-// within 4e-11 (also N = 20, the free-velocity batch, C = 4)
-#define SRB_QP_WARM_TOL 1e-2
+// this tolerance (srb_ctx_set_option SRB_OPT_QP_WARM_TOL; 0: the reference's 1e-6).  Round 5: 1e-2 (QP
+// iterations 5.8 -> 3.8 on average at configs[2], NLP iterations and statuses unchanged, the result within
+// 4e-11), then 0.3 from a scan on the GPU (1e-2 / 3e-2 / 0.1 / 0.3 / 1 / 3: configs[2] 0.317 -> 0.309 ms,
+// config 5 1.74 -> 1.68 ms; QP iterations 3.8 -> 3.0 and 4.4 -> 3.7, NLP iterations and every status
+// unchanged; profiles/r05_qp_warm_tol_scan.txt)
+#define SRB_QP_WARM_TOL 3e-1
 // NLP stage: dual-residual and complementarity tests this much looser than the QP's (the polish
 // after the solve lands on the exact KKT point of the active set the interior point identified;
 // 15 % fewer NLP iterations on the bench batches, polished results unchanged within 4e-7)
