@@ -337,6 +337,8 @@ def main_srb12(args, world, rank, local_rank, dev):
     nbr_all = T(b["nbr_state"])
     nbr_local = nbr_all[lo:hi].contiguous()
     prm = srb12.default_params(N, K_obs=Ko_, K_nbr=Kn_)
+    if args.qp_warm_tol is not None:                     # diagnostics: the QP stage's tolerance before the NLP
+        prm.tol_qp = args.qp_warm_tol
     solver = srb12.Solver12(prm, n_loc, local_rank)
     Ko, Kn = srb12.n_selected(prm, obst.shape[0], A_total)
     out = dict(x_qp=None, x=torch.zeros((n_loc, prm.nv), dtype=torch.float64, device=dev),
