@@ -914,12 +914,21 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     // (x0 and the LDS iterate are read through their own address spaces -- no generic pointer selecting
     // between them: a flat access in this kernel changed its code generation enough to break the polish
     // of the run-time instance)
-    const double g0x = x0[0], g1x = x0[1], g2x = x0[2], g3x = x0[3];
     double r = 0.0;
+#if defined(SRB_DIAG_FLAT_EQRES)         // diagnostic builds only: round 5's first form (one generic pointer)
+#ifndef SRB_DIAG_BUILD
+#error "SRB_DIAG_FLAT_EQRES is a diagnostic-build option"
+#endif
+    for (int k = tid; k < N; k += NTH) {
+        const double *xp = k ? xs + 4 * (k - 1) : x0;
+        const double p0 = xp[0], p1 = xp[1], p2 = xp[2], p3 = xp[3];
+#else
+    const double g0x = x0[0], g1x = x0[1], g2x = x0[2], g3x = x0[3];
     for (int k = tid; k < N; k += NTH) {
         const int kp = k ? k - 1 : 0;
         const double p0 = k ? xs[4 * kp] : g0x, p1 = k ? xs[4 * kp + 1] : g1x;
         const double p2 = k ? xs[4 * kp + 2] : g2x, p3 = k ? xs[4 * kp + 3] : g3x;
+#endif
         const double u0 = xs[4 * N + 2 * k], u1 = xs[4 * N + 2 * k + 1];
 #pragma unroll
         for (int d = 0; d < 4; d++) {
@@ -1103,6 +1112,19 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     } \
     do {} while (0)
 
+// Diagnostic builds only (-DSRB_DIAG_POLISH_OUT, make lipvar): the fused polish's last acceptance test --
+// its equality residual into obj, the tests it met as bits into the QP iteration count (1 primal, 2 active
+// rows, 4 multipliers, 8 last step, 16 equality rows, 32 equality residual not finite, 64 a pass ran)
+#ifdef SRB_DIAG_POLISH_OUT
+#ifndef SRB_DIAG_BUILD
+#error "SRB_DIAG_POLISH_OUT is a diagnostic-build option"
+#endif
+#define SRB_POLISH_DIAG() do { dg_eqr = eqr; dg_bits = 64 | (pv <= SRB_POLISH_PTOL) | ((cv <= SRB_POLISH_PTOL) << 1) | \
+    ((nzmin <= 1e-9 * zm) << 2) | ((lastdx <= SRB_POLISH_DXTOL) << 3) | ((eqr <= SRB_POLISH_EQTOL) << 4) | ((!isfinite(eqr)) << 5); } while (0)
+#else
+#define SRB_POLISH_DIAG() do {} while (0)
+#endif
+
 // The passes of the active-set polish (polish_agent, and the fused polish at the end of nmpc_agent):
 // PS[t] holds each slot's active mask (ds), multiplier z_A (dz) and the inactive rows' proximal weight
 // (s); xs the interior-point result, also saved in xsv.  Sets `accepted`.
@@ -1213,6 +1235,7 @@ _Pragma("unroll")                                                               
         }                                                                                                                                     \
         POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);                           \
         POLDBG(pass, 5, lastdx); POLDBG(pass, 7, eqr);                                                                                        \
+        SRB_POLISH_DIAG();                                                                                                                    \
         if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&                             \
             eqr <= SRB_POLISH_EQTOL) {                                                                                                        \
             POLDBG(pass, 6, 1.0);                                                                                                             \
@@ -1291,6 +1314,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     STAMP_END(0);
 
     int qp_flag = 3, qp_it = 0, nlp_flag = 0, nlp_it = 0;
+#ifdef SRB_DIAG_POLISH_OUT
+    double dg_eqr = -1.0;
+    int dg_bits = 0;
+#endif
     const int nstage = prm.use_nlp ? 2 : 1;
     // One loop over the two stages so that the interior-point iteration exists once in the
     // code object (keeps the hot loop small for the instruction cache).
@@ -1868,6 +1895,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         obj_out[agent] = f;
         status_out[2 * agent] = qp_flag; status_out[2 * agent + 1] = nlp_flag;
         iters_out[2 * agent] = qp_it; iters_out[2 * agent + 1] = nlp_it;
+#ifdef SRB_DIAG_POLISH_OUT
+        obj_out[agent] = dg_eqr; iters_out[2 * agent] = dg_bits;
+#endif
     }
 }
 
@@ -1945,6 +1975,10 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             }
         }
         bool accepted = false;
+#ifdef SRB_DIAG_POLISH_OUT
+        double dg_eqr = -1.0;
+        int dg_bits = 0;
+#endif
         SRB_POLISH_PASSES_LOOP(P);
         SYNC();
         if (accepted) {

@@ -614,8 +614,15 @@ extern "C" __global__ void __launch_bounds__(64) __attribute__((amdgpu_waves_per
         sh.vg[lane] = f;
         io.QP_force[A12 + lane] = f;
     }
+    // (each load through its own address space: the plain select had been merged into one generic-pointer
+    // flat load -- the shipped code objects carry no flat memory instruction, tests/test_isa_hazard.py)
     double taut = 0.0;
-    if (lane < NQ) taut = (lane < 6) ? io.tau[A18 + lane] : sh.vx[con + lane - 6];
+    if (lane < NQ) {
+        const __attribute__((address_space(1))) double *tg = (const __attribute__((address_space(1))) double *)(io.tau + A18);
+        const __attribute__((address_space(3))) double *tl = (const __attribute__((address_space(3))) double *)(sh.vx + con);
+        const double a = tg[lane < 6 ? lane : 0], b = tl[lane < 6 ? 0 : lane - 6];
+        taut = (lane < 6) ? a : b;
+    }
     const int sw = NU - con;
     double *sJs = sh.u.as.J, *sJD = sh.u.as.M, *sDl = sh.u.as.K;
     if (sw > 0) {

@@ -195,6 +195,17 @@ def scan(body):
 
 
 STORES = ("global_store", "ds_write", "scratch_store", "buffer_store")
+FLAT_MEM = re.compile(r"^\s*(flat_(load|store|atomic)\w*)\b")
+
+
+def flat_mem(body):
+    """(line index, line) of every FLAT (generic-address) memory instruction in one kernel body.  A flat
+    access may target LDS; it is counted in both vmcnt and lgkmcnt, returns out of order with the DS
+    operations of its own wave, and falls outside the in-order argument the NW = 1 SYNC() (a wavefront
+    fence without s_waitcnt) rests on.  The round-5 build whose lip_eq_res read x0 (global) or the LDS
+    iterate through one pointer carried them and broke the polish; the shipped
+    kernels carry none (tests/test_isa_hazard.py)."""
+    return [(k, ln.strip()) for k, ln in enumerate(body) if FLAT_MEM.match(ln)]
 
 
 def read_before_redefined(body, start, live0, labels, budget=6000):
@@ -241,7 +252,11 @@ def main():
         total += len(f)
         for k, t, r in f:
             print(f"{name}: line {k}: {t}   (read after the exec restore: {r})")
-    print(f"{total} hazardous copies")
+        fl = flat_mem(body)
+        total += len(fl)
+        for k, t in fl:
+            print(f"{name}: line {k}: {t}   (flat memory instruction)")
+    print(f"{total} findings (hazardous copies + flat memory instructions)")
     return 1 if total else 0
 
 
