@@ -397,7 +397,7 @@ def main_srb12(args, world, rank, local_rank, dev):
                                "inter-agent CBF, fp64", "agents_per_gpu": A_local, "agents_total": A_total,
                    "parallelism": f"agents sharded x{world}"},
         "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
-        "optimal_frac": float((status == 0).all(1).mean()), "iters_mean": iters.mean(0).tolist(),
+        "optimal_frac": float((np.isin(status[:, 0], (0, 4)) & (status[:, 1] == 0)).mean()), "iters_mean": iters.mean(0).tolist(),
         "iters_max": iters.max(0).tolist(),
         "roofline": {"bound": "mfma", "limiter": "latency", "achieved": achieved, "peak": FP64_PEAK_TFLOPS,
                      "unit": "TFLOP/s", "frac": achieved / FP64_PEAK_TFLOPS, "traffic": traffic_from("s12", n_loc)[0],
@@ -564,8 +564,24 @@ def main():
     Ko, Kn = solver.n_selected(sh["obstacles"].shape[0], A_total if cfg["K_nbr"] > 0 else 0)
     out["sel"] = torch.zeros((n_loc, Ko + Kn), dtype=torch.int32, device=dev)
 
+    if exchange is not None:
+        solver.set_option("selection", 0)          # the step selects around the collective (below)
+
     def step():
-        nb = exchange(nbr_local) if exchange is not None else nbr_all
+        if exchange is None:
+            solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nbr_all, out, agent_offset=lo,
+                                stream=stream.cuda_stream, alpha_buf=alpha_buf, obstacles_version=1)
+            return
+        # multi-GPU: the all-gather of the neighbour snapshot is issued first (RCCL on its own
+        # stream), the static obstacles -- which need no neighbour row -- are selected on the compute stream
+        # while it is in flight, then the compute stream waits for the collective (no host block) and the
+        # neighbour selection and the solve follow
+        pend = exchange.start(nbr_local)
+        solver.select_device(t["x0"], t["obstacles"], exchange.out, out["sel"], tables=1, agent_offset=lo,
+                             stream=stream.cuda_stream, obstacles_version=1)
+        nb = pend.wait()
+        solver.select_device(t["x0"], t["obstacles"], nb, out["sel"], tables=2, agent_offset=lo,
+                             stream=stream.cuda_stream)
         solver.solve_device(t["x0"], t["ref"], t["foot"], t["obstacles"], nb, out, agent_offset=lo,
                             stream=stream.cuda_stream, alpha_buf=alpha_buf, obstacles_version=1)
 
@@ -633,8 +649,8 @@ def main():
                    "emulated_shards": args.emulate_shards, "n_obs": int(sh["obstacles"].shape[0]),
                    "nbr_rows": int(A_total if cfg["K_nbr"] else 0)},
         "p50_ms": float(np.percentile(per_step, 50)), "p99_ms": float(np.percentile(per_step, 99)),
-        "optimal_frac": float((status == 0).all(1).mean()),
-        "acceptable_frac": float(((status[:, 0] == 0) & (status[:, 1] == 4)).mean()),
+        "optimal_frac": float((np.isin(status[:, 0], (0, 4)) & (status[:, 1] == 0)).mean()),
+        "acceptable_frac": float((np.isin(status[:, 0], (0, 4)) & (status[:, 1] == 4)).mean()),
         "iters_mean": [float(iters[:, 0].mean()), float(iters[:, 1].mean())],
         "iters_max": [int(iters[:, 0].max()), int(iters[:, 1].max())],
         "qp_init": args.qp_init,

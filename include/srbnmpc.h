@@ -81,10 +81,14 @@ int srb_nv(const srb_params *p);     /* (6+C)N+1 */
  *                           may be NULL when K_nbr == 0.  Local agent a is global agent
  *                           agent_offset + a (itself excluded from its neighbours).
  * Outputs:
- *   x_qp      [A][nv]       QP-stage solution (qp_solution_eventbased_, :350-354); may be NULL
+ *   x_qp      [A][nv]       QP-stage solution (qp_solution_eventbased_, :350-354); may be NULL.  With the NLP
+ *                           stage on it is the NLP's warm start, solved to SRB_OPT_QP_WARM_TOL (default 0.3,
+ *                           status 4 below), not to iSWIFT's 1e-6 -- set that option to 0 for the reference's
+ *                           point (the MPC_dist shims do); srb_solve_qp always solves to 1e-6
  *   x         [A][nv]       final decision vector (mpc_state_eventbased_ after :423-426)
  *   obj       [A]           0.5 x'Q_qp x + f'x (ExCost::GetCost)
  *   status    [A][2] int    QP, NLP exit codes: 0 OPTIMAL, 1 KKTFAIL, 2 MAXIT, 3 FATAL (iSWIFT's);
+ *                           QP also 4 QP_WARM: converged at the warm-start tolerance only (the NLP follows);
  *                           NLP also 4 ACCEPTABLE: stopped at a near-optimal iterate (primal and
  *                           complementarity met, dual residual within 100x of its threshold)
  *                           whose next step was blocked or needed an inertia shift, or met only
@@ -154,7 +158,12 @@ int srb_ctx_waves(srb_ctx *ctx);
  *                                result is unchanged (the polish makes it exact; statuses and NLP iterations
  *                                unchanged on the bench batches) while the QP stage takes 3.0 instead of 5.8
  *                                iterations at configs[2]; x_qp is then that rougher point.  The
- *                                QP-only solve (srb_solve_qp, use_nlp = 0) always runs to the full tolerance */
+ *                                QP-only solve (srb_solve_qp, use_nlp = 0) always runs to the full tolerance.
+ *                                Such a QP stage reports status 4 (QP_WARM: converged at this tolerance), never
+ *                                0; with 0 here it reports iSWIFT's codes (0 OPTIMAL at 1e-6)
+ *   SRB_OPT_SELECTION            1 (default): srb_solve_batch_device runs the obstacle / neighbour selection
+ *                                itself; 0: the caller has filled batch.sel with srb_select_device (the two
+ *                                tables may then be selected on either side of the neighbour all-gather) */
 #define SRB_OPT_POLISH 1
 #define SRB_OPT_POLISH_RHO 2
 #define SRB_OPT_POLISH_WAVES 3
@@ -164,6 +173,7 @@ int srb_ctx_waves(srb_ctx *ctx);
 #define SRB_OPT_LAST_POLISH 7
 #define SRB_OPT_TIMING 8
 #define SRB_OPT_QP_WARM_TOL 9
+#define SRB_OPT_SELECTION 10
 int srb_ctx_set_option(srb_ctx *ctx, int opt, double value);
 int srb_ctx_get_option(srb_ctx *ctx, int opt, double *value);
 
@@ -194,6 +204,13 @@ int srb_solve_qp(srb_ctx *ctx, int n_agents, const srb_batch *host_io);
  * events -- is therefore never used by two launches in flight.  For solves that run
  * concurrently, use one context per stream. */
 int srb_solve_batch_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, void *stream);
+
+/* The selection alone (MPC_dist.cpp:371-396 generalised to K), asynchronous on `stream`: tables = 1 the static
+ * obstacles (columns 0 .. Ko-1 of dev_io->sel), 2 the neighbour snapshot (columns Ko .. Ko+Kn-1), 3 both.
+ * dev_io->sel is required; the other members are read as srb_solve_batch_device reads them.  Multi-GPU use
+ * (bench.py): select the static obstacles while the neighbour all-gather is in flight, the neighbours after
+ * it, then solve with SRB_OPT_SELECTION = 0.  Indices are identical to the solve's own selection. */
+int srb_select_device(srb_ctx *ctx, int n_agents, const srb_batch *dev_io, int tables, void *stream);
 int srb_sync(srb_ctx *ctx);
 
 /*

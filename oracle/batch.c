@@ -27,6 +27,7 @@ int orc_solve_agent(const orc_params *p_in, const double x0[4], const double *re
      * SRB_OPT_QP_WARM_TOL; the reference runs iSWIFT to 1e-6 there -- a documented deviation) */
     const double tq = (p->use_nlp && p->tol_qp > 0.0) ? p->tol_qp : p->tol;
     status[0] = orc_qp_solve_init(nv, mq, neq, Pd, c, A, b, G, h, p->qp_maxit, tq, p->qp_init, xq, NULL, &iters[0]);
+    if (status[0] == 0 && tq > p->tol) status[0] = 4;      /* converged at the warm-start tolerance only (the kernel's rule) */
     if (x_qp) memcpy(x_qp, xq, sizeof(double) * nv);
     status[1] = 0; iters[1] = 0;
     if (p->use_nlp) {

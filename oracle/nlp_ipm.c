@@ -155,6 +155,9 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
 #define ORC_POLISH_EQTOL 1e-8     /* the equality rows hold to this at an accepted point (kernel SRB_POLISH_EQTOL) */
+#define ORC_POLISH_STOL 1e-7      /* ... and the reduced stationarity |Z'(grad f + J_A' z_A)|_inf <= this max(1, |grad f|_inf)
+                                     (kernel SRB_POLISH_STOL; round 6: 2.2e-9 at most on the accepted polishes of six
+                                     bench workloads -- the guard is against a point that is feasible but not stationary) */
 #define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */
 #define ORC_POLISH_DX1 1e-4       /* a Newton step this small whose active rows then hold to CTOL ends the pass */
 #define ORC_POLISH_CTOL 1e-10
@@ -163,6 +166,8 @@ static double g_polish_rho = ORC_POLISH_RHO;
 static double g_polish_kappa = 1e4;
 static int g_polish_zinit = 1;    /* exploration: 1 = a later pass starts from the previous pass's z_A */
 int orc_early_stats[2];
+unsigned long long orc_polish_stat_max[2];   /* exploration: the largest reduced stationarity / scale of an accepted (0) /
+                                                rejected (1) pass, as the bits of a non-negative double (ordered as the values) */
 int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */          /* exploration counters: early polish attempts failed / accepted */
 static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
 static double g_polish_omcap = ORC_POLISH_OMCAP;
@@ -268,8 +273,8 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
             if (act[r]) { nact++; zm = fmax(zm, fabs(za[r])); zmin = fmin(zmin, za[r]); cv = fmax(cv, fabs(g[r] - hh[r])); }
         }
         /* reduced stationarity: gradient part and multiplier part separately for the scale */
-        double gf = 0.0, gz = 0.0, res = 0.0;
-        for (int j = 0; j < n; j++) v[j] = P->Pd[j] * xt[j] + P->c[j];
+        double gf = 0.0, gz = 0.0, res = 0.0, gmax = 0.0;
+        for (int j = 0; j < n; j++) { v[j] = P->Pd[j] * xt[j] + P->c[j]; gmax = fmax(gmax, fabs(v[j])); }
         for (int a = 0; a < nz; a++) { double acc = 0; for (int j = 0; j < n; j++) acc += Z[(size_t)j * nz + a] * v[j]; gr[a] = acc; gf = fmax(gf, fabs(acc)); }
         for (int j = 0; j < n; j++) v[j] = 0.0;
         for (int r = 0; r < m; r++) if (act[r]) for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) v[Ji[4 * r + t]] += Jv[4 * r + t] * za[r];
@@ -282,18 +287,26 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
          * polished point: the kernel's SRB_POLISH_EQTOL test (the LU step keeps them to round-off) */
         double eqr = 0.0;
         for (int k = 0; k < P->p; k++) eqr = fmax(eqr, fabs(dotv(P->A + (size_t)k * n, xt, n) - P->b[k]));
-        /* converged Newton iteration (the last correction) stands for stationarity: the step solves
-         * grad f + H dx + J_A' z_A+ = 0, so at x + dx the reduced gradient of the Lagrangian is
-         * O(|H| |dx|); `res` (the reduced stationarity itself) is reported by the trace only */
-        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL && eqr <= ORC_POLISH_EQTOL;
+        /* a converged Newton iteration (the last correction) makes the reduced gradient of the Lagrangian
+         * O(|H| |dx|); round 6 tests it as well, from the problem data (grad f = Pd x + c) and the polish's own
+         * multipliers: a point that is feasible, converged and dual feasible but not stationary -- what the
+         * round-5 generic-pointer build returned as OPTIMAL -- is rejected (kernel, same rule) */
+        ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL && eqr <= ORC_POLISH_EQTOL &&
+             res <= ORC_POLISH_STOL * fmax(1.0, gmax);
         if (trace)
             fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  last dx %.2e  stat %.2e (scale %.2e)  -> %s\n",
-                    pass, nact, pv, cv, nact ? zmin : 0.0, zm, lastdx, res, fmax(1.0, fmax(gf, gz)), ok ? "accepted" : "rejected");
+                    pass, nact, pv, cv, nact ? zmin : 0.0, zm, lastdx, res, fmax(1.0, gmax), ok ? "accepted" : "rejected");
         if (trace > 1)
             for (int r = 0; r < m; r++)
                 if (act[r] || g[r] - hh[r] > ORC_POLISH_PTOL)
                     fprintf(stderr, "    row %3d (%s) act %d  s %.3e z %.3e  za %.4e  g-h %.3e\n", r,
                             r < P->mq ? "lin" : r < P->mq + P->mo ? "obs" : "vel", act[r], s[r], z[r], za[r], g[r] - hh[r]);
+        {
+            const double sr = res / fmax(1.0, gmax);
+            unsigned long long bits, *dst = &orc_polish_stat_max[ok ? 0 : 1], cur = __atomic_load_n(dst, __ATOMIC_RELAXED);
+            memcpy(&bits, &sr, sizeof bits);
+            while (bits > cur && !__atomic_compare_exchange_n(dst, &cur, bits, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}
+        }
         if (ok) break;
         /* next pass: the row with the most negative multiplier leaves the active set (one at a
          * time: near-dependent active rows -- one obstacle at consecutive grids -- share large

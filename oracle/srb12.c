@@ -593,6 +593,7 @@ int orc12_solve_agent(const orc12_params *p_in, const double x0[12], const doubl
         }
     }
     status[0] = ipm(&P, 0, z, lam, &iters[0]);
+    if (status[0] == 0 && prm->use_nlp && prm->tol_qp > prm->tol) status[0] = 4;   /* warm-start tolerance only (kernel rule) */
     if (x_qp) memcpy(x_qp, z, sizeof(double) * n);
     status[1] = (prm->use_nlp && status[0] == 3) ? 3 : 0;      /* FATAL QP: the NLP stage is not run (kernel, same rule) */
     iters[1] = 0;

@@ -1111,7 +1111,8 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             S12ST(7);   // corrector row step + update
         }
         if (stage == 0) {
-            qp_flag = flag; qp_it = it;
+            // stopped at the warm-start tolerance tol_qp: 4, never OPTIMAL (oracle/srb12.c, same rule)
+            qp_flag = (flag == 0 && tol_s > tol) ? 4 : flag; qp_it = it;
             if (x_qp_out)
                 for (int v = tid; v < nv; v += 64) x_qp_out[(size_t)agent * nv + v] = L.Z[v];
             // a FATAL QP stage ends the solve: the NLP stage does not run and reports FATAL too (a

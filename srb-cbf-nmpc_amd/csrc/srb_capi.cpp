@@ -36,7 +36,7 @@ typedef void (*srb_polish_fn)(SrbKParams, int, const double *, const double *, c
 struct SrbGrid;
 extern "C" __global__ void srb_knn_kernel(int n_agents, const double *x0g, const double *obstacles, int n_obs,
                                           const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
-                                          int *sel_out, const SrbGrid *gob, const int *oob, const double2 *pob,
+                                          int *sel_out, int sel_stride, const SrbGrid *gob, const int *oob, const double2 *pob,
                                           const int *iob, const SrbGrid *gnb, const int *onb, const double2 *pnb,
                                           const int *inb);
 extern "C" __global__ void srb_grid_build_kernel(const double *tab0, int stride0, int n0, SrbGrid *g0, int *off0,
@@ -122,6 +122,7 @@ struct srb_ctx {
     int polish, polish_waves, grid_min_rows, grid_min_rows_static, polish_fused;
     int last_polish;               // how the last launch polished: 0 no, 1 polish kernel, 2 fused
     int timing;                    // 1: HIP events around the kernels (srb_last_kernel_ms); 0: none
+    int selection;                 // SRB_OPT_SELECTION: 1 the solve launches the selection, 0 the caller did
     double polish_rho;
     double qp_warm_tol;            // SRB_OPT_QP_WARM_TOL
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
@@ -312,7 +313,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->grid_src = nullptr; c->grid_n = 0; c->grid_ver = 0;
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
-    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->qp_warm_tol = SRB_QP_WARM_TOL; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1;
+    c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->qp_warm_tol = SRB_QP_WARM_TOL; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1; c->selection = 1;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -363,8 +364,9 @@ extern "C" int srb_ctx_destroy(srb_ctx *c)
 // (stride 4); shared with the SRB-12 mode (srb12_capi.cpp), which hands over its CoM positions so.
 static int launch_select(srb_ctx *c, int n_agents, const double *x0, const double *obstacles, int n_obs,
                          const double *nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
-                         int obstacles_version, int *sel, hipStream_t s)
+                         int obstacles_version, int *sel, hipStream_t s, int sel_stride = -1)
 {
+    if (sel_stride < 0) sel_stride = K_obs + K_nbr;
     // long tables (a swarm sharded over GPUs: the whole neighbour snapshot, obstacles scaled
     // with the arena) get a uniform grid so each agent scans only the cells around it
     // (a versioned static obstacle table builds its grid once, so it pays off at fewer rows;
@@ -386,7 +388,7 @@ static int launch_select(srb_ctx *c, int n_agents, const double *x0, const doubl
     }
     if (go_build) { c->grid_src = obstacles; c->grid_n = n_obs; c->grid_ver = obstacles_version; }
     hipLaunchKernelGGL(srb_knn_kernel, dim3(n_agents), dim3(64 * SRB_KNN_WAVES), 0, s, n_agents, x0, obstacles, n_obs,
-                       nbr_state, n_all, agent_offset, K_obs, K_nbr, sel,
+                       nbr_state, n_all, agent_offset, K_obs, K_nbr, sel, sel_stride,
                        go ? (const SrbGrid *)G0.g : nullptr, G0.off, G0.spos, G0.sidx,
                        gn ? (const SrbGrid *)G1.g : nullptr, G1.off, G1.spos, G1.sidx);
     HIPCHK(hipGetLastError());
@@ -436,7 +438,9 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     if (c->timing) HIPCHK(hipEventRecord(c->ev[0], s));
     // two launches: nearest obstacle / neighbour selection, then QP and NLP stages per agent
     int *sel = d->sel ? d->sel : c->sel;
-    if (use_nlp && k.K_obs + k.K_nbr > 0) {
+    // SRB_OPT_SELECTION 0: the caller filled d->sel by srb_select_device (its two tables may then be selected
+    // around a collective, bench.py's multi-GPU step)
+    if (use_nlp && k.K_obs + k.K_nbr > 0 && c->selection) {
         int rc = launch_select(c, n_agents, d->x0, d->obstacles, n_obs, d->nbr_state, n_all, d->agent_offset, k.K_obs,
                                k.K_nbr, d->obstacles_version, sel, s);
         if (rc) return rc;
@@ -509,6 +513,9 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
     case SRB_OPT_TIMING:
         if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_TIMING: 0 or 1");
         c->timing = (int)v; return SRB_OK;
+    case SRB_OPT_SELECTION:
+        if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_SELECTION: 0 or 1");
+        c->selection = (int)v; return SRB_OK;
     case SRB_OPT_GRID_MIN_ROWS:
     case SRB_OPT_GRID_MIN_ROWS_STATIC:
         if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
@@ -532,6 +539,7 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_LAST_POLISH: *v = c->last_polish; return SRB_OK;
     case SRB_OPT_TIMING: *v = c->timing; return SRB_OK;
     case SRB_OPT_QP_WARM_TOL: *v = c->qp_warm_tol; return SRB_OK;
+    case SRB_OPT_SELECTION: *v = c->selection; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }
@@ -555,6 +563,38 @@ extern "C" int srb_solve_batch_device(srb_ctx *c, int n_agents, const srb_batch 
     int rc = order_after_last(c, s);
     if (!rc) rc = launch(c, n_agents, dev_io, s, c->p.use_nlp);
     if (!rc && n_agents > 0) rc = mark_done(c, s);
+    return rc;
+}
+
+// One or both tables of the selection into dev_io->sel (required; [A][Ko + Kn], the layout the solve reads):
+// tables bit 0 the static obstacles (its columns 0 .. Ko - 1), bit 1 the neighbour snapshot (Ko .. Ko + Kn - 1).
+// With SRB_OPT_SELECTION = 0 the solve then uses sel as it is, so a caller can select the static obstacles
+// while the neighbour all-gather is in flight and the neighbours after it (bench.py).
+extern "C" int srb_select_device(srb_ctx *c, int n_agents, const srb_batch *d, int tables, void *stream)
+{
+    if (d && d->struct_size != (int)sizeof(srb_batch))
+        return fail(SRB_ERR_ARG, "srb_batch.struct_size != sizeof(srb_batch): caller built against another ABI");
+    if (!c || !d) return fail(SRB_ERR_ARG, "null argument");
+    if (tables < 1 || tables > 3) return fail(SRB_ERR_ARG, "tables: 1 (static obstacles), 2 (neighbours) or 3 (both)");
+    if (n_agents < 0 || n_agents > c->max_agents) return fail(SRB_ERR_ARG, "n_agents exceeds max_agents");
+    if (!d->x0 || !d->sel) return fail(SRB_ERR_ARG, "missing buffer (x0, sel)");
+    if (n_agents == 0) return SRB_OK;
+    const srb_params *p = &c->p;
+    int Ko = p->K_obs, Kn = p->K_nbr;                     // clamped exactly as the solve does
+    if (Ko > d->n_obs) Ko = d->n_obs > 0 ? d->n_obs : 0;
+    const int others = d->nbr_state ? d->n_all - 1 : 0;
+    if (Kn > others) Kn = others > 0 ? others : 0;
+    if ((tables & 1) && Ko > 0 && !d->obstacles) return fail(SRB_ERR_ARG, "obstacles missing");
+    if ((tables & 2) && Kn > 0 && (d->agent_offset < 0 || d->agent_offset + n_agents > d->n_all))
+        return fail(SRB_ERR_ARG, "agent_offset out of range of the neighbour table");
+    hipStream_t s = (hipStream_t)stream;
+    HIPCHK(hipSetDevice(c->device));
+    int rc = order_after_last(c, s);
+    const int ko = (tables & 1) ? Ko : 0, kn = (tables & 2) ? Kn : 0;
+    if (!rc && ko + kn > 0)
+        rc = launch_select(c, n_agents, d->x0, d->obstacles, ko ? d->n_obs : 0, d->nbr_state, kn ? d->n_all : 0,
+                           d->agent_offset, ko, kn, d->obstacles_version, d->sel + (ko ? 0 : Ko), s, Ko + Kn);
+    if (!rc) rc = mark_done(c, s);
     return rc;
 }
 

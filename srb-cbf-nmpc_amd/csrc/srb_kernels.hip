@@ -948,6 +948,51 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
     return r;
 }
 
+// Reduced stationarity of the polished point (round 6): g = Z'(grad f(x) + J_A' z_A), grad f from the problem data
+// (var_weight, the reference window in LDS) rather than the slots' cost registers, z_A the polish's multipliers
+// (ds: active mask, dz: z_A); accepted only where max |g| <= SRB_POLISH_STOL max(1, |grad f|_inf).  The other
+// tests (feasibility, multiplier signs, converged step, equality rows) held on the points the round-5 generic-
+// pointer build returned as OPTIMAL although they were not stationary; this one does not.  The
+// term rows are those of the last Newton step (the obstacle rows linearised at its start: O(|dx|) <= 1e-7 off).
+// Uniform over the workgroup (every value reduced).  oracle/nlp_ipm.c `polish`: the same test.
+template <int NZL, int TS, int NW>
+__device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, const SrbKParams &prm, const double *xs,
+                                                  const double *ref, double *CF, const double *R, int cnt, const ObsFold &OF,
+                                                  int nko, double *vg, int nz, int tid, double *part, uint64_t bmask,
+                                                  double *red, int N, int n, int TT)
+{
+    double gmax = 0.0;
+    SYNC();                                              // every lane's reads of CF / vg of the last step are done
+#pragma unroll
+    for (int t = 0; t < TS; t++)
+        if (t < nts) {
+            const Slot &q = Q[t];
+            const double zj = q.ds[0] * q.dz[0] - q.ds[1] * q.dz[1];
+            const int kd = kind_of(q);
+            if (kd == K_VAR) {
+                const int v = q.i0;
+                const double a0 = var_weight(prm, v), gf = fma(a0, xs[v], (v < 4 * N) ? -a0 * ref[v] : 0.0);
+                gmax = fmax(gmax, fabs(gf));
+                CF[q.wr] = gf + zj;
+            } else if (kd == K_COP || kd == K_OBS) {
+                CF[q.wr] = zj;
+            }
+        }
+    if (NW > 1) SYNC();                                  // the VAR rows' plain stores land before the VEL adds
+#pragma unroll
+    for (int t = 0; t < TS; t++)
+        if (t < nts && kind_of(Q[t]) == K_VEL)
+            __hip_atomic_fetch_add(&CF[Q[t].r], Q[t].ds[0] * Q[t].dz[0] - Q[t].ds[1] * Q[t].dz[1], __ATOMIC_RELAXED,
+                                   __HIP_MEMORY_SCOPE_WORKGROUP);
+    SYNC();
+    rhs_only<NZL, NW>(R, CF, cnt, OF, nko, vg, nz, tid, part, bmask);
+    SYNC();
+    const int lane = tid & 63;
+    double rv[2] = {gmax, (lane < nz) ? fabs(vg[lane]) : 0.0};
+    wred_x<2, 3u, NW>(rv, red + 5 * 8 * NW, tid);
+    return rv[1] <= SRB_POLISH_STOL * fmax(1.0, rv[0]);
+}
+
 // --------------------------------------------------------------------------- shared agent code
 // The solve kernel and the polish kernel run on the same per-agent LDS layout and rebuild the
 // same null-space basis, so the code they share is written once, as statement macros expanded in
@@ -1237,7 +1282,8 @@ _Pragma("unroll")                                                               
         POLDBG(pass, 5, lastdx); POLDBG(pass, 7, eqr);                                                                                        \
         SRB_POLISH_DIAG();                                                                                                                    \
         if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&                             \
-            eqr <= SRB_POLISH_EQTOL) {                                                                                                        \
+            eqr <= SRB_POLISH_EQTOL && polish_stationary<NZL, TS, NW>(PS, nts, prm, xs, ref, CF, R, cnt, OF, nko, vg, nz, tid, part,      \
+                                                                      bmask, red, N, n, TT)) {                                                \
             POLDBG(pass, 6, 1.0);                                                                                                             \
             accepted = true;                                                                                                                  \
             break;                                                                                                                            \
@@ -1851,7 +1897,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         } else if ((zpol_g || prm.polish_fused) && nl) {
             export_zpol();
         }
-        if (stage == 0) { qp_flag = flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
+        // a QP stage that stopped at the warm-start tolerance reports 4 (its point is the NLP's warm start, not
+        // iSWIFT's 1e-6 point), never OPTIMAL (oracle/batch.c, the same rule)
+        if (stage == 0) { qp_flag = (flag == 0 && tolS > tol) ? 4 : flag; qp_it = it; } else { nlp_flag = flag; nlp_it = it; }
     }
     SYNC();
     if (x_qp_out && nstage == 1)
@@ -2047,7 +2095,7 @@ SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
 extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(int n_agents,
                 const double *__restrict__ x0g, const double *__restrict__ obstacles, int n_obs,
                 const double *__restrict__ nbr_state, int n_all, int agent_offset, int K_obs, int K_nbr,
-                int *__restrict__ sel_out, const SrbGrid *__restrict__ gob, const int *__restrict__ oob,
+                int *__restrict__ sel_out, int sel_stride, const SrbGrid *__restrict__ gob, const int *__restrict__ oob,
                 const double2 *__restrict__ pob, const int *__restrict__ iob, const SrbGrid *__restrict__ gnb,
                 const int *__restrict__ onb, const double2 *__restrict__ pnb, const int *__restrict__ inb)
 {
@@ -2056,7 +2104,9 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
     const int agent = xcd_agent(blockIdx.x, gridDim.x), tid = threadIdx.x;
     if (agent >= n_agents) return;                 // whole workgroup: the barriers stay uniform
     const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
-    int *sel = sel_out + (size_t)agent * (K_obs + K_nbr);
+    // sel_stride = Ko + Kn of the whole selection; a pass over one table (srb_select_device) hands over
+    // K_obs or K_nbr alone and sel_out already offset to its columns
+    int *sel = sel_out + (size_t)agent * sel_stride;
     if (SRB_KNN_WAVES == 2 && K_obs > 0 && K_nbr > 0) {
         // the two tables on the two waves at once, each selection wave-local (DPP argmins, no barrier):
         // configs[2] selection 23.5 -> 20.9 us a step (HIP events, round 5); the same rows.  (Selecting

@@ -26,10 +26,14 @@ LIB_PATH = os.path.join(_HERE, "libsrbnmpc.so")
 _dp = ctypes.POINTER(ctypes.c_double)
 _ip = ctypes.POINTER(ctypes.c_int)
 
-OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4   # ACCEPTABLE: NLP stage only
+OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4
+# status 4 means, by stage: NLP -- ACCEPTABLE (round-off floor, or a loosened exit whose polish was not
+# accepted); QP stage followed by the NLP -- QP_WARM, converged at the warm-start tolerance (SRB_OPT_QP_WARM_TOL;
+# x_qp is the NLP's warm start, not iSWIFT's 1e-6 point); the last stage of an SRB-12 solve -- its polish rejected
+QP_WARM = 4
 # srb_ctx_set_option codes (SRB_OPT_* of include/srbnmpc.h)
 OPTIONS = {"polish": 1, "polish_rho": 2, "polish_waves": 3, "grid_min_rows": 4, "grid_min_rows_static": 5,
-           "polish_fused": 6, "last_polish": 7, "timing": 8, "qp_warm_tol": 9}
+           "polish_fused": 6, "last_polish": 7, "timing": 8, "qp_warm_tol": 9, "selection": 10}
 ABI_VERSION = 5                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 
@@ -103,6 +107,7 @@ def lib():
         for f in ("srb_solve_batch", "srb_solve_qp"):
             getattr(L, f).argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch)]
         L.srb_solve_batch_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_void_p]
+        L.srb_select_device.argtypes = [ctypes.c_void_p, ctypes.c_int, ctypes.POINTER(Batch), ctypes.c_int, ctypes.c_void_p]
         L.srb_sync.argtypes = [ctypes.c_void_p]
         L.srb_ctx_set_waves.argtypes = [ctypes.c_void_p, ctypes.c_int]
         L.srb_ctx_waves.argtypes = [ctypes.c_void_p]
@@ -245,6 +250,26 @@ class BatchSolver:
                   dptr(out.get("alpha") if alpha_buf is not None else None),
                   iptr(out["sel"]) if out.get("sel") is not None else None, int(obstacles_version))
         _check(lib().srb_solve_batch_device(self._h, A, ctypes.byref(b), self._stream(stream)))
+
+    def select_device(self, x0, obstacles, nbr_state, sel, tables: int = 3, agent_offset: int = 0, stream=None,
+                      obstacles_version: int = 0):
+        """The obstacle / neighbour selection alone (srb_select_device) into the int32 tensor sel [A][Ko + Kn]:
+        tables 1 the static obstacles, 2 the neighbour snapshot, 3 both.  With the option "selection" set
+        to 0, solve_device then uses out["sel"] as filled here (bench.py selects the static obstacles while
+        the neighbour all-gather is in flight).  Asynchronous on `stream` like solve_device."""
+        A = x0.shape[0]
+        Ko, Kn = self.n_selected(0 if obstacles is None else obstacles.shape[0],
+                                 0 if nbr_state is None else nbr_state.shape[0])
+        if sel.dtype != torch_int32() or tuple(sel.shape) != (A, Ko + Kn) or not sel.is_contiguous():
+            raise ValueError(f"sel must be a contiguous int32 tensor of shape ({A}, {Ko + Kn}), got {tuple(sel.shape)} {sel.dtype}")
+
+        def dptr(t):
+            return None if t is None else ctypes.cast(ctypes.c_void_p(t.data_ptr()), _dp)
+        b = Batch(dptr(x0), None, None, dptr(obstacles), dptr(nbr_state),
+                  0 if obstacles is None else obstacles.shape[0], 0 if nbr_state is None else nbr_state.shape[0],
+                  int(agent_offset), None, None, None, None, None, None, None,
+                  ctypes.cast(ctypes.c_void_p(sel.data_ptr()), _ip), int(obstacles_version))
+        _check(lib().srb_select_device(self._h, A, ctypes.byref(b), int(tables), self._stream(stream)))
 
     def _stream(self, stream):
         """hipStream_t for a launch: the caller's, else torch's current stream on this device

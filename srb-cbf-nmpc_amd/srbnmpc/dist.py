@@ -43,22 +43,46 @@ class NeighbourExchange:
             rows = [r * self.cmax + i for r in range(world) for i in range(self.counts[r])]
             self.rows = _t.as_tensor(rows, dtype=_t.long, device=device)
             self.table = _t.zeros((n_total, 4), dtype=dtype, device=device)
+        self.out = self.recv if self.equal else self.table     # the [n_total, 4] table wait() returns
         # gloo (CPU tests) has no all_gather_into_tensor on every torch build: list form there
         self.flat = dist.is_initialized() and dist.get_backend() != "gloo"
 
     def __call__(self, local_state: torch.Tensor) -> torch.Tensor:
+        return self.start(local_state).wait()
+
+    def start(self, local_state: torch.Tensor) -> "PendingExchange":
+        """Issue the all-gather without waiting for it (async_op): the caller runs work that does not need
+        the neighbour table -- the static-obstacle selection (bench.py) -- then .wait() on the handle.  With
+        RCCL, wait() orders the caller's current stream after the collective without blocking the host, so
+        the static selection kernel and the all-gather overlap on the GPU."""
         if self.world == 1 and not self.force:
-            return local_state
+            return PendingExchange(self, None, local_state)
         if local_state.shape[0] != self.counts[self.rank]:
             raise ValueError(f"rank {self.rank} holds {self.counts[self.rank]} agents, got {local_state.shape[0]} rows")
         self.send[:local_state.shape[0]].copy_(local_state)
         if self.flat:
-            dist.all_gather_into_tensor(self.recv, self.send)
+            work = dist.all_gather_into_tensor(self.recv, self.send, async_op=True)
         else:
-            dist.all_gather(list(self.recv.view(self.world, self.cmax, 4).unbind(0)), self.send)
-        if self.equal:
-            return self.recv
-        torch.index_select(self.recv, 0, self.rows, out=self.table)
+            work = dist.all_gather(list(self.recv.view(self.world, self.cmax, 4).unbind(0)), self.send, async_op=True)
+        return PendingExchange(self, work, None)
+
+
+class PendingExchange:
+    """An all-gather in flight (NeighbourExchange.start); wait() returns the [n_total, 4] table."""
+
+    def __init__(self, ex: NeighbourExchange, work, table):
+        self.ex, self.work, self.table = ex, work, table
+
+    def wait(self) -> torch.Tensor:
+        if self.table is not None:
+            return self.table
+        self.work.wait()
+        ex = self.ex
+        if ex.equal:
+            self.table = ex.recv
+        else:
+            torch.index_select(ex.recv, 0, ex.rows, out=ex.table)
+            self.table = ex.table
         return self.table
 
 

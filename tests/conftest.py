@@ -36,6 +36,22 @@ def _ensure_built():
 _ensure_built()
 
 
+QP_WARM = 4   # srbnmpc.QP_WARM: a QP stage followed by the NLP that stopped at the warm-start tolerance
+
+
+def ok_elem(st):
+    """Per stage: converged -- OPTIMAL, or for the QP stage (column 0) QP_WARM."""
+    st = np.asarray(st)
+    o = st == 0
+    o[:, 0] |= st[:, 0] == QP_WARM
+    return o
+
+
+def converged(st):
+    """Rows whose stages all converged (QP OPTIMAL or QP_WARM, NLP OPTIMAL)."""
+    return ok_elem(st).all(1)
+
+
 def load_golden(name):
     import json
     with open(os.path.join(GOLDEN, name)) as f:

@@ -53,6 +53,18 @@ def _worker(rank, world, port, n_total, q):
             ok_nbr &= bool(np.array_equal(o1, o2))
             ok_nbr &= bool(np.array_equal(oracle.select_idx(p, b["x0"][a], b["obstacles"], gathered, a),
                                           oracle.select_idx(p, b["x0"][a], b["obstacles"], b["nbr_state"], a)))
+        # split selection around the collective (bench.py's multi-GPU step): the all-gather is
+        # issued (start), the static obstacles are selected while it is in flight -- they need no neighbour
+        # row --, then wait() and the neighbour selection; the two parts together == the one-pass selection
+        p_st, p_nb = oracle.params(10, 2, K_obs=2, K_nbr=0), oracle.params(10, 2, K_obs=0, K_nbr=4)
+        for cycle, tab in enumerate((moved, b["nbr_state"])):
+            pend = ex.start(torch.as_tensor(tab[lo:hi]))
+            st = [oracle.select_idx(p_st, b["x0"][a], b["obstacles"], None, a) for a in range(lo, hi)]
+            got = pend.wait().numpy()
+            ok_nbr &= bool(np.array_equal(got, tab))
+            for i, a in enumerate(range(lo, hi)):
+                nb = oracle.select_idx(p_nb, b["x0"][a], b["obstacles"], got, a)
+                ok_nbr &= bool(np.array_equal(np.r_[st[i], nb], oracle.select_idx(p, b["x0"][a], b["obstacles"], tab, a)))
         # shard solve through the oracle with agent_offset == whole-batch rows
         r_local = oracle.solve_batch(p, b["x0"][lo:hi], b["ref"][lo:hi], b["foot"][lo:hi], b["obstacles"],
                                      gathered, agent_offset=lo)

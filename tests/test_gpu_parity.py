@@ -9,7 +9,7 @@ Tolerances (written here, from SURVEY.md §8c / BASELINE.json north star):
 """
 import numpy as np
 import pytest
-from conftest import load_golden
+from conftest import converged, load_golden, ok_elem
 
 import bench
 import oracle
@@ -116,7 +116,7 @@ def test_nlp_random_vs_certified_goldens():
     x0 = np.array([c["x0"] for c in cases]); ref = np.array([c["ref"] for c in cases]); foot = np.array([c["foot"] for c in cases])
     out = s.solve(x0, ref, foot, obstacles)
     xr = np.array([c["x"] for c in cases])
-    assert (out["status"] == 0).all()
+    assert converged(out["status"]).all()
     np.testing.assert_array_equal(out["iters"][:, 1], [c["iters"] for c in cases])
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, xr), atol=NLP_TOL, rtol=0)
     np.testing.assert_allclose(out["x"], xr, atol=1e-6, rtol=0)
@@ -179,7 +179,7 @@ def test_free_velocity_workload_statuses_and_solutions_vs_oracle():
     assert nonopt.sum() >= 5, nonopt.sum()                       # the workload is hard: some fail in both
     diff = np.where((out["status"] != r["status"]).any(1))[0]
     assert diff.size == 0, [(int(a), out["status"][a].tolist(), r["status"][a].tolist()) for a in diff]
-    ok_g, ok_o = out["status"] == 0, r["status"] == 0
+    ok_g, ok_o = ok_elem(out["status"]), ok_elem(r["status"])
     assert (ok_g[:, 0] == ok_o[:, 0]).mean() >= 0.99
     assert (ok_g.all(1) == ok_o.all(1)).mean() >= 0.98, (ok_g.all(1) != ok_o.all(1)).sum()
     both = ok_g.all(1) & ok_o.all(1)
@@ -237,7 +237,7 @@ def test_full_size_properties(A, Kn):
     s = solver(N, C, Ko, Kn)
     out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
     p = s.params
-    assert (out["status"] == 0).all(1).mean() >= 0.999          # OPTIMAL (polished) on both stages
+    assert converged(out["status"]).mean() >= 0.999            # converged (NLP polished: OPTIMAL) on both stages
     x = out["x"]
     assert _dynamics_residual(p, b["x0"], x) < 1e-9                          # Aeq x = beq (dynamics)
     Xs, U, L, sl = srbnmpc.split(p, x)
@@ -285,7 +285,7 @@ def test_unpolished_loosened_exit_is_acceptable_not_optimal():
     assert prov.sum() >= A // 10, prov.sum()                    # the loosened exit is the common case
     assert ((off["status"] == r["status"]).all(1)).mean() >= 0.99
     assert not ((off["status"][:, 1] == 0) & (r["status"][:, 1] == 4)).any()
-    assert (on["status"] == 0).all()                            # polished: OPTIMAL
+    assert converged(on["status"]).all()                        # polished: OPTIMAL
     # the interior-point results themselves are unchanged by the status rule
     np.testing.assert_allclose(xus(N, off["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
@@ -357,13 +357,13 @@ def test_config5_full_size_vs_oracle_and_acceptable_exit():
     s = solver(N, C, Ko, Kn)
     out = s.solve(b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
     st, it = out["status"], out["iters"]
-    assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
+    assert (st[:, 0] == srbnmpc.QP_WARM).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
     acc = np.where(st[:, 1] == srbnmpc.ACCEPTABLE)[0]
     assert acc.size <= 0.001 * A, acc.size                         # polish accepted on >= 99.9 %
     assert it[:, 1].max() <= 20                                    # no MAXIT tail (measured max 17)
     op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
     r = oracle.solve_batch(op, b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"], nthreads=16)
-    assert np.isin(r["status"][:, 1], [0, 4]).all() and (r["status"][:, 0] == 0).all()
+    assert np.isin(r["status"][:, 1], [0, 4]).all() and (r["status"][:, 0] == srbnmpc.QP_WARM).all()
     e = np.abs(xus(N, out["x"]) - xus(N, r["x"])).max(1)
     assert e.max() < NLP_TOL, (int(np.argmax(e)), float(e.max()))
     both = (st[:, 1] == 0) & (r["status"][:, 1] == 0)        # polished on both sides: the same KKT point
@@ -566,25 +566,48 @@ def test_qp_only_equals_qp_stage():
     assert (qp["iters"][:, 1] == 0).all()
 
 
-def test_qp_warm_tolerance_leaves_the_nlp_result():
-    """SRB_OPT_QP_WARM_TOL (default 0.3): the QP stage only warm-starts the NLP, so stopping it early changes
-    neither the NLP's statuses nor its result (to 1e-9) while the QP stage takes fewer iterations -- the
-    configs[2] batch against the full-tolerance QP stage (0), and against the oracle, which does the same."""
-    A, b, _, _ = bench.rank_batch(3, 1024, 1, 0)
-    cfg = bench.CONFIGS[3]
-    N, C, Ko, Kn = cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"]
+def _warm_workload(name):
+    if name == "c3":
+        A, b, _, _ = bench.rank_batch(3, 1024, 1, 0)
+        cfg = bench.CONFIGS[3]
+        return cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"], b
+    if name == "c5":
+        A, b, _, _ = bench.rank_batch(5, 2048, 1, 0)
+        cfg = bench.CONFIGS[5]
+        return cfg["N"], cfg["C"], cfg["K_obs"], cfg["K_nbr"], b
+    if name == "free":                       # infeasible and near-infeasible instances (FATAL in both)
+        return 10, 2, 3, 8, workload.make_batch(512, 10, 2, seed=0, velocity="free")
+    # crowded: four times the obstacle density of the reference's arena
+    return 10, 2, 3, 8, workload.make_batch(1024, 10, 2, seed=5, n_obs=int(round(80 * workload.arena_scale(1024) ** 2)))
+
+
+@pytest.mark.parametrize("name", ["c3", "free", "dense", "c5"])
+def test_qp_warm_tolerance_leaves_the_nlp_result(name):
+    """SRB_OPT_QP_WARM_TOL (default 0.3): the QP stage only warm-starts the NLP
+    (MPC_dist.cpp:403 starts SNOPT from iSWIFT's point), so stopping it early must leave the NLP's statuses
+    unchanged and its result within the polish's step tolerance (1e-7) -- on the configs[2] batch, the hard
+    free-velocity workload, a crowded arena and config 5 (N = 20), the kernel at 0.3 against the kernel at 0
+    (the full 1e-6).  A warm QP stage reports QP_WARM (4), never OPTIMAL.  The oracle makes the same
+    comparison on the CPU (tests/test_oracle.py::test_oracle_qp_warm_tolerance_leaves_the_nlp_result)."""
+    N, C, Ko, Kn, b = _warm_workload(name)
     args = (b["x0"], b["ref"], b["foot"], b["obstacles"], b["nbr_state"])
     s = solver(N, C, Ko, Kn)
     assert s.get_option("qp_warm_tol") == 3e-1
     warm = s.solve(*args)
     full = solver(N, C, Ko, Kn, qp_warm_tol=0.0).solve(*args)
-    np.testing.assert_array_equal(warm["status"], full["status"])
-    np.testing.assert_allclose(xus(N, warm["x"]), xus(N, full["x"]), atol=1e-9, rtol=0)
-    assert warm["iters"][:, 0].mean() < full["iters"][:, 0].mean() - 1.0 and warm["iters"][:, 0].max() < full["iters"][:, 0].max()
-    r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), *args, nthreads=16)
-    np.testing.assert_array_equal(conv(warm["status"]), conv(r["status"]))
-    assert (warm["iters"][:, 0] == r["iters"][:, 0]).mean() > 0.95
-    np.testing.assert_allclose(xus(N, warm["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
+    np.testing.assert_array_equal(warm["status"][:, 1], full["status"][:, 1])
+    np.testing.assert_array_equal(ok_elem(warm["status"])[:, 0], ok_elem(full["status"])[:, 0])
+    assert not (warm["status"][:, 0] == 0).any() and not (full["status"][:, 0] == srbnmpc.QP_WARM).any()
+    both = warm["status"][:, 1] == 0
+    assert both.mean() >= (0.9 if name == "free" else 0.99)
+    np.testing.assert_allclose(xus(N, warm["x"][both]), xus(N, full["x"][both]), atol=1e-7, rtol=0)
+    assert warm["iters"][:, 0].mean() < full["iters"][:, 0].mean() - 1.0
+    if name == "c3":
+        assert warm["iters"][:, 0].max() < full["iters"][:, 0].max()
+        r = oracle.solve_batch(oracle.params(N, C, K_obs=Ko, K_nbr=Kn), *args, nthreads=16)
+        np.testing.assert_array_equal(conv(warm["status"]), conv(r["status"]))
+        assert (warm["iters"][:, 0] == r["iters"][:, 0]).mean() > 0.95
+        np.testing.assert_allclose(xus(N, warm["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
 def test_device_api_matches_host():
@@ -604,6 +627,50 @@ def test_device_api_matches_host():
     torch.cuda.current_stream(dev).synchronize()
     np.testing.assert_array_equal(out["x"].cpu().numpy(), host["x"])
     np.testing.assert_array_equal(out["status"].cpu().numpy(), host["status"])
+
+
+@pytest.mark.parametrize("world,rank", [(1, 0), (8, 3)])
+def test_split_selection_around_the_collective_equals_one_pass(world, rank):
+    """bench.py's multi-GPU step: the static obstacles selected on the compute
+    stream while the neighbour all-gather is in flight (srb_select_device, tables 1), the neighbours after it
+    (tables 2, ordered by the collective's wait), then the solve with SRB_OPT_SELECTION = 0 -- bit-identical to
+    the solve's own one-pass selection (sel, x, status), for a single GPU and rank 3 of an 8-GPU configs[3]
+    swarm (its agent_offset, the whole snapshot)."""
+    A_total, b, lo, hi = bench.rank_batch(3, 1024 // world if world > 1 else 256, world, rank)
+    N, C, Ko, Kn = 10, 2, 3, 8
+    dev = torch.device("cuda:0")
+    t = {k: torch.as_tensor(np.ascontiguousarray(v), dtype=torch.float64, device=dev) for k, v in b.items()}
+    x0, ref, foot = t["x0"][lo:hi].contiguous(), t["ref"][lo:hi].contiguous(), t["foot"][lo:hi].reshape(hi - lo, -1).contiguous()
+    A = hi - lo
+    res = {}
+    for mode in ("one", "split"):
+        s = srbnmpc.BatchSolver(srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn), A)
+        ko, kn = s.n_selected(t["obstacles"].shape[0], A_total)
+        out = dict(x_qp=None, x=torch.zeros((A, s.params.nv), dtype=torch.float64, device=dev),
+                   obj=torch.zeros(A, dtype=torch.float64, device=dev),
+                   status=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+                   iters=torch.zeros((A, 2), dtype=torch.int32, device=dev),
+                   sel=torch.full((A, ko + kn), -7, dtype=torch.int32, device=dev))
+        st = torch.cuda.current_stream(dev).cuda_stream
+        if mode == "split":
+            side = torch.cuda.Stream(dev)
+            s.select_device(x0, t["obstacles"], t["nbr_state"], out["sel"], tables=1, agent_offset=lo, stream=st)
+            ev = torch.cuda.Event()
+            with torch.cuda.stream(side):             # stands in for the RCCL stream of the all-gather
+                nb = t["nbr_state"].clone()
+                ev.record(side)
+            torch.cuda.current_stream(dev).wait_event(ev)
+            s.select_device(x0, t["obstacles"], nb, out["sel"], tables=2, agent_offset=lo, stream=st)
+            s.set_option("selection", 0)
+        else:
+            nb = t["nbr_state"]
+        s.solve_device(x0, ref, foot, t["obstacles"], nb, out, agent_offset=lo, stream=st)
+        torch.cuda.current_stream(dev).synchronize()
+        res[mode] = {k: v.cpu().numpy() for k, v in out.items() if v is not None}
+        s.close()
+    for k in ("sel", "x", "status", "iters", "obj"):
+        np.testing.assert_array_equal(res["split"][k], res["one"][k])
+    assert (res["one"]["sel"] >= 0).all()
 
 
 def test_edge_cases():

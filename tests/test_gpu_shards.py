@@ -111,7 +111,7 @@ def test_rank_shard_of_8gpu_swarm_vs_oracle(config, rank):
     np.testing.assert_allclose(out["x_qp"][smp][:, :6 * N], np.array([r["x_qp"] for r in ref])[:, :6 * N], atol=1e-6)
     # 3. properties on every agent of the shard
     st = out["status"]
-    assert (st[:, 0] == 0).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
+    assert (st[:, 0] == srbnmpc.QP_WARM).all() and np.isin(st[:, 1], [0, srbnmpc.ACCEPTABLE]).all()
     p = srbnmpc.default_params(N, C)
     x = out["x"]
     Ad, Bd = oracle.lip(oracle.params(N, C))
@@ -168,12 +168,16 @@ full = torch.randn(1000, 4, dtype=torch.float64, device="cuda")
 ex3 = sd.NeighbourExchange(1000, 3, 1, x.device)
 assert ex3.flat and not ex3.equal and ex3.counts == [333, 333, 334]
 lo, hi = sd.shard_range(1000, 3, 1)
-def fake_all_gather(recv, send):
+class _Done:
+    def wait(self):
+        return True
+def fake_all_gather(recv, send, async_op=False):
     v = recv.view(3, ex3.cmax, 4)
     v.zero_()
     for r in range(3):
         a, b = sd.shard_range(1000, 3, r)
         v[r, :b - a] = send[:b - a] if r == 1 else full[a:b]
+    return _Done() if async_op else None
 real = dist.all_gather_into_tensor
 dist.all_gather_into_tensor = fake_all_gather
 try:
@@ -182,6 +186,18 @@ finally:
     dist.all_gather_into_tensor = real
 torch.cuda.synchronize()
 assert torch.equal(tab, full), (tab - full).abs().max()
+# the split form bench.py's multi-GPU step uses: start() issues the RCCL all-gather asynchronously, the
+# compute stream runs work that needs no neighbour row (the static selection; here a kernel writing y),
+# wait() orders the compute stream after the collective without blocking the host
+y = torch.zeros(1 << 20, dtype=torch.float64, device="cuda")
+for cycle in range(3):
+    pend = ex.start(x + 10 * cycle)
+    y.add_(1.0)
+    tab1 = pend.wait()
+    assert tab1.data_ptr() == ex.out.data_ptr()
+    z = tab1 * 2.0                                       # consumer on the compute stream, after the wait
+    torch.cuda.synchronize()
+    assert torch.equal(z, 2.0 * (x + 10 * cycle)) and float(y[0]) == cycle + 1.0
 dist.destroy_process_group()
 print("rccl ok")
 """

@@ -16,6 +16,14 @@ from srbnmpc import srb12, workload
 N = 10
 
 
+
+def _opt(st):
+    """Rows whose stages all converged: the QP stage OPTIMAL, or -- when the NLP follows it -- stopped at its
+    warm-start tolerance tol_qp (status 4: that point is only the NLP's warm start, never reported OPTIMAL),
+    and the NLP stage OPTIMAL."""
+    st = np.asarray(st)
+    return np.isin(st[:, 0], (0, 4)) & (st[:, 1] == 0)
+
 def _batch(A, gait, seed, Kn=8):
     b = workload.make_batch12(A, N, gait, seed=seed)
     p = oracle.params12(N, K_obs=3, K_nbr=Kn)
@@ -114,7 +122,7 @@ def test_srb12_oracle_kkt_certificate(gait):
     own multipliers, bounded least squares; no solver trusted)."""
     b, p = _batch(8, gait, 11)
     r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
-    assert (r["status"] == 0).all(), r["status"]
+    assert _opt(r["status"]).all(), r["status"]
     for a in range(8):
         obs, eps = _obs_for(p, b, a)
         Pd, c, Aeq, beq, gJ, hh = _problem(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a], obs, eps)
@@ -157,7 +165,7 @@ def test_srb12_oracle_forces_within_1e4_of_certified_optimum(gait, A, Nh):
     r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     rej, acc = st[0], st[1]
     t = _tight(p, b)
-    ok = (t["status"] == 0).all(1) & (r["status"] == 0).all(1)
+    ok = _opt(t["status"]) & _opt(r["status"])
     assert ok.mean() >= 0.95
     U, Ut = r["x"][ok, 12 * Nh:24 * Nh], t["x"][ok, 12 * Nh:24 * Nh]
     assert np.abs(U - Ut).max() < 1e-4, np.abs(U - Ut).max()
@@ -225,7 +233,7 @@ def test_srb12_oracle_polish_equals_independent_exact_optimum(gait):
     p = oracle.params12(N, K_obs=3, K_nbr=8)
     r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     t = _tight(p, b)
-    assert (r["status"] == 0).all()
+    assert _opt(r["status"]).all()
     for a in range(A):
         xe = _exact_active_set_optimum(p, b, a, t["x"][a])
         # (the reference is exact, or the tight run's own point when that certifies: then within 1e-7 N)
@@ -282,7 +290,7 @@ def test_srb12_gpu_vs_oracle(gait):
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     s.close()
     r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
-    assert (r["status"] == 0).all()
+    assert _opt(r["status"]).all()
     assert (out["status"] == r["status"]).all(), [(a, out["status"][a].tolist(), r["status"][a].tolist())
                                                    for a in range(A) if (out["status"][a] != r["status"][a]).any()]
     same_it = (out["iters"] == r["iters"]).all(1).mean()
@@ -294,7 +302,7 @@ def test_srb12_gpu_vs_oracle(gait):
     # tight optimum (both polished to the exact KKT point of their active sets)
     assert ex < 1e-6 and eu < 1e-4 and es < 1e-6, (ex, eu, es)
     t = _tight(p, b)
-    ok = (t["status"] == 0).all(1)
+    ok = _opt(t["status"])
     assert ok.mean() >= 0.95
     eut = np.abs(U[ok] - t["x"][ok, 12 * N:24 * N]).max()
     assert eut < 1e-4, eut
@@ -341,10 +349,10 @@ def test_srb12_full_size_properties():
     s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     s.close()
-    assert (out["status"] == 0).all(1).mean() >= 0.99, np.bincount(out["status"][:, 1])
+    assert _opt(out["status"]).mean() >= 0.99, np.bincount(out["status"][:, 1])
     X, U, sl = srb12.split(p, out["x"])
     mus = p.mu / np.sqrt(2)
-    ok = (out["status"] == 0).all(1)
+    ok = _opt(out["status"])
     for a in np.where(ok)[0][:256]:
         Am, Bm, cm = oracle.dynamics12(p, b["x0"][a], b["xref"][a], b["foot"][a], b["contact"][a])
         prev = b["x0"][a]
@@ -389,7 +397,7 @@ def test_srb12_variants_vs_oracle(Nh, Ko, Kn, use_nlp):
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     s.close()
     r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
-    assert (r["status"] == 0).all() and (out["status"] == r["status"]).all()
+    assert _opt(r["status"]).all() and (out["status"] == r["status"]).all()
     np.testing.assert_allclose(out["x"][:, :12 * Nh], r["x"][:, :12 * Nh], atol=1e-6)
     np.testing.assert_allclose(out["x"][:, 12 * Nh:], r["x"][:, 12 * Nh:], atol=1e-4)      # forces: 1e-4 N
 
@@ -437,11 +445,11 @@ def test_srb12_gpu_forces_within_1e4_of_exact_optimum_1024(gait):
     s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     s.close()
-    opt = (out["status"] == 0).all(1)
+    opt = _opt(out["status"])
     assert np.isin(out["status"][:, 1], (0, 4)).all() and opt.mean() >= 0.995, np.bincount(out["status"][:, 1])
     U = out["x"][:, 12 * N:24 * N]
     t = _tight(p, b)
-    tok = (t["status"] == 0).all(1)
+    tok = _opt(t["status"])
     assert tok.mean() >= 0.97
     e = np.abs(U - t["x"][:, 12 * N:24 * N]).max(1)
     assert e[opt & tok].max() < 1e-4, (np.argmax(np.where(opt & tok, e, 0)), e[opt & tok].max())
