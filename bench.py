@@ -487,6 +487,10 @@ def main():
     ap.add_argument("--waves", type=int, default=0, help="waves per agent (0 automatic; srb_ctx_set_waves)")
     ap.add_argument("--qp-init", type=int, default=1,
                     help="QP-stage start: 1 scaled (default), 0 iSWIFT's kkt_initialize (srb_ctx_set_qp_init)")
+    ap.add_argument("--kkt-fp32-mu", type=float, default=0.0,
+                    help="SRB_OPT_KKT_FP32_MU: invert the reduced Newton matrix in fp32 while mu > this, refined in fp64 "
+                         "(BASELINE configs[4] 'fp32 KKT with fp64 iterative-refine residuals'); 0 = fp64 throughout")
+    ap.add_argument("--kkt-fp32-refine", type=int, default=3, help="SRB_OPT_KKT_FP32_REFINE")
     ap.add_argument("--qp-warm-tol", type=float, default=None,
                     help="diagnostics: the QP stage's tolerance before the NLP (SRB_OPT_QP_WARM_TOL; default: the library's)")
     ap.add_argument("--polish-fused", type=int, default=1,
@@ -556,6 +560,9 @@ def main():
     solver.set_option("polish_fused", args.polish_fused)
     if args.qp_warm_tol is not None:
         solver.set_option("qp_warm_tol", args.qp_warm_tol)
+    if args.kkt_fp32_mu > 0:
+        solver.set_option("kkt_fp32_mu", args.kkt_fp32_mu)
+        solver.set_option("kkt_fp32_refine", args.kkt_fp32_refine)
     # one explicit stream for the collective, both kernels and the timing events (the C ABI
     # launches on the stream it is handed; the null stream would not order against it)
     stream = torch.cuda.Stream(dev)
@@ -640,10 +647,13 @@ def main():
                 traffic_polish = tj.get("kernels", {}).get("srb_polish_kernel", {}).get("hbm_bytes")
         except Exception:
             traffic = None
+    kkt32 = args.kkt_fp32_mu > 0 and solver.get_option("last_kkt_fp32") == 1.0
     line = {
         "metric": METRIC, "value": value, "unit": "solves/s", "n_gpus": world, "steps": args.steps,
         "warmup": args.warmup, "ms_per_step": ms_per_step, "higher_is_better": True, "scaling": "weak",
-        "vs_baseline": None, "dtype": "f64", "data": "synthetic",
+        "vs_baseline": None,
+        "dtype": ("f64 (reduced Newton matrix inverted in fp32 while mu > %g, %d fp64 refinement steps per solve)"
+                  % (args.kkt_fp32_mu, args.kkt_fp32_refine)) if kkt32 else "f64", "data": "synthetic",
         "config": {"workload": cfg["name"], "agents_per_gpu": A_local, "agents_total": A_total, "horizon": N,
                    "contacts": C, "K_obs": cfg["K_obs"], "K_nbr": cfg["K_nbr"], "parallelism": f"agents sharded x{world}",
                    "emulated_shards": args.emulate_shards, "n_obs": int(sh["obstacles"].shape[0]),

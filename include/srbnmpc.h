@@ -163,7 +163,14 @@ int srb_ctx_waves(srb_ctx *ctx);
  *                                0; with 0 here it reports iSWIFT's codes (0 OPTIMAL at 1e-6)
  *   SRB_OPT_SELECTION            1 (default): srb_solve_batch_device runs the obstacle / neighbour selection
  *                                itself; 0: the caller has filled batch.sel with srb_select_device (the two
- *                                tables may then be selected on either side of the neighbour all-gather) */
+ *                                tables may then be selected on either side of the neighbour all-gather)
+ *   SRB_OPT_KKT_FP32_MU          0 (default): the reduced Newton matrix is inverted in fp64.  > 0: BASELINE
+ *                                configs[4]'s "fp32 KKT with fp64 iterative-refine residuals" -- where the
+ *                                instance has an fp32-factor variant (the configs[2] and config-5 shapes), the
+ *                                matrix (assembled in fp64) is inverted in fp32 while the complementarity mu is
+ *                                above this value, each solve then refined SRB_OPT_KKT_FP32_REFINE times (default
+ *                                3) against the fp64 matrix; fp64 below it
+ *   SRB_OPT_LAST_KKT_FP32        read only: 1 if the last launch ran an fp32-factor instance */
 #define SRB_OPT_POLISH 1
 #define SRB_OPT_POLISH_RHO 2
 #define SRB_OPT_POLISH_WAVES 3
@@ -174,6 +181,9 @@ int srb_ctx_waves(srb_ctx *ctx);
 #define SRB_OPT_TIMING 8
 #define SRB_OPT_QP_WARM_TOL 9
 #define SRB_OPT_SELECTION 10
+#define SRB_OPT_KKT_FP32_MU 11
+#define SRB_OPT_KKT_FP32_REFINE 12
+#define SRB_OPT_LAST_KKT_FP32 13
 int srb_ctx_set_option(srb_ctx *ctx, int opt, double value);
 int srb_ctx_get_option(srb_ctx *ctx, int opt, double *value);
 

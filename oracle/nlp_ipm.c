@@ -155,9 +155,11 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #define ORC_POLISH_PTOL 1e-9      /* primal: g_i(x) - h_i <= this on every row, |c_A| <= this on active rows */
 #define ORC_POLISH_DXTOL 1e-7     /* the last Newton correction |dx|_inf <= this (converged) */
 #define ORC_POLISH_EQTOL 1e-8     /* the equality rows hold to this at an accepted point (kernel SRB_POLISH_EQTOL) */
-#define ORC_POLISH_STOL 1e-7      /* ... and the reduced stationarity |Z'(grad f + J_A' z_A)|_inf <= this max(1, |grad f|_inf)
-                                     (kernel SRB_POLISH_STOL; round 6: 2.2e-9 at most on the accepted polishes of six
-                                     bench workloads -- the guard is against a point that is feasible but not stationary) */
+#define ORC_POLISH_STOL 1e-6      /* ... and the Newton correction the reduced stationarity residual g = Z'(grad f + J_A' z_A)
+                                     implies, |M^-1 g|_inf with M the last step's reduced matrix, is <= this (kernel
+                                     SRB_POLISH_STOL): the distance to the stationary point, whatever the gradient's
+                                     scale -- a guard against a point that is feasible but not stationary;
+                                     round 6: at most 6e-8 on the accepted polishes of six bench workloads */
 #define ORC_POLISH_OMCAP 1e-2     /* inactive rows: Hessian weight min(z/s, this), a proximal term */
 #define ORC_POLISH_DX1 1e-4       /* a Newton step this small whose active rows then hold to CTOL ends the pass */
 #define ORC_POLISH_CTOL 1e-10
@@ -281,7 +283,26 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
         for (int a = 0; a < nz; a++) {
             double acc = 0; for (int j = 0; j < n; j++) acc += Z[(size_t)j * nz + a] * v[j];
             gz = fmax(gz, fabs(acc)); res = fmax(res, fabs(gr[a] + acc));
+            gr[a] += acc;
         }
+        /* the Newton correction that residual implies, with the last step's factor (Hr: Cholesky of the reduced
+         * matrix; the kernel uses its inverse of the same matrix) */
+        orc_chol_solve(nz, Hr, gr);
+        double sdx = 0.0;
+        for (int a = 0; a < nz; a++) sdx = fmax(sdx, fabs(gr[a]));
+        /* ... and the multipliers that step leaves, z_A + rho (c_A + J_A Z dxi) with dxi = -M^-1 g, keep their sign
+         * (kernel polish_stationary: the same test) */
+        for (int j = 0; j < n; j++) { double acc = 0; for (int a = 0; a < nz; a++) acc += Z[(size_t)j * nz + a] * gr[a]; v[j] = -acc; }
+        double zn_min = 1e300, zn_max = 1.0;
+        for (int r = 0; r < m; r++) {
+            if (!act[r]) continue;
+            double jd = 0;
+            for (int t = 0; t < 4; t++) if (Ji[4 * r + t] >= 0) jd += Jv[4 * r + t] * v[Ji[4 * r + t]];
+            const double zn = za[r] + g_polish_rho * ((g[r] - hh[r]) + jd);
+            zn_min = fmin(zn_min, zn); zn_max = fmax(zn_max, fabs(zn));
+        }
+        /* (rho |c_A| <= rho PTOL = 1 is the resolution of that update: the tolerance) */
+        if (!(zn_min >= -(g_polish_rho * ORC_POLISH_PTOL + 1e-9 * zn_max))) sdx = 1e300;
         const int dual_ok = nact == 0 || zmin >= -1e-9 * zm;
         /* the equality rows (LIP dynamics, CoP, sum lambda; dec_vars_constr_cost.h:154-206) at the
          * polished point: the kernel's SRB_POLISH_EQTOL test (the LU step keeps them to round-off) */
@@ -292,7 +313,7 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
          * multipliers: a point that is feasible, converged and dual feasible but not stationary -- what the
          * round-5 generic-pointer build returned as OPTIMAL -- is rejected (kernel, same rule) */
         ok = pv <= ORC_POLISH_PTOL && cv <= ORC_POLISH_PTOL && dual_ok && lastdx <= ORC_POLISH_DXTOL && eqr <= ORC_POLISH_EQTOL &&
-             res <= ORC_POLISH_STOL * fmax(1.0, gmax);
+             sdx <= ORC_POLISH_STOL;
         if (trace)
             fprintf(stderr, "  polish pass %d: |A| %d  primal %.2e  |c_A| %.2e  zmin %.2e (zmax %.2e)  last dx %.2e  stat %.2e (scale %.2e)  -> %s\n",
                     pass, nact, pv, cv, nact ? zmin : 0.0, zm, lastdx, res, fmax(1.0, gmax), ok ? "accepted" : "rejected");
@@ -302,7 +323,7 @@ static int polish(const nlp_t *P, const double *hh, const double *Z, int nz, dou
                     fprintf(stderr, "    row %3d (%s) act %d  s %.3e z %.3e  za %.4e  g-h %.3e\n", r,
                             r < P->mq ? "lin" : r < P->mq + P->mo ? "obs" : "vel", act[r], s[r], z[r], za[r], g[r] - hh[r]);
         {
-            const double sr = res / fmax(1.0, gmax);
+            const double sr = sdx;
             unsigned long long bits, *dst = &orc_polish_stat_max[ok ? 0 : 1], cur = __atomic_load_n(dst, __ATOMIC_RELAXED);
             memcpy(&bits, &sr, sizeof bits);
             while (bits > cur && !__atomic_compare_exchange_n(dst, &cur, bits, 0, __ATOMIC_RELAXED, __ATOMIC_RELAXED)) {}

@@ -42,6 +42,13 @@
 #ifndef SRB12_REFINE                  // 0: no iterative refinement at all (A/B builds)
 #define SRB12_REFINE 1
 #endif
+#ifdef SRB12_REFINE2_MU               // diagnostic builds: a second refinement step of the corrector once mu < this
+#ifndef SRB_DIAG_BUILD
+#error "SRB12_REFINE2_MU is a diagnostic-build option"
+#endif
+#else
+#define SRB12_REFINE2_MU 0.0
+#endif
 #ifndef SRB12_REFINE_MU               // the corrector's solve is refined once mu < this
 #define SRB12_REFINE_MU 1e-3
 #endif
@@ -439,10 +446,17 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
 #pragma unroll
                 for (int i = kk + 1; i < 12; i++) col[i] = fma(-readlane_d(col[i], kk), t, col[i]);
                 // 1 / sqrt(piv): v_rsq_f64 and two Newton steps (a failed pivot's value is never used)
+#ifdef SRB12_EXACT_RSQ                // diagnostic builds: the correctly rounded 1 / sqrt
+#ifndef SRB_DIAG_BUILD
+#error "SRB12_EXACT_RSQ is a diagnostic-build option"
+#endif
+                dinv[kk] = 1.0 / sqrt(piv);
+#else
                 double rs = __builtin_amdgcn_rsq(piv);
                 rs = fma(0.5 * rs, fma(-piv * rs, rs, 1.0), rs);
                 rs = fma(0.5 * rs, fma(-piv * rs, rs, 1.0), rs);
                 dinv[kk] = rs;
+#endif
             }
             // (Two pivots a step -- every broadcast of the step reading values from before it, the same fma
             // forms, bit-identical -- measured slower: SRB-12 step 0.756 -> 0.793 ms, round 5.)
@@ -1088,6 +1102,7 @@ __device__ __forceinline__ void srb12_agent(const Srb12KParams &prm, int agent, 
             build_rhs(1, sigma * mu);
             riccati_solve(0, false);
             if (SRB12_REFINE && refn) refine(delta);
+            if (SRB12_REFINE2_MU > 0.0 && mu < SRB12_REFINE2_MU) refine(delta);
             S12ST(6);   // corrector rhs + solve (+ refinement)
             al = row_step(1, sigma * mu, dls, dlz, dos, doz);
             const double ap = fmin(1.0, 0.99 * al.x), ad = fmin(1.0, 0.99 * al.y);

@@ -26,6 +26,14 @@
         const double *alpha_buf, double *alpha_out, const int *sel_g, const float *zpol_g, int zstride);
 SRB_KERNEL_INSTANCES(DECL_NMPC)
 #undef DECL_NMPC
+#define DECL_NMPC_F32(NZL, TS, NW, NC, CC, KC)                                                                \
+    extern "C" __global__ void srb_nmpc_kernel_f32_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                 \
+        SrbKParams prm, int n_agents, const double *x0g, const double *refg, const double *footg,              \
+        const double *obstacles, int n_obs, const double *nbr_state, int n_all, int agent_offset,              \
+        double *x_qp_out, double *x_out, double *obj_out, int *status_out, int *iters_out,                    \
+        const double *alpha_buf, double *alpha_out, const int *sel_g, float *zpol_g, int zstride);
+SRB_KF32_INSTANCES(DECL_NMPC_F32)
+#undef DECL_NMPC_F32
 
 typedef void (*srb_kernel_fn)(SrbKParams, int, const double *, const double *, const double *, const double *, int,
                               const double *, int, int, double *, double *, double *, int *, int *, const double *,
@@ -48,6 +56,17 @@ struct srb_instance { int nzl, ts, nw, nc, cc, kc; srb_kernel_fn fn; srb_polish_
      srb_polish_kernel_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC},
 static const srb_instance g_instances[] = {SRB_KERNEL_INSTANCES(ENTRY_NMPC)};
 #undef ENTRY_NMPC
+// the fp32-factor variant of an instance (SRB_OPT_KKT_FP32_MU > 0), or null
+struct srb_instance_f32 { int nzl, ts, nw, nc, cc, kc; srb_kernel_fn fn; };
+#define ENTRY_F32(NZL, TS, NW, NC, CC, KC) {NZL, TS, NW, NC, CC, KC, srb_nmpc_kernel_f32_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC},
+static const srb_instance_f32 g_instances_f32[] = {SRB_KF32_INSTANCES(ENTRY_F32)};
+#undef ENTRY_F32
+static srb_kernel_fn f32_variant(const srb_instance *in)
+{
+    for (const srb_instance_f32 &v : g_instances_f32)
+        if (v.nzl == in->nzl && v.ts == in->ts && v.nw == in->nw && v.nc == in->nc && v.cc == in->cc && v.kc == in->kc) return v.fn;
+    return nullptr;
+}
 
 // Waves per agent: small batches (up to one agent per CU) spread each agent over the four
 // SIMDs of a CU (NW = 4) for latency; larger batches run one wave per agent so that agents,
@@ -123,8 +142,11 @@ struct srb_ctx {
     int last_polish;               // how the last launch polished: 0 no, 1 polish kernel, 2 fused
     int timing;                    // 1: HIP events around the kernels (srb_last_kernel_ms); 0: none
     int selection;                 // SRB_OPT_SELECTION: 1 the solve launches the selection, 0 the caller did
+    int last_f32;                  // the last launch ran an fp32-factor instance (SRB_OPT_LAST_KKT_FP32, read only)
     double polish_rho;
     double qp_warm_tol;            // SRB_OPT_QP_WARM_TOL
+    double kkt32_mu;               // SRB_OPT_KKT_FP32_MU: fp32 factor while mu > this (0: off, the fp64 instances)
+    int kkt32_ref;                 // SRB_OPT_KKT_FP32_REFINE: fp64 refinement steps per solve with the fp32 factor
     float *zpol;                   // [max_agents][zstride] NLP active set / multipliers for the polish kernel
     int zstride;
     float polish_ms;
@@ -314,6 +336,7 @@ extern "C" int srb_ctx_create(const srb_params *p, int max_agents, int device, s
     c->last = nullptr; c->any = false;
     c->qp_init = 1; c->polish_ms = 0.0f;
     c->polish = SRB_POLISH_ON; c->polish_rho = SRB_POLISH_RHO; c->qp_warm_tol = SRB_QP_WARM_TOL; c->polish_waves = 0; c->polish_fused = 1; c->last_polish = 0; c->timing = 1; c->selection = 1;
+    c->kkt32_mu = 0.0; c->kkt32_ref = 3;
     c->grid_min_rows = SRB_GRID_MIN_ROWS; c->grid_min_rows_static = SRB_GRID_MIN_ROWS_STATIC;
     c->zstride = 2 * srb_r4(srb_slots(p->N, p->C, p->K_obs + p->K_nbr));
     const int N = p->N, C = p->C, nv = srb_nv(p);
@@ -423,6 +446,8 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     k.qp_init = c->qp_init;
     k.polish_rho = c->polish_rho;
     k.qp_warm_tol = c->qp_warm_tol;
+    k.kkt32_mu = c->kkt32_mu;
+    k.kkt32_ref = c->kkt32_ref;
     // "up to K nearest": clamp to what exists (batch-uniform), so no row is ever a dummy
     if (k.K_obs > d->n_obs) k.K_obs = d->n_obs > 0 ? d->n_obs : 0;
     const int others = d->nbr_state ? d->n_all - 1 : 0;
@@ -453,7 +478,14 @@ static int launch(srb_ctx *c, int n_agents, const srb_batch *d, hipStream_t s, i
     const bool polish = use_nlp && c->polish && !fused;
     k.polish_fused = fused ? 1 : 0;
     c->last_polish = fused ? 2 : polish ? 1 : 0;
-    hipLaunchKernelGGL(in->fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
+    // SRB_OPT_KKT_FP32_MU > 0: the instance's fp32-factor variant where one is compiled (else the fp64 one)
+    srb_kernel_fn fn = in->fn;
+    c->last_f32 = 0;
+    if (c->kkt32_mu > 0.0) {
+        srb_kernel_fn f = f32_variant(in);
+        if (f) { fn = f; c->last_f32 = 1; }
+    }
+    hipLaunchKernelGGL(fn, dim3(n_agents), dim3(64 * in->nw), lds, s, k, n_agents, d->x0, d->ref, d->foot, d->obstacles,
                        n_obs, d->nbr_state, n_all, d->agent_offset, d->x_qp, d->x, d->obj, d->status, d->iters,
                        d->alpha ? d->alpha_buf : nullptr, d->alpha_buf ? d->alpha : nullptr, (const int *)sel,
                        polish ? c->zpol : nullptr, c->zstride);
@@ -516,6 +548,14 @@ extern "C" int srb_ctx_set_option(srb_ctx *c, int opt, double v)
     case SRB_OPT_SELECTION:
         if (v != 0.0 && v != 1.0) return fail(SRB_ERR_ARG, "SRB_OPT_SELECTION: 0 or 1");
         c->selection = (int)v; return SRB_OK;
+    case SRB_OPT_KKT_FP32_MU:
+        if (!(v >= 0.0 && v <= 1e30)) return fail(SRB_ERR_ARG, "SRB_OPT_KKT_FP32_MU: 0 (off) .. 1e30");
+        c->kkt32_mu = v; return SRB_OK;
+    case SRB_OPT_KKT_FP32_REFINE:
+        if (!whole || v < 1.0 || v > 8.0) return fail(SRB_ERR_ARG, "SRB_OPT_KKT_FP32_REFINE: 1 .. 8");
+        c->kkt32_ref = (int)v; return SRB_OK;
+    case SRB_OPT_LAST_KKT_FP32:
+        return fail(SRB_ERR_ARG, "SRB_OPT_LAST_KKT_FP32 is read only");
     case SRB_OPT_GRID_MIN_ROWS:
     case SRB_OPT_GRID_MIN_ROWS_STATIC:
         if (!whole || v < 1.0 || v > 2147483647.0) return fail(SRB_ERR_ARG, "SRB_OPT_GRID_MIN_ROWS*: a row count >= 1");
@@ -540,6 +580,9 @@ extern "C" int srb_ctx_get_option(srb_ctx *c, int opt, double *v)
     case SRB_OPT_TIMING: *v = c->timing; return SRB_OK;
     case SRB_OPT_QP_WARM_TOL: *v = c->qp_warm_tol; return SRB_OK;
     case SRB_OPT_SELECTION: *v = c->selection; return SRB_OK;
+    case SRB_OPT_KKT_FP32_MU: *v = c->kkt32_mu; return SRB_OK;
+    case SRB_OPT_KKT_FP32_REFINE: *v = c->kkt32_ref; return SRB_OK;
+    case SRB_OPT_LAST_KKT_FP32: *v = c->last_f32; return SRB_OK;
     default: return fail(SRB_ERR_ARG, "unknown option");
     }
 }

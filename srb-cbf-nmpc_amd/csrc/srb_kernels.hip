@@ -79,7 +79,7 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 #define STAMP_DECL unsigned long long st_t0 = 0; int st_off = 0
 #define STAMP_BEGIN() do { __builtin_amdgcn_sched_barrier(0); st_t0 = __builtin_amdgcn_s_memtime(); __builtin_amdgcn_sched_barrier(0); } while (0)
 #define STAMP_END(slot) do { __builtin_amdgcn_sched_barrier(0); const unsigned long long _t = __builtin_amdgcn_s_memtime(); \
-    __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0) atomicAdd(&stamp_lds[st_off + (slot)], _t - st_t0); st_t0 = _t; } while (0)
+    __builtin_amdgcn_sched_barrier(0); if (threadIdx.x == 0 && stamp_lds) atomicAdd(&stamp_lds[st_off + (slot)], _t - st_t0); st_t0 = _t; } while (0)
 #define STAMP_STAGE(s) (st_off = 32 * (s))
 #define STAMP_FLUSH(agent) do { SYNC(); if ((agent) == 0 && threadIdx.x < 64) atomicAdd(&srb_stamp_buf[threadIdx.x], stamp_lds[threadIdx.x]); } while (0)
 #else
@@ -88,6 +88,45 @@ __device__ unsigned long long srb_stamp_buf[SRB_NSTAMP];
 #define STAMP_END(slot) do {} while (0)
 #define STAMP_STAGE(s) do {} while (0)
 #define STAMP_FLUSH(agent) do {} while (0)
+#endif
+
+// --------------------------------------------------------------------------- fp32 storage (diagnostic)
+// Built only with -DSRB_DIAG_ROUND32 (make lipvar TAG=r32): every term row and every entry of the
+// assembled reduced matrix rounded to fp32 where it is stored -- the arithmetic effect of storing them in fp32 with
+// fp64 accumulation and the fp64 refinement (which then refines against the rounded matrix).  The LDS it would save
+// buys no occupancy (config 5 is register-bound at two agents per CU), so only the accuracy is measured.
+#ifdef SRB_DIAG_ROUND32
+#ifndef SRB_DIAG_BUILD
+#error "SRB_DIAG_ROUND32 is a diagnostic-build option"
+#endif
+#define R32(v) ((double)(float)(v))
+#else
+#define R32(v) (v)
+#endif
+
+// --------------------------------------------------------------------------- LDS bounds (diagnostic)
+// Built only with -DSRB_DIAG_LDS_CHECK (make fullvar TAG=ldsck VARFLAGS=-DSRB_DIAG_LDS_CHECK):
+// the indices a slot derives its LDS accesses from -- its term row, weight entry, iterate entries, obstacle and
+// dual entries, exported active-set entry --, the term-row ranges of the Gram, and the carve's end against the
+// size the host allocated (srb_lds_doubles) are checked, each failed check setting one bit of a workgroup
+// flag; a flagged agent reports QP status 1000 + flag (never a fault: the kernel goes on).  Round 5's fold
+// build read obstacle term rows past the end of R with four waves -- bit 1 here.
+#ifdef SRB_DIAG_LDS_CHECK
+#ifndef SRB_DIAG_BUILD
+#error "SRB_DIAG_LDS_CHECK is a diagnostic-build option"
+#endif
+__device__ __forceinline__ int *lds_oob_flag()
+{
+    __shared__ int f;
+    return &f;
+}
+#define LCK(ok, bit) do { if (!(ok)) __hip_atomic_fetch_or(lds_oob_flag(), 1 << (bit), __ATOMIC_RELAXED, __HIP_MEMORY_SCOPE_WORKGROUP); } while (0)
+#define LCK_INIT() do { if (threadIdx.x == 0) *lds_oob_flag() = 0; } while (0)
+#define LCK_REPORT(slot) do { SYNC(); if (tid == 0 && *lds_oob_flag()) status_out[(slot)] = 1000 + *lds_oob_flag(); } while (0)
+#else
+#define LCK(ok, bit) do {} while (0)
+#define LCK_INIT() do {} while (0)
+#define LCK_REPORT(slot) do {} while (0)
 #endif
 
 // --------------------------------------------------------------------------- diagnostic trace
@@ -159,12 +198,12 @@ __device__ __forceinline__ void ul_add(const double *R, const double *W, const d
     const int c1 = F.C - 1, np = F.N * c1 * c1, rl = F.rU + 2 * F.N, rs = F.rU + F.n - 1 - 4 * F.N;
     if (GRAM) {
         for (int e = tid0; e <= np; e += step) {
-            if (e == np) { H[0] += W[rs]; continue; }             // slack row: Z = e_0
+            if (e == np) { H[0] = R32(H[0] + W[rs]); continue; }  // slack row: Z = e_0
             const int j = e / (c1 * c1), rem = e - j * c1 * c1, a = 1 + j * c1 + rem / c1, b = 1 + j * c1 + rem % c1;
             double v = 0.0;
             for (int d = 0; d < 2; d++) { const int r = F.rU + 2 * j + d; v = fma(W[r] * R[r * LDR + a], R[r * LDR + b], v); }
             for (int i = 0; i < F.C; i++) { const int r = rl + F.C * j + i; v = fma(W[r] * R[r * LDR + a], R[r * LDR + b], v); }
-            H[a * LDH + b] += v;
+            H[a * LDH + b] = R32(H[a * LDH + b] + v);
         }
     }
     if (RHS) {
@@ -401,7 +440,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
         // wave 0 stores its tiles; with two waves, wave 1 then adds its own in place (a fixed
         // order: bit-reproducible, and no partial-Gram scratch in LDS)
         auto put = [&](int i, int j, double v, bool add) {
-            if (i < NZL && j < NZL) H[i * LDH + j] = add ? H[i * LDH + j] + v : v;
+            if (i < NZL && j < NZL) H[i * LDH + j] = R32(add ? H[i * LDH + j] + v : v);
         };
 #pragma unroll
         for (int ph = 0; ph < NW; ph++) {
@@ -441,6 +480,7 @@ __device__ __forceinline__ void gram_rhs(const double *R, const double *W, const
 #pragma unroll
             for (int w2 = 0; w2 < NW; w2++) v += part[((w2 * NT + t) * 4 + q) * 64 + ln];
             const int r = (ln >> 4) + 4 * q, cl = ln & 15;
+            v = R32(v);
             if (t == 0) { if (r < NZL && cl < NZL) H[r * LDH + cl] = v; }
             else if (t == 1) { if (16 + cl < NZL) { H[r * LDH + 16 + cl] = v; H[(16 + cl) * LDH + r] = v; } }
             else if (16 + r < NZL && 16 + cl < NZL) H[(16 + r) * LDH + 16 + cl] = v;
@@ -608,7 +648,7 @@ __device__ __forceinline__ void obs_relin(double *R, double *OJ, int rO, int o, 
         double *dst = R + (rO + o) * LDR;
         const double *zx = R + i0 * LDR, *zy = R + i1 * LDR;
 #pragma unroll
-        for (int a = 0; a < NZL; a++) dst[a] = fma(jx, zx[a], fma(jy, zy[a], (a == 0) ? -1.0 : 0.0));
+        for (int a = 0; a < NZL; a++) dst[a] = R32(fma(jx, zx[a], fma(jy, zy[a], (a == 0) ? -1.0 : 0.0)));
     } else {
         OJ[2 * o] = jx; OJ[2 * o + 1] = jy;
     }
@@ -671,9 +711,12 @@ __device__ __forceinline__ int gj_reduced(double (&A)[NZL], int nz, int lane, in
 // (y = M g; y += M (g - Hs y)): the explicit inverse alone is not backward stable, and near
 // the end of an interior-point solve Hs carries barrier weights of 1e8..1e12.
 // g, y, r, out: LDS vectors (zero beyond nz).  Returns out in registers (uniform).
-template <int NZL, int NW, int NZE = NZL>
+// KF (the fp32-factor instances, configs[4] "fp32 KKT with fp64 iterative-refine residuals"): `nref` steps of
+// refinement instead of SRB_REFINE, run-time (more while M is the fp32 inverse); the product instances (KF = 0)
+// keep the compile-time count and are unchanged.
+template <int NZL, int NW, int NZE = NZL, int KF = 0>
 __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *Hs, const double *Zs, double dl, const double *g,
-                                         double *y, double *r, double *out, double (&res)[NZL], int nz, int lane)
+                                         double *y, double *r, double *out, double (&res)[NZL], int nz, int lane, int nref = SRB_REFINE)
 {
     constexpr int LDH = NZL + 1;
     if constexpr (NZL <= 16 && SRB_USE_DPP) {
@@ -687,8 +730,10 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
         // SRB_REFINE steps of iterative refinement with fp64 residuals (1 in the product build;
         // the fp32-factor diagnostic build uses more)
         double y1 = y0;
+        const int nr = KF ? nref : SRB_REFINE;
 #pragma unroll
-        for (int it = 0; it < SRB_REFINE; it++) {
+        for (int it = 0; it < (KF ? 8 : SRB_REFINE); it++) {
+            if (KF && it >= nr) break;
             double rr = gi;
             if (dl != 0.0) {                 // the NLP's inertia shift, applied on the fly (H stays unshifted)
 #pragma unroll
@@ -713,7 +758,8 @@ __device__ __forceinline__ void la_solve(const double (&M)[NZL], const double *H
 #pragma unroll
     for (int j = 0; j < NZE; j++) y0 = fma(M[j], gv[j], y0);
     double y1 = y0;
-    for (int it = 0; it < SRB_REFINE; it++) {
+    const int nr = KF ? nref : SRB_REFINE;
+    for (int it = 0; it < nr; it++) {
         if (it > 0) SYNC();                      // every lane has read the previous r
         if (lane < nz) y[lane] = y1;
         SYNC();
@@ -876,6 +922,15 @@ __device__ __forceinline__ void slot_stage(Slot &q, int n, bool nl, int TT)
     q.wr = (q.kind == K_VAR || q.kind == K_COP || q.kind == K_OBS) ? q.r : TT;
 }
 
+// LDS-bounds diagnostic build: the indices slot q (slot number sl) reads and writes through (LCK above)
+#define SRB_SLOT_LCK(q, sl) do { \
+    LCK((q).wr <= TT, 2); \
+    LCK((q).kind == K_NONE || ((q).i0 >= 0 && (q).i0 < n && (q).i1 >= 0 && (q).i1 < n), 3); \
+    LCK(!((q).kind == K_VAR || (q).kind == K_COP || (q).kind == K_VEL || ((q).kind == K_OBS && SRB_OBS_STORED(NZL))) || \
+        ((q).r >= 0 && (q).r < RROWS), 1); \
+    LCK((q).kind != K_OBS || ((sl) - sO >= 0 && (sl) - sO < NK && (q).r - rO == (sl) - sO), 5); \
+} while (0)
+
 // cost weight of variable v (Q_qp diagonal, MPC_dist.cpp:168-178)
 __device__ __forceinline__ double var_weight(const SrbKParams &prm, int v)
 {
@@ -950,19 +1005,26 @@ __device__ __forceinline__ double lip_eq_res(const SrbKParams &prm, const double
 
 // Reduced stationarity of the polished point (round 6): g = Z'(grad f(x) + J_A' z_A), grad f from the problem data
 // (var_weight, the reference window in LDS) rather than the slots' cost registers, z_A the polish's multipliers
-// (ds: active mask, dz: z_A); accepted only where max |g| <= SRB_POLISH_STOL max(1, |grad f|_inf).  The other
+// (ds: active mask, dz: z_A); returns max |M^-1 g| (M: the last Newton step's reduced matrix, Mi its inverse), the
+// correction a further step would make, accepted only up to SRB_POLISH_STOL and only where the multipliers that step
+// leaves keep their sign (else 1e300).  The other
 // tests (feasibility, multiplier signs, converged step, equality rows) held on the points the round-5 generic-
 // pointer build returned as OPTIMAL although they were not stationary; this one does not.  The
 // term rows are those of the last Newton step (the obstacle rows linearised at its start: O(|dx|) <= 1e-7 off).
 // Uniform over the workgroup (every value reduced).  oracle/nlp_ipm.c `polish`: the same test.
-template <int NZL, int TS, int NW>
-__device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, const SrbKParams &prm, const double *xs,
-                                                  const double *ref, double *CF, const double *R, int cnt, const ObsFold &OF,
-                                                  int nko, double *vg, int nz, int tid, double *part, uint64_t bmask,
-                                                  double *red, int N, int n, int TT)
+template <int NZL, int TS, int NW, int NZE>
+__device__ __forceinline__ double polish_stationary(Slot (&Q)[TS], int nts, const SrbKParams &prm, const double *xs,
+                                                  const double *ref, double *CF, double *R, double *OJ, double *zo, int rO,
+                                                  int cnt, const ObsFold &OF, int nko, double *vg, double *vy, double *vr,
+                                                  double *vd, const double (&Mi)[NZL], const double *H0, int nz, int tid,
+                                                  double *part, uint64_t bmask, double *red, int N, int n, int TT, int srow)
 {
     double gmax = 0.0;
-    SYNC();                                              // every lane's reads of CF / vg of the last step are done
+    SYNC();                                              // every lane's reads of R / OJ / CF / vg of the last step are done
+    // the obstacle rows linearised at the polished point itself (the last Newton step, up to 1e-4 when the
+    // active rows then hold to 1e-10, ran on rows taken before it: J'z would be off by 2 |dx| |z| there)
+    polish_rows<NZL, TS, NW>(Q, nts, xs, OJ, zo, n, rO, R, nz);
+    SYNC();
 #pragma unroll
     for (int t = 0; t < TS; t++)
         if (t < nts) {
@@ -987,10 +1049,38 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
     SYNC();
     rhs_only<NZL, NW>(R, CF, cnt, OF, nko, vg, nz, tid, part, bmask);
     SYNC();
-    const int lane = tid & 63;
-    double rv[2] = {gmax, (lane < nz) ? fabs(vg[lane]) : 0.0};
+    // the Newton correction g implies, with the last step's inverse (Mi) and matrix (H0): the distance to the
+    // stationary point in the reduced coordinates, whatever the scale of the gradient (oracle: the same test)
+    double dxs[NZL];
+    la_solve<NZL, NW, NZE>(Mi, H0, H0, 0.0, vg, vy, vr, vd, dxs, nz, tid & 63);
+    double dm = 0.0;
+#pragma unroll
+    for (int j = 0; j < NZL; j++) dm = fmax(dm, fabs(dxs[j]));
+    // ... and the multipliers that step would leave on the active rows, z_A + rho (c_A + J_A Z dxi) with dxi = -dxs
+    // (the polish's own update), must keep their sign: a point stationary only through an active row that
+    // should not be active (the row's multiplier of the wrong sign) is not a KKT point either
+    constexpr int LDR = NZL + 1;
+    double zmin = 1e300, zmax = 1.0;
+#pragma unroll
+    for (int t = 0; t < TS; t++)
+        if (t < nts && (Q[t].ds[0] != 0.0 || Q[t].ds[1] != 0.0)) {
+            const Slot &q = Q[t];
+            const double jd = -((!SRB_OBS_STORED(NZL) && kind_of(q) == K_OBS)
+                ? fma(OJ[2 * (q.r - rO)], row_dot<NZL, NZE>(R + q.i0 * LDR, dxs),
+                      fma(OJ[2 * (q.r - rO) + 1], row_dot<NZL, NZE>(R + q.i1 * LDR, dxs), -row_dot<NZL, NZE>(R + srow * LDR, dxs)))
+                : row_dot<NZL, NZE>(R + q.r * LDR, dxs));
+#pragma unroll
+            for (int r = 0; r < 2; r++)
+                if (q.ds[r] != 0.0) {
+                    const double zn = fma(prm.polish_rho, q.r3[r] + (r ? -jd : jd), q.dz[r]);
+                    zmin = fmin(zmin, zn); zmax = fmax(zmax, fabs(zn));
+                }
+        }
+    double rv[2] = {-zmin, zmax};
     wred_x<2, 3u, NW>(rv, red + 5 * 8 * NW, tid);
-    return rv[1] <= SRB_POLISH_STOL * fmax(1.0, rv[0]);
+    (void)gmax;
+    // (rho |c_A| <= rho SRB_POLISH_PTOL = 1 is the resolution of that update: the tolerance)
+    return (-rv[0] >= -(prm.polish_rho * SRB_POLISH_PTOL + 1e-9 * rv[1])) ? dm : 1e300;
 }
 
 // --------------------------------------------------------------------------- shared agent code
@@ -1049,6 +1139,11 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
     double *red = p; p += (NW > 1) ? 8 * SRB_RED_SITES * NW : 0;   /* cross-wave reduction sites */ \
     double *part = p; p += (NW > 2) ? NW * ((NZM == 16) ? 1 : 3) * 256 + NW * NZM : 0;   /* partial Gram / rhs (NW = 4) */ \
     float *zpl = (float *)p; p += SRB_FUSED_POLISH_OK(NZL) ? rnd4(S) : 0;   /* fused polish: the exported active set (2 floats a slot) */ \
+    const int RROWS = SRB_OBS_STORED(NZL) ? TT : rO;   /* term rows stored in R */ \
+    LCK_INIT(); \
+    LCK((int)(p - lds) <= srb_lds_doubles(prm, NZL, NW) - (SRB_FUSED_POLISH_OK(NZL) ? 0 : 0), 0); \
+    LCK(rU <= RROWS && (!SRB_OBS_STORED(NZL) || rO + NKP <= TT), 4); \
+    (void)RROWS; \
     do {} while (0)
 
 #define SRB_AGENT_SETUP \
@@ -1059,7 +1154,9 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
     for (int i = tid; i < (int)(xs - R) + 2 * n4; i += NTH) R[i] = 0.0; \
     for (int i = tid; i < NK4; i += NTH) zo[i] = 0.0; \
     SYNC(); \
+    STAMP_END(23);                 /* stamps build: inputs loaded, LDS cleared */ \
     if (prm.use_nlp) { SRB_AGENT_OBSTACLES; } \
+    STAMP_END(24);                 /* stamps build: obstacle rows */ \
     /* null-space basis Z and particular point xbar (forward LIP rollout, MPC_dist.cpp:232-261) */ \
     if (tid == 0) { \
         double X[4] = {x0[0], x0[1], x0[2], x0[3]}; \
@@ -1083,13 +1180,13 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
         if (!is_null) \
             _Pragma("unroll") for (int i = 0; i < 4; i++) \
                 if (i < C) { g0 += foot[(j * 2 + 0) * C + i] * lam[i]; g1 += foot[(j * 2 + 1) * C + i] * lam[i]; } \
-        _Pragma("unroll") for (int i = 0; i < 4; i++) if (i < C) R[TL.zr(6 * N + C * j + i) * LDR + col] = lam[i]; \
-        R[TL.zr(4 * N + 2 * j) * LDR + col] = g0; \
-        R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = g1; \
+        _Pragma("unroll") for (int i = 0; i < 4; i++) if (i < C) R[TL.zr(6 * N + C * j + i) * LDR + col] = R32(lam[i]); \
+        R[TL.zr(4 * N + 2 * j) * LDR + col] = R32(g0); \
+        R[TL.zr(4 * N + 2 * j + 1) * LDR + col] = R32(g1); \
         double v[4]; \
         for (int d = 0; d < 4; d++) v[d] = prm.Bd[d * 2] * g0 + prm.Bd[d * 2 + 1] * g1; \
         for (int k = j; k < N; k++) { \
-            for (int d = 0; d < 4; d++) R[(4 * k + d) * LDR + col] = v[d]; \
+            for (int d = 0; d < 4; d++) R[(4 * k + d) * LDR + col] = R32(v[d]); \
             double tt[4]; \
             for (int d = 0; d < 4; d++) tt[d] = prm.Ad[d * 4] * v[0] + prm.Ad[d * 4 + 1] * v[1] + prm.Ad[d * 4 + 2] * v[2] + prm.Ad[d * 4 + 3] * v[3]; \
             for (int d = 0; d < 4; d++) v[d] = tt[d]; \
@@ -1097,10 +1194,11 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
     } \
     if (tid == 0) R[TL.zr(n - 1) * LDR] = 1.0; \
     SYNC(); \
+    STAMP_END(25);                 /* stamps build: null-space basis, xbar */ \
     /* CoM-CoP term rows M_e = Z_p - Z_u (p: CoM of grid i, u: CoP of grid i+1); xs = xbar */ \
     if (tid < NE) { \
         const int i = tid >> 1, d = tid & 1, pp = 4 * i + 2 * d, uu = 4 * N + 2 * (i + 1) + d; \
-        for (int a = 0; a < NZL; a++) Rt[tid * LDR + a] = R[pp * LDR + a] - R[TL.zr(uu) * LDR + a]; \
+        for (int a = 0; a < NZL; a++) Rt[tid * LDR + a] = R32(R[pp * LDR + a] - R[TL.zr(uu) * LDR + a]); \
     } \
     for (int v = tid; v < n; v += NTH) xs[v] = xb[v]; \
     do {} while (0)
@@ -1158,14 +1256,16 @@ __device__ __forceinline__ bool polish_stationary(const Slot (&Q)[TS], int nts, 
     do {} while (0)
 
 // Diagnostic builds only (-DSRB_DIAG_POLISH_OUT, make lipvar): the fused polish's last acceptance test --
-// its equality residual into obj, the tests it met as bits into the QP iteration count (1 primal, 2 active
-// rows, 4 multipliers, 8 last step, 16 equality rows, 32 equality residual not finite, 64 a pass ran)
+// its stationarity ratio (or, where the other tests failed, its equality residual) into obj, the tests it met
+// as bits into the QP iteration count (1 primal, 2 active rows, 4 multipliers, 8 last step, 16 equality rows,
+// 32 equality residual not finite, 64 a pass ran, 128 stationary)
 #ifdef SRB_DIAG_POLISH_OUT
 #ifndef SRB_DIAG_BUILD
 #error "SRB_DIAG_POLISH_OUT is a diagnostic-build option"
 #endif
-#define SRB_POLISH_DIAG() do { dg_eqr = eqr; dg_bits = 64 | (pv <= SRB_POLISH_PTOL) | ((cv <= SRB_POLISH_PTOL) << 1) | \
-    ((nzmin <= 1e-9 * zm) << 2) | ((lastdx <= SRB_POLISH_DXTOL) << 3) | ((eqr <= SRB_POLISH_EQTOL) << 4) | ((!isfinite(eqr)) << 5); } while (0)
+#define SRB_POLISH_DIAG() do { dg_eqr = pcand ? sratio : eqr; dg_bits = 64 | (pv <= SRB_POLISH_PTOL) | ((cv <= SRB_POLISH_PTOL) << 1) | \
+    ((nzmin <= 1e-9 * zm) << 2) | ((lastdx <= SRB_POLISH_DXTOL) << 3) | ((eqr <= SRB_POLISH_EQTOL) << 4) | ((!isfinite(eqr)) << 5) | \
+    ((pcand && sratio <= SRB_POLISH_STOL) << 7); } while (0)
 #else
 #define SRB_POLISH_DIAG() do {} while (0)
 #endif
@@ -1280,10 +1380,12 @@ _Pragma("unroll")                                                               
         }                                                                                                                                     \
         POLDBG(pass, 0, pv); POLDBG(pass, 1, cv); POLDBG(pass, 2, nzmin); POLDBG(pass, 3, zm); POLDBG(pass, 4, vi);                           \
         POLDBG(pass, 5, lastdx); POLDBG(pass, 7, eqr);                                                                                        \
+        const bool pcand = pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&           \
+                           eqr <= SRB_POLISH_EQTOL;                                                                                           \
+        const double sratio = pcand ? polish_stationary<NZL, TS, NW, NZE>(PS, nts, prm, xs, ref, CF, R, OJ, zo, rO, cnt, OF, nko, vg, vy,    \
+                                                              vr, vd, Mi, H0, nz, tid, part, bmask, red, N, n, TT, TL.zr(n - 1)) : 0.0;       \
         SRB_POLISH_DIAG();                                                                                                                    \
-        if (pv <= SRB_POLISH_PTOL && cv <= SRB_POLISH_PTOL && nzmin <= 1e-9 * zm && lastdx <= SRB_POLISH_DXTOL &&                             \
-            eqr <= SRB_POLISH_EQTOL && polish_stationary<NZL, TS, NW>(PS, nts, prm, xs, ref, CF, R, cnt, OF, nko, vg, nz, tid, part,      \
-                                                                      bmask, red, N, n, TT)) {                                                \
+        if (pcand && sratio <= SRB_POLISH_STOL) {                                                                                             \
             POLDBG(pass, 6, 1.0);                                                                                                             \
             accepted = true;                                                                                                                  \
             break;                                                                                                                            \
@@ -1321,7 +1423,7 @@ _Pragma("unroll")                                                               
 // the row slots and the term-row passes are split across the waves and combined through LDS;
 // the reduced-system factorisation and solves run redundantly in every wave (identical data,
 // identical results, no communication).
-template <int NZL, int TS, int NW, int NC, int CC, int KC>
+template <int NZL, int TS, int NW, int NC, int CC, int KC, int KF = 0>
 __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 const double *__restrict__ x0g, const double *__restrict__ refg, const double *__restrict__ footg,
                 const double *__restrict__ obstacles, int n_obs,
@@ -1345,7 +1447,10 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
     // ---- slot constants
     Slot Q[TS];
 #pragma unroll
-    for (int t = 0; t < TS; t++) slot_init(Q[t], tid + NTH * t, prm, TL, ref, sE, sV, sO, S, rC, rO, K, TT);
+    for (int t = 0; t < TS; t++) {
+        slot_init(Q[t], tid + NTH * t, prm, TL, ref, sE, sV, sO, S, rC, rO, K, TT);
+        SRB_SLOT_LCK(Q[t], tid + NTH * t);
+    }
     double Mi[NZL];                                          // inverse of the reduced Newton matrix (row = lane)
     double dxi[NZL];                                         // Newton direction in xi (uniform)
 #pragma unroll
@@ -1491,6 +1596,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     Slot &q = Q[t];
                     if (q.kind == K_OBS) {
                         const int o = tid + NTH * t - sO;
+                        LCK(o >= 0 && o < NK, 5);
                         q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K];
                     }
                     const double f = slot_f(q, xs, s_var);
@@ -1622,6 +1728,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                 nrx = sqrt(rv[0]); nrz = sqrt(rv[1]); sz = rv[2]; gm = rv[3]; dxm = rv[4]; zmx = rv[5];
             }
             const double mu = sz * inv_m;
+            const bool f32 = KF && mu > prm.kkt32_mu;          // KF instances: fp32 factor this iteration
+            (void)f32;
             STAMP_END(3);
             // divergence: a dual beyond SRB_Z_DIV means infeasible rows (converging solves keep their duals
             // below ~1e4; infeasible ones pass 1e10 within a few iterations and then overflow): FATAL at
@@ -1740,7 +1848,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         dstart = 1e-10 * fmax(1.0, wmax(dm));
                     }
                     gj_load<NZL, NZE>(Mi, H0, ZZ, delta, nz, lane);    // H0 + delta Z'Z (the solves shift on the fly too)
-                    const int cf = gj_reduced<NZL, NZE>(Mi, nz, lane, !nl);
+                    // KF instances: the inverse in fp32 while mu > kkt32_mu (then nref fp64 refinement steps per solve)
+                    const int cf = (KF && f32) ? gj_invert_f32<NZL>(Mi, mrow<NZL>(lane), !nl) : gj_reduced<NZL, NZE>(Mi, nz, lane, !nl);
                     if (cf == 0) { ok = 1; break; }
                     delta = (delta == 0.0) ? dstart : delta * 10.0;
                 }
@@ -1761,7 +1870,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     SYNC();
                     STAMP_END(7 + 4 * pass);
                 }
-                la_solve<NZL, NW, NZE>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane);
+                la_solve<NZL, NW, NZE, KF>(Mi, H0, ZZ, delta, vg, vy, vr, vd, dxi, nz, lane, (KF && f32) ? prm.kkt32_ref : SRB_REFINE);
                 STAMP_END(8 + 4 * pass);
                 // J dx per slot; dz = om (J dx - r3); ds = (dsT - s dz) / z; step-length maxima
                 double mxs = 0.0, mxz = 0.0;
@@ -1780,6 +1889,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         Slot &q = Q[t];
                         const int kd = kind_of(q);
                         if constexpr (SRB_OBS_STORED(NZL)) {
+                            LCK(q.r >= 0 && q.r < RROWS, 1);
                             q.jd = row_dot<NZL, NZE>(R + q.r * LDR, dxi);
                         } else if (kd == K_OBS) {                     /* (QP stage: masked rows, 0) */
                             const int o = q.r - rO;
@@ -1920,6 +2030,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             const int sl = tid + NTH * t;
 #pragma unroll
             for (int r = 0; r < 2; r++) {
+                LCK(!(t < nts && sl < S) || 2 * sl + r < 2 * rnd4(S), 6);
                 const double v = (t < nts && sl < S) ? (double)zpl[2 * sl + r] : 0.0;
                 Q[t].ds[r] = (v > 0.0) ? 1.0 : 0.0;
                 Q[t].dz[r] = fmax(v, 0.0);
@@ -1927,12 +2038,21 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
             }
         }
         bool accepted = false;
+#ifdef SRB_DIAG_CORRUPT_COST       // diagnostic builds only: the defect class of the round-5 generic-pointer build --
+#ifndef SRB_DIAG_BUILD             // the polish's cost registers off (here c_v of the X rows by 1 %), its data intact
+#error "SRB_DIAG_CORRUPT_COST is a diagnostic-build option"
+#endif
+#pragma unroll
+        for (int t = 0; t < TS; t++)
+            if (Q[t].kind == K_VAR && Q[t].i0 < 4 * N) Q[t].a1 *= 1.01;
+#endif
         SRB_POLISH_PASSES_LOOP(Q);
         SYNC();
         if (accepted) nlp_flag = 0;
         else
             for (int v = tid; v < n; v += NTH) xs[v] = xsv[v];
         SYNC();
+        STAMP_END(26);                                      // stamps build: the fused polish
     }
 
     // ---- outputs: x, objective (ExCost::GetCost, dec_vars_constr_cost.h:423-438), alpha_COM
@@ -1947,6 +2067,7 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
         obj_out[agent] = dg_eqr; iters_out[2 * agent] = dg_bits;
 #endif
     }
+    LCK_REPORT(2 * agent);
 }
 
 
@@ -1966,6 +2087,9 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                 const int *__restrict__ sel_g, const float *__restrict__ zpol_g, int zstride, double *lds)
 {
     SRB_AGENT_LAYOUT;
+#ifdef SRB_STAMPS
+    unsigned long long *stamp_lds = nullptr;                // (the stamps build times the solve kernel only)
+#endif
     double *Rt = R + rC * LDR;
     (void)xb; (void)dxv; (void)th; (void)tol; (void)wv;
     const int st1 = status_out[2 * agent + 1];
@@ -2012,6 +2136,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             Slot &q = P[t];
             const int sl = tid + NTH * t;
             slot_init(q, sl, prm, TL, ref, sE, sV, sO, S, rC, rO, K, TT);
+            SRB_SLOT_LCK(q, sl);
             slot_stage(q, n, true, TT);
             if (q.kind == K_OBS) { const int o = sl - sO; q.a0 = obs[2 * o]; q.a1 = obs[2 * o + 1]; q.h[0] = -eps[o % K]; }
 #pragma unroll
@@ -2034,6 +2159,7 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
             if (tid == 0) { obj_out[agent] = f; status_out[2 * agent + 1] = 0; }
         }
     }
+    LCK_REPORT(2 * agent);
 
 }
 
@@ -2069,6 +2195,27 @@ __device__ __forceinline__ void polish_agent(const SrbKParams &prm, int agent,
                                   status_out, alpha_buf, alpha_out, sel_g, zpol_g, zstride, lds);             \
     }
 
+// fp32-factor instances (KF = 1; SRB_OPT_KKT_FP32_MU > 0 selects them): configs[4]'s "fp32 KKT with fp64
+// iterative-refine residuals" -- the reduced Newton matrix assembled and refined against in fp64, inverted in
+// fp32 while the complementarity mu is above prm.kkt32_mu, in fp64 below
+#define SRB_NMPC_KERNEL_F32(NZL, TS, NW, NC, CC, KC)                                                           \
+    extern "C" __global__ void __launch_bounds__(64 * NW) SRB_WPE                                              \
+    srb_nmpc_kernel_f32_##NZL##_##TS##_##NW##_##NC##_##CC##_##KC(                                             \
+        SrbKParams prm, int n_agents, const double *__restrict__ x0g, const double *__restrict__ refg,          \
+        const double *__restrict__ footg, const double *__restrict__ obstacles, int n_obs,                       \
+        const double *__restrict__ nbr_state, int n_all, int agent_offset, double *__restrict__ x_qp_out,        \
+        double *__restrict__ x_out, double *__restrict__ obj_out, int *__restrict__ status_out,                 \
+        int *__restrict__ iters_out, const double *__restrict__ alpha_buf, double *__restrict__ alpha_out,       \
+        const int *__restrict__ sel_g, float *__restrict__ zpol_g, int zstride)                               \
+    {                                                                                                          \
+        extern __shared__ __attribute__((aligned(16))) double lds[];                                           \
+        const int agent = xcd_agent(blockIdx.x, gridDim.x);                                                   \
+        if (agent >= n_agents) return;                                                                         \
+        nmpc_agent<NZL, TS, NW, NC, CC, KC, 1>(prm, agent, x0g, refg, footg, obstacles, n_obs, nbr_state, n_all, agent_offset, \
+                                x_qp_out, x_out, obj_out, status_out, iters_out, alpha_buf, alpha_out, sel_g, \
+                                zpol_g, zstride, lds);                                                         \
+    }
+
 #if defined(SRB_PART) && !defined(SRB_DEV_INSTANCES)
 #if SRB_PART == 0
 SRB_KI_PART0(SRB_NMPC_KERNEL)
@@ -2076,11 +2223,16 @@ SRB_KI_PART0(SRB_NMPC_KERNEL)
 SRB_KI_PART1(SRB_NMPC_KERNEL)
 #elif SRB_PART == 2
 SRB_KI_PART2(SRB_NMPC_KERNEL)
+SRB_KF32_PART2(SRB_NMPC_KERNEL_F32)
 #else
 SRB_KI_PART3(SRB_NMPC_KERNEL)
+SRB_KF32_PART3(SRB_NMPC_KERNEL_F32)
 #endif
 #else
 SRB_KERNEL_INSTANCES(SRB_NMPC_KERNEL)
+#ifndef SRB_DEV_INSTANCES
+SRB_KF32_INSTANCES(SRB_NMPC_KERNEL_F32)
+#endif
 #endif
 
 #if !defined(SRB_PART) || SRB_PART == 0

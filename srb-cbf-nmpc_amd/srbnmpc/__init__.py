@@ -33,7 +33,8 @@ OPTIMAL, KKTFAIL, MAXIT, FATAL, ACCEPTABLE = 0, 1, 2, 3, 4
 QP_WARM = 4
 # srb_ctx_set_option codes (SRB_OPT_* of include/srbnmpc.h)
 OPTIONS = {"polish": 1, "polish_rho": 2, "polish_waves": 3, "grid_min_rows": 4, "grid_min_rows_static": 5,
-           "polish_fused": 6, "last_polish": 7, "timing": 8, "qp_warm_tol": 9, "selection": 10}
+           "polish_fused": 6, "last_polish": 7, "timing": 8, "qp_warm_tol": 9, "selection": 10,
+           "kkt_fp32_mu": 11, "kkt_fp32_refine": 12, "last_kkt_fp32": 13}
 ABI_VERSION = 5                                               # SRB_ABI_VERSION of include/srbnmpc.h
 
 

@@ -25,7 +25,8 @@ it = out['iters'][0]
 names = {0: 'setup', 1: 'qp-init', 2: 'nlp-init', 18: 'resid loop', 3: 'resid reduce', 16: 'weights', 17: 'P: rhs',
          4: 'gram', 5: 'factor (GJ)', 6: 'P: rhs', 7: 'P: rmul', 8: 'P: solve', 21: 'P: Jdx', 9: 'P: steplen',
          10: 'rho + C: rhs', 11: 'C: rmul', 12: 'C: solve', 22: 'C: Jdx', 13: 'C: steplen', 19: 'update: s z',
-         20: 'update: x rx', 14: 'update: hess', 15: 'output'}
+         20: 'update: x rx', 14: 'update: hess', 15: 'output', 23: 'setup: inputs', 24: 'setup: obstacles',
+         25: 'setup: basis', 26: 'fused polish'}
 periter = set(range(3, 15)) | set(range(16, 23))
 print(f"agent0 iters qp={it[0]} nlp={it[1]}; kernel ms {s.last_kernel_ms()[1]:.4f}")
 tot_all = v.sum()
