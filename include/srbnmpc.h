@@ -383,7 +383,10 @@ int srb12_nv(const srb12_params *p);   /* 24N + 1: X = x_1..x_N (12N) | U = u_0.
  *   RR RL); contact [A][N][4] int (1 stance); obstacles / nbr_state / n_obs / n_all / agent_offset /
  *   sel / obstacles_version as in srb_batch (the neighbour snapshot rows are [x, y, xdot, ydot]);
  *   outputs x_qp (may be NULL), x [A][24N+1], obj [A], status [A][2], iters [A][2]; a FATAL (3) QP stage ends the
- *   solve before the NLP stage, whose status then reads FATAL as well (use_nlp = 1) */
+ *   solve before the NLP stage, whose status then reads FATAL as well (use_nlp = 1).
+ *   status codes 0..3 as iSWIFT's; 4 by stage: the LAST stage (the NLP, or the QP when use_nlp = 0) converged but
+ *   its polish was rejected (the interior-point result is returned); the QP stage followed by the NLP converged at
+ *   tol_qp only (QP_WARM, x_qp is the NLP's warm start); with use_nlp = 0 status[1] and iters[1] read 0 */
 typedef struct srb12_batch {
     int struct_size;              /* sizeof(srb12_batch) (ABI check) */
     const double *x0, *xref, *foot;

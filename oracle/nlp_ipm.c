@@ -164,13 +164,16 @@ static void build_Z(const orc_params *pp, const double *foot, double *Z, int n, 
 #define ORC_POLISH_DX1 1e-4       /* a Newton step this small whose active rows then hold to CTOL ends the pass */
 #define ORC_POLISH_CTOL 1e-10
 
+/* The polish and exit constants below are read from the environment only in a diagnostics build of the
+ * oracle (-DORC_DIAG_ENV): the library the tests load computes the same results whatever the
+ * environment holds (tests/test_oracle.py test_oracle_environment_does_not_change_the_numerics). */
 static double g_polish_rho = ORC_POLISH_RHO;
 static double g_polish_kappa = 1e4;
 static int g_polish_zinit = 1;    /* exploration: 1 = a later pass starts from the previous pass's z_A */
-int orc_early_stats[2];
+int orc_early_stats[2];          /* exploration counters: early polish attempts failed / accepted */
 unsigned long long orc_polish_stat_max[2];   /* exploration: the largest reduced stationarity / scale of an accepted (0) /
                                                 rejected (1) pass, as the bits of a non-negative double (ordered as the values) */
-int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */          /* exploration counters: early polish attempts failed / accepted */
+int orc_polish_stats[16];        /* exploration counters: [0] rejected, [1 + p] accepted after pass p */
 static int g_polish_it = ORC_POLISH_IT, g_polish_passes = ORC_POLISH_PASSES;
 static double g_polish_omcap = ORC_POLISH_OMCAP;
 
@@ -424,7 +427,9 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     /* diagnostics: ORC_NLP_EXIT="fx fmu acc" scales the dual-residual threshold, the
      * complementarity threshold and the ACCEPTABLE window (exploration of exit rules only) */
     double fx = ORC_NLP_EXITF, fmu = ORC_NLP_EXITF, facc = 100.0, fdx = ORC_NLP_DXTOL;
+#ifdef ORC_DIAG_ENV
     if (getenv("ORC_NLP_EXIT")) sscanf(getenv("ORC_NLP_EXIT"), "%lf %lf %lf %lf", &fx, &fmu, &facc, &fdx);
+#endif
     double dxlast = 1e300;                                  /* max |ap dx| of the last update */
     int npassed = 0;                                        /* near-optimal iterates so far */
     int saved = 0, restore = 0;                             /* best near-optimal iterate */
@@ -432,11 +437,15 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
     int provisional = 0;
     double *xsave = malloc(sizeof(double) * n), *ssave = malloc(sizeof(double) * m), *zsave = malloc(sizeof(double) * m);
     int nearwait = ORC_NLP_NEARWAIT;
+#ifdef ORC_DIAG_ENV
     if (getenv("ORC_NLP_NEARWAIT")) nearwait = atoi(getenv("ORC_NLP_NEARWAIT"));
+#endif
     double tr_sigma = 0.0;
     double early_mu = 0.0, early_rz = 1e300;
     int early_tried = 0, early_done = 0;
+#ifdef ORC_DIAG_ENV
     if (getenv("ORC_NLP_EARLY")) sscanf(getenv("ORC_NLP_EARLY"), "%lf %lf %lf", &early_mu, &early_rz, &fdx);
+#endif
     double *xe = malloc(sizeof(double) * n), *ze = malloc(sizeof(double) * m);
     for (int iter = 0; iter < pp->nlp_maxit; iter++) {
         rows_eval(&P, x, g, Jv, Ji);
@@ -585,12 +594,14 @@ int orc_nlp_solve(const orc_params *pp, const double x0[4], const double *foot,
         memcpy(x, xsave, sizeof(double) * n); memcpy(s, ssave, sizeof(double) * m); memcpy(z, zsave, sizeof(double) * m);
         flag = 4;
     }
+#ifdef ORC_DIAG_ENV
     if (getenv("ORC_POLISH_RHO")) g_polish_rho = atof(getenv("ORC_POLISH_RHO"));
     if (getenv("ORC_POLISH_ZINIT")) g_polish_zinit = atoi(getenv("ORC_POLISH_ZINIT"));
     if (getenv("ORC_POLISH_KAPPA")) g_polish_kappa = atof(getenv("ORC_POLISH_KAPPA"));
     if (getenv("ORC_POLISH_IT")) g_polish_it = atoi(getenv("ORC_POLISH_IT"));
     if (getenv("ORC_POLISH_PASSES")) g_polish_passes = atoi(getenv("ORC_POLISH_PASSES"));
     if (getenv("ORC_POLISH_OMCAP")) g_polish_omcap = atof(getenv("ORC_POLISH_OMCAP"));
+#endif
     const int do_polish = pp->polish;   /* orc_params.polish (a parameter, not the environment: ADVICE r04) */
     if (do_polish && !early_done && (flag == 0 || flag == 4 || flag == 2) && polish(&P, hh, Z, nz, x, s, z, trace)) flag = 0;
     free(xe); free(ze);

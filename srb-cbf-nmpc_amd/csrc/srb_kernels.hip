@@ -1639,6 +1639,9 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                     __hip_atomic_fetch_add(&CF[Q[t].r], Q[t].m[0] * Q[t].z[0] - Q[t].m[1] * Q[t].z[1], __ATOMIC_RELAXED,
                                            __HIP_MEMORY_SCOPE_WORKGROUP);
             SYNC();
+            // the first write of ZZ: the obstacle positions it may alias (SRB_OBS_IN_ZZ) were read by the slots'
+            // setup above, and until here every ZZ operand was scaled by a zero shift, never read (gj_load / la_solve
+            // test delta != 0; the LDS-check build asserts it, bit 7)
             gram_rhs<NZL, true, NW>(R, W, CF, cnt, OF, nko, ZZ, vg, nz, tid, part, bmask);
             SYNC();
             gj_load<NZL, NZE>(Mi, ZZ, ZZ, 0.0, nz, lane);
@@ -1847,6 +1850,8 @@ __device__ __forceinline__ void nmpc_agent(const SrbKParams &prm, int agent,
                         const double dm = (lane < nz) ? H0[lane * LDH + lane] : 1.0;
                         dstart = 1e-10 * fmax(1.0, wmax(dm));
                     }
+                    // the QP stage never shifts: ZZ may still hold the obstacle positions there (SRB_OBS_IN_ZZ)
+                    LCK(nl || delta == 0.0, 7);
                     gj_load<NZL, NZE>(Mi, H0, ZZ, delta, nz, lane);    // H0 + delta Z'Z (the solves shift on the fly too)
                     // KF instances: the inverse in fp32 while mu > kkt32_mu (then nref fp64 refinement steps per solve)
                     const int cf = (KF && f32) ? gj_invert_f32<NZL>(Mi, mrow<NZL>(lane), !nl) : gj_reduced<NZL, NZE>(Mi, nz, lane, !nl);

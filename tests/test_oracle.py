@@ -289,3 +289,29 @@ def test_oracle_qp_warm_tolerance_leaves_the_nlp_result(name):
     xus = np.r_[0:6 * N, (6 + C) * N]
     assert np.abs(w["x"][both][:, xus] - f["x"][both][:, xus]).max() < 1e-7
     assert w["iters"][:, 0].mean() < f["iters"][:, 0].mean() - 1.0
+
+
+def test_oracle_environment_does_not_change_the_numerics():
+    """the oracle the parity tests compare against reads its polish and exit constants from the
+    environment only in a diagnostics build (-DORC_DIAG_ENV); the built liboracle.so holds none of those names,
+    and a solve under extreme values of them equals the plain solve bit for bit (only ORC_*_TRACE remains:
+    stderr output, no numerics)."""
+    import subprocess
+    import sys
+    blob = open(oracle._LIB, "rb").read()
+    names = (b"ORC_POLISH_RHO", b"ORC_POLISH_ZINIT", b"ORC_POLISH_KAPPA", b"ORC_POLISH_IT", b"ORC_POLISH_PASSES",
+             b"ORC_POLISH_OMCAP", b"ORC_NLP_EXIT", b"ORC_NLP_NEARWAIT", b"ORC_NLP_EARLY")
+    for name in names:
+        assert name not in blob, name
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    code = ("import sys, hashlib; sys.path[:0] = sys.argv[1:3]; import oracle; from srbnmpc import workload; "
+            "b = workload.make_batch(16, 10, 2, seed=2); "
+            "r = oracle.solve_batch(oracle.params(10, 2, K_obs=3, K_nbr=8), b['x0'], b['ref'], b['foot'], "
+            "b['obstacles'], b['nbr_state'], nthreads=1); "
+            "print(hashlib.sha256(r['x'].tobytes() + r['status'].tobytes()).hexdigest())")
+    argv = [sys.executable, "-c", code, root, os.path.join(root, "srb-cbf-nmpc_amd")]
+    env = {k: v for k, v in os.environ.items() if not k.startswith("ORC")}
+    plain = subprocess.run(argv, env=env, capture_output=True, text=True, check=True).stdout
+    stray = dict(env, ORC_POLISH_IT="0", ORC_POLISH_PASSES="0", ORC_POLISH_OMCAP="1e3", ORC_POLISH_RHO="1",
+                 ORC_NLP_EXIT="1e3 1e3 1e3 1", ORC_NLP_NEARWAIT="0", ORC_NLP_EARLY="1 1 1")
+    assert subprocess.run(argv, env=stray, capture_output=True, text=True, check=True).stdout == plain

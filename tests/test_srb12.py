@@ -257,6 +257,55 @@ def test_srb12_oracle_polish_exact_without_obstacle_rows():
     assert np.abs(r["x"][:, 12 * Nh:24 * Nh] - t["x"][:, 12 * Nh:24 * Nh]).max() < 1e-5
 
 
+def _rejected_polish_batch():
+    """QP stage alone (use_nlp = 0) stopped at tol = tol_final = 1 with force bounds of 1 N: the interior-point
+    point is too loose for the polish on about a third of the agents (a rejected last-stage polish
+    reads 4, whichever stage is last)."""
+    b = workload.make_batch12(64, N, "stand", seed=23)
+    return b, dict(tol=1.0, tol_final=1.0, fmax=1.0)
+
+
+def test_srb12_oracle_qp_only_rejected_polish_reads_4():
+    """with use_nlp = 0 the QP stage is the last stage; a rejected polish returns the
+    interior-point result with status[0] = 4, and status[1] / iters[1] read 0 (include/srbnmpc.h srb12_batch)."""
+    b, kw = _rejected_polish_batch()
+    p = oracle.params12(N, K_obs=3, K_nbr=8, use_nlp=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    rej = r["status"][:, 0] == 4
+    assert 0 < rej.sum() < len(rej) and np.isin(r["status"][:, 0], (0, 4)).all()
+    assert (r["status"][:, 1] == 0).all() and (r["iters"][:, 1] == 0).all()
+    p.polish = 0      # without the polish the same agents end OPTIMAL at the interior-point result
+    r0 = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    assert (r0["status"][:, 0] == 0).all()
+    np.testing.assert_array_equal(r["x"][rej], r0["x"][rej])
+
+
+@pytest.mark.gpu
+def test_srb12_gpu_qp_only_rejected_polish_reads_4():
+    """The kernel's counterpart: status 4 on the rejected-polish agents, their interior-point result as the
+    oracle's (forces to 1e-4 N), and every other agent OPTIMAL at the oracle's polished point."""
+    _gpu()
+    b, kw = _rejected_polish_batch()
+    A = b["x0"].shape[0]
+    p = oracle.params12(N, K_obs=3, K_nbr=8, use_nlp=0)
+    g = srb12.default_params(N, K_obs=3, K_nbr=8, use_nlp=0)
+    for k, v in kw.items():
+        setattr(p, k, v)
+        setattr(g, k, v)
+    s = srb12.Solver12(g, A)
+    out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    s.close()
+    r = oracle.solve_batch12(p, b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
+    assert (out["status"][:, 0] == 4).any() and np.isin(out["status"][:, 0], (0, 4)).all()
+    assert (out["status"][:, 1] == 0).all() and (out["iters"][:, 1] == 0).all()
+    same = out["status"][:, 0] == r["status"][:, 0]
+    assert same.sum() >= A - 2, (out["status"][:, 0], r["status"][:, 0])   # a polish decision at its threshold
+    np.testing.assert_allclose(out["x"][same][:, :12 * N], r["x"][same][:, :12 * N], atol=1e-6)
+    np.testing.assert_allclose(out["x"][same][:, 12 * N:], r["x"][same][:, 12 * N:], atol=1e-4)
+
+
 def test_srb12_params_defaults_match_oracle():
     """srb12_params_default (C ABI, no GPU) == the oracle's defaults; reference constants."""
     pg = srb12.default_params(N)
