@@ -42,12 +42,14 @@
 #ifndef SRB12_REFINE                  // 0: no iterative refinement at all (A/B builds)
 #define SRB12_REFINE 1
 #endif
-#ifdef SRB12_REFINE2_MU               // diagnostic builds: a second refinement step of the corrector once mu < this
-#ifndef SRB_DIAG_BUILD
-#error "SRB12_REFINE2_MU is a diagnostic-build option"
-#endif
-#else
-#define SRB12_REFINE2_MU 0.0
+// a second refinement step of the corrector's solve once mu < this (round 6): below
+// s'z/m ~ 1e-9 the barrier weights z/s reach 1e10 and one step left the corrector at the Riccati solve's
+// round-off floor (|r_d| 4e-6 -> 4e-3, the iterate wandering into MAXIT on 3 of 1024 stand agents at tol_final
+// 1e-9, 20 at 1e-10); with the second step every agent converges at 1e-9 and 1e-10 (profiles/r06_s12_tolfinal.txt).
+// At the default tol_final 1e-8 it never runs (results identical).  The correctly rounded 1/sqrt pivot
+// (SRB12_EXACT_RSQ) was not the cause: alone it changes nothing.
+#ifndef SRB12_REFINE2_MU
+#define SRB12_REFINE2_MU 1e-8
 #endif
 #ifndef SRB12_REFINE_MU               // the corrector's solve is refined once mu < this
 #define SRB12_REFINE_MU 1e-3

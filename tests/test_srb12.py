@@ -236,9 +236,10 @@ def test_srb12_oracle_polish_equals_independent_exact_optimum(gait):
     assert _opt(r["status"]).all()
     for a in range(A):
         xe = _exact_active_set_optimum(p, b, a, t["x"][a])
-        # (the reference is exact, or the tight run's own point when that certifies: then within 1e-7 N)
+        # (the reference is exact, or the tight run's own point when that certifies: then within 1e-7 N).
+        # Measured (round 6, seed 21): forces to 1.3e-8 N (trot) / 2.9e-7 N (stand), X to 6e-11 / 2.5e-10
         assert np.abs(r["x"][a, 12 * N:24 * N] - xe[12 * N:24 * N]).max() < 1e-6
-        assert np.abs(r["x"][a, :12 * N] - xe[:12 * N]).max() < 1e-7
+        assert np.abs(r["x"][a, :12 * N] - xe[:12 * N]).max() < 1e-9
 
 
 def test_srb12_oracle_polish_exact_without_obstacle_rows():
@@ -479,23 +480,27 @@ def test_srb12_tables_shorter_than_k_vs_oracle(n_obs, n_all):
 
 
 @pytest.mark.gpu
-@pytest.mark.parametrize("gait", ["stand", "trot"])
-def test_srb12_gpu_forces_within_1e4_of_exact_optimum_1024(gait):
+@pytest.mark.parametrize("gait,tol_final", [("stand", 1e-8), ("trot", 1e-8), ("stand", 1e-9)])
+def test_srb12_gpu_forces_within_1e4_of_exact_optimum_1024(gait, tol_final):
     """VERDICT r04 item 2, the north star's GRF clause on a whole 1024-agent batch: every agent the GPU
     reports OPTIMAL has its forces within 1e-4 N of the exact optimum -- the tight interior-point run
     (s'z/m < 1e-11, no polish) where that run converges, the independent numpy active-set solve
     (_exact_active_set_optimum) where it stops at its round-off floor (~1.5 % of stand agents, up to
     1e-4 N off there) and on a sample of 48 more agents, to 1e-6 N.  A rejected polish reads
-    ACCEPTABLE (4), never OPTIMAL; at most 0.5 % of the agents may end so."""
+    ACCEPTABLE (4), never OPTIMAL; at most 0.5 % of the agents may end so.  VERDICT r05 item 4: at tol_final 1e-9
+    (below the round-5 Riccati floor) no agent may run into MAXIT."""
     _gpu()
     A = 1024
     b = workload.make_batch12(A, N, gait, seed=21)
     p = oracle.params12(N, K_obs=3, K_nbr=8)
-    s = srb12.Solver12(srb12.default_params(N, K_obs=3, K_nbr=8), A)
+    g = srb12.default_params(N, K_obs=3, K_nbr=8)
+    g.tol_final = tol_final
+    s = srb12.Solver12(g, A)
     out = s.solve(b["x0"], b["xref"], b["foot"], b["contact"], b["obstacles"], b["nbr_state"])
     s.close()
     opt = _opt(out["status"])
     assert np.isin(out["status"][:, 1], (0, 4)).all() and opt.mean() >= 0.995, np.bincount(out["status"][:, 1])
+    assert out["iters"][:, 1].max() < g.nlp_maxit
     U = out["x"][:, 12 * N:24 * N]
     t = _tight(p, b)
     tok = _opt(t["status"])
