@@ -307,9 +307,9 @@ def srb12_executed_flops(N, K, iters):
 
 def traffic_from(name, agents):
     """roofline.traffic of a non-default path: hbm bytes per launch of its PMC summary
-    (tools/pmc_traffic.py, profiles/r05_pmc_traffic_<name>.json; the LL kernel, unchanged since,
-    also r04's and r03's) when it matches the batch."""
-    for rnd in ("r05", "r04", "r03") if name == "ll" else ("r05",):
+    (tools/pmc_traffic.py, profiles/r06_pmc_traffic_<name>.json, else round 5's; the LL kernel, unchanged
+    since, also r04's and r03's) when it matches the batch."""
+    for rnd in ("r06", "r05", "r04", "r03") if name == "ll" else ("r06", "r05"):
         f = os.path.join(ROOT, "profiles", f"{rnd}_pmc_traffic_{name}.json")
         try:
             tj = json.load(open(f))
@@ -500,7 +500,7 @@ def main():
                     help="diagnostic: solve rank 0's shard of a swarm this many GPUs wide on one GPU (the whole "
                          "neighbour snapshot and obstacle arena of that swarm, no collective)")
     ap.add_argument("--traffic-json", default=None,
-                    help="PMC summary (tools/pmc_traffic.py); default profiles/r05_pmc_traffic_c<config>.json")
+                    help="PMC summary (tools/pmc_traffic.py); default profiles/r06_pmc_traffic_c<config>.json, else r05's")
     ap.add_argument("--lib", default=None,
                     help="diagnostics: time the variant build libsrbnmpc_<tag>.so instead of the product library")
     ap.add_argument("--plumbing", action="store_true",
@@ -636,8 +636,10 @@ def main():
     cyc_iter = solve_ms * 1e-3 * SCLK_GHZ * 1e9 / max(1, int(iters.sum(1).max()))
     traffic = traffic_polish = None
     fused = solver.polish_fused_active()
-    if args.traffic_json is None:
-        args.traffic_json = os.path.join(ROOT, "profiles", f"r05_pmc_traffic_c{args.config}.json")
+    if args.traffic_json is None:           # this round's PMC summary of the config, else round 5's
+        args.traffic_json = next((f for f in (os.path.join(ROOT, "profiles", f"{r}_pmc_traffic_c{args.config}.json")
+                                              for r in ("r06", "r05")) if os.path.exists(f)),
+                                 os.path.join(ROOT, "profiles", f"r06_pmc_traffic_c{args.config}.json"))
     if os.path.exists(args.traffic_json):
         try:
             tj = json.load(open(args.traffic_json))
@@ -674,7 +676,7 @@ def main():
                      "cycles_per_iter": cyc_iter,
                      "cycles_per_iter_note": "solve-kernel HIP-event time x 2.4 GHz / IPM iterations (QP + NLP) of "
                                              "the slowest agent: the critical-path cost of one iteration; per-phase "
-                                             "split in profiles/r05_*_stamps.txt",
+                                             "split in profiles/r06_c3_stamps.txt (r05_*_stamps.txt)",
                      "kernel": "srb_nmpc_kernel", "waves_per_agent": solver.waves(), "kernel_ms": solve_ms, "knn_ms": float(np.median([k[0] for k in kern])),
                      "flop_model": "executed fp64 flops of the condensed IPM (bench.executed_flops, DESIGN.md 6) over "
                                    "the fp64 peak; the kernel is latency-bound (dependent FMA / cross-lane chains per "
