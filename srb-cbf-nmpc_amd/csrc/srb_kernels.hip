@@ -2278,6 +2278,20 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
                           gnb, onb, pnb, inb);
         return;
     }
+    // one table (srb_select_device's passes, or a batch without neighbour rows): a table that one wave scans
+    // with the threshold pass (knn_thresh) or through a grid runs on wave 0 alone -- the two-wave form pays two
+    // barriers per pop round (round 6: the neighbour pass of the multi-GPU step 19.3 us with both waves)
+    if (SRB_KNN_WAVES == 2 && (K_obs > 0) != (K_nbr > 0)) {
+        const bool o = K_obs > 0;
+        const SrbGrid *g = o ? gob : gnb;
+        if ((o ? n_obs : n_all) <= 64 * SRB_KNN_RB || (g && g->ok)) {
+            if (tid >= 64) return;                     // whole wave: no barrier follows on the one-wave path
+            if (o) knn_select<1>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds, gob, oob, pob, iob);
+            else knn_select<1>(tid, px, py, nbr_state, 4, n_all, agent_offset + agent, K_nbr, 0, sel + K_obs, wd_lds, wi_lds,
+                               gnb, onb, pnb, inb);
+            return;
+        }
+    }
     if (K_obs > 0)
         knn_select<SRB_KNN_WAVES>(tid, px, py, obstacles, 2, n_obs, -1, K_obs, 1, sel, wd_lds, wi_lds, gob, oob, pob, iob);
     if (K_nbr > 0)

@@ -371,6 +371,32 @@ __device__ __forceinline__ void wargmin(double &d, int &idx)
     d = a; idx = (int)i32[0]; lexmin(d, idx, b, (int)i32[1]);
 }
 
+// The same (d, index) lexicographic wave argmin as wargmin, by a double minimum and a ballot (round 6,
+// tools/ubench/knn_phase.hip): one fmin per stage instead of the pair's three compares and three selects;
+// the index comes from the one lane holding the minimum (v_readlane), or -- when several lanes hold it: an
+// exact distance tie, or every head exhausted (+inf) -- from an integer minimum over those lanes' indices.
+// Every lane ends with the same (d, idx).  d is never NaN here (knn_select_k offers no NaN keys).
+__device__ __forceinline__ int wmin_i(int v)
+{
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0xB1, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x4E, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x141, 0xf, 0xf, false));
+    v = min(v, __builtin_amdgcn_update_dpp(0, v, 0x140, 0xf, 0xf, false));
+    auto p16 = __builtin_amdgcn_permlane16_swap((unsigned)v, (unsigned)v, false, false);
+    v = min((int)p16[0], (int)p16[1]);
+    auto p32 = __builtin_amdgcn_permlane32_swap((unsigned)v, (unsigned)v, false, false);
+    return min((int)p32[0], (int)p32[1]);
+}
+__device__ __forceinline__ void wargmin_b(double &d, int &idx)
+{
+    const double m = wmin(d);
+    const unsigned long long tie = __ballot(d == m);
+    int w;
+    if (__popcll(tie) == 1) w = __builtin_amdgcn_readlane(idx, __ffsll((long long)tie) - 1);
+    else w = wmin_i((d == m) ? idx : 0x7fffffff);
+    d = m; idx = w;
+}
+
 // wargmin over the NW waves of the workgroup: per-wave DPP argmin, lane 0 of every wave
 // publishes (d, idx) to scr[2 NW], every thread combines the partials in wave order
 template <int NW>
@@ -396,6 +422,12 @@ struct SrbGrid {
     int ok;                        // 0: not built (brute-force scan)
 };
 
+// rows a lane holds in registers on the thresholded brute-force path of knn_select_k (larger tables: the
+// batched scan); 32: the neighbour snapshot of a 2048-agent shard on one wave
+#ifndef SRB_KNN_RB
+#define SRB_KNN_RB 32
+#endif
+
 // per-lane insertion of candidate (cd = sqrt distance, ci = row) into the sorted top-K
 // (bd, bi), ordered lexicographically by (distance, index)
 template <int KM>
@@ -407,6 +439,55 @@ __device__ __forceinline__ void knn_insert(double (&bd)[KM], int (&bi)[KM], doub
         const double td = bd[j]; const int ti = bi[j];
         bd[j] = lt ? cd : td; bi[j] = lt ? ci : ti;
         cd = lt ? td : cd; ci = lt ? ti : ci;
+    }
+}
+
+// The thresholded brute-force pass of knn_select_k (round 6) over a table of at most RB rows a lane: every
+// row's d^2 kept in registers (row tid + r STEP in slot r; NaN for the agent itself, rows past the table and
+// rows with NaN coordinates, which are never selected), then a bound T on the K-th smallest d^2 from the lanes'
+// minima -- the K-th smallest of them: at least K rows of this wave lie within it -- and only the rows with
+// d^2 <= T (1 + 1e-14) (the filter's padding: a row beyond cannot round to a sqrt at or below the K-th's)
+// enter the lanes' sorted lists, each lane taking its candidates one per trip.  The per-row insertion was
+// three quarters of the neighbour scan (tools/ubench/knn_phase.hip); configs[2] selection 20.6 -> 14.5 us.
+template <int KM, int RB, int STEP>
+__device__ __forceinline__ void knn_thresh(int tid, double px, double py, const double *__restrict__ tab, int stride,
+                                           int n_rows, int self, int K, double (&bd)[KM], int (&bi)[KM])
+{
+#pragma clang fp contract(off)
+    double key[RB];
+#pragma unroll
+    for (int r = 0; r < RB; r++) {
+        const int i = tid + r * STEP;
+        const bool in = i < n_rows;
+        const double tx = in ? tab[(size_t)stride * i] : 0.0, ty = in ? tab[(size_t)stride * i + 1] : 0.0;
+        const double dx = px - tx, dy = py - ty;
+        key[r] = (in && i != self) ? dx * dx + dy * dy : __builtin_nan("");
+    }
+    double lm = __builtin_inf();
+#pragma unroll
+    for (int r = 0; r < RB; r++) lm = fmin(lm, key[r]);      // NaN keys ignored
+    double T = __builtin_inf();
+    for (int cnt = 0; cnt < K;) {                  // uniform: every lane holds the same t
+        const double t = wmin(lm);
+        if (!(t < __builtin_inf())) { T = __builtin_inf(); break; }
+        cnt += __popcll(__ballot(lm == t));
+        T = t;
+        lm = (lm == t) ? __builtin_inf() : lm;
+    }
+    const double wT = (T < __builtin_inf()) ? T * (1.0 + 1e-14) : __builtin_inf();
+    unsigned long long cm = 0;
+#pragma unroll
+    for (int r = 0; r < RB; r++)
+        if (key[r] <= wT) cm |= 1ull << r;         // NaN keys fail
+    while (__ballot(cm != 0)) {
+        if (cm) {
+            const int rr = __ffsll((long long)cm) - 1;
+            cm &= cm - 1;
+            double kd = key[0];
+#pragma unroll
+            for (int r = 1; r < RB; r++) kd = (rr == r) ? key[r] : kd;
+            knn_insert<KM>(bd, bi, sqrt(kd), tid + rr * STEP, K);
+        }
     }
 }
 
@@ -515,9 +596,19 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
             }
         }
     }
+    if (!done && n_rows <= STEP * SRB_KNN_RB) {
+        // ---- brute force with a threshold (knn_thresh), as many register slots as the table needs
+        if (n_rows <= STEP * 4) knn_thresh<KM, 4, STEP>(tid, px, py, tab, stride, n_rows, self, K, bd, bi);
+        else if (n_rows <= STEP * 16) knn_thresh<KM, 16, STEP>(tid, px, py, tab, stride, n_rows, self, K, bd, bi);
+        else knn_thresh<KM, SRB_KNN_RB, STEP>(tid, px, py, tab, stride, n_rows, self, K, bd, bi);
+        done = true;
+    }
     if (!done) {
         // ---- brute force: KNN_U rows per lane per batch, all loads issued before the first use
-        constexpr int KNN_U = 4;
+#ifndef SRB_KNN_U
+#define SRB_KNN_U 4
+#endif
+        constexpr int KNN_U = SRB_KNN_U;
         for (int i0 = tid; i0 < n_rows; i0 += KNN_U * STEP) {
             double tx[KNN_U], ty[KNN_U];
 #pragma unroll
@@ -538,7 +629,7 @@ __device__ __forceinline__ void knn_select_k(int tid, double px, double py, cons
 #pragma clang loop unroll(disable)
     for (int j = 0; j < K; j++) {
         double d = bd[0]; int idx = bi[0];
-        wargmin(d, idx);
+        wargmin_b(d, idx);
         if (KW > 1) {
             if (lane == 0) { wd_lds[wv] = d; wi_lds[wv] = idx; }
             __syncthreads();

@@ -71,6 +71,40 @@ __global__ void __launch_bounds__(64) kp(int n_agents, const double *x0g, const 
     if (lane == 0) { cyc[2 * agent] = t1 - t0; cyc[2 * agent + 1] = t2 - t1; }
 }
 
+// round 6: the product's functions (srb_wave.h knn_thresh + the ballot-argmin pop rounds), stamped between
+// them; BITS 1: skip the pop rounds
+template <int BITS>
+__global__ void __launch_bounds__(64) kq(int n_agents, const double *x0g, const double *tab, int n_rows, int K, int *sel_out,
+                                         unsigned long long *cyc)
+{
+    const int agent = blockIdx.x, lane = threadIdx.x;
+    int *sel = sel_out + (size_t)agent * 8;
+    const unsigned long long t0 = __builtin_amdgcn_s_memtime();
+    const double px = x0g[4 * (size_t)agent], py = x0g[4 * (size_t)agent + 2];
+    double bd[8]; int bi[8];
+#pragma unroll
+    for (int j = 0; j < 8; j++) { bd[j] = __builtin_inf(); bi[j] = 0x7fffffff; }
+    knn_thresh<8, 16, 64>(lane, px, py, tab, 4, n_rows, agent, K, bd, bi);
+    const unsigned long long t1 = __builtin_amdgcn_s_memtime();
+    int mine = -1;
+    if (!(BITS & 1)) {
+#pragma clang loop unroll(disable)
+        for (int j = 0; j < K; j++) {
+            double d = bd[0]; int idx = bi[0];
+            wargmin_b(d, idx);
+            if (bi[0] == idx) {
+#pragma unroll
+                for (int t = 0; t + 1 < 8; t++) { bd[t] = bd[t + 1]; bi[t] = bi[t + 1]; }
+                bd[7] = __builtin_inf(); bi[7] = 0x7fffffff;
+            }
+            if (lane == j) mine = idx;
+        }
+    } else mine = bi[0];
+    const unsigned long long t2 = __builtin_amdgcn_s_memtime();
+    if (lane < K) sel[lane] = mine;
+    if (lane == 0) { cyc[2 * agent] = t1 - t0; cyc[2 * agent + 1] = t2 - t1; }
+}
+
 #define CK(x) do { hipError_t e = (x); if (e != hipSuccess) { printf("%s\n", hipGetErrorString(e)); return 1; } } while (0)
 template <int MODE, int U>
 int run(const char *name, int A, double *x0, double *tab, int n, int *sel, unsigned long long *cyc)
@@ -82,6 +116,29 @@ int run(const char *name, int A, double *x0, double *tab, int n, int *sel, unsig
     for (int r = 0; r < 50; r++) {
         (void)hipEventRecord(a, 0);
         hipLaunchKernelGGL((kp<MODE, U>), dim3(A), dim3(64), 0, 0, A, x0, tab, n, 8, sel, cyc);
+        (void)hipEventRecord(b, 0); (void)hipEventSynchronize(b);
+        float ms = 0; (void)hipEventElapsedTime(&ms, a, b);
+        best = ms < best ? ms : best;
+    }
+    std::vector<unsigned long long> h(2 * A);
+    CK(hipMemcpy(h.data(), cyc, 2 * A * 8, hipMemcpyDeviceToHost));
+    double s1 = 0, s2 = 0, m1 = 0;
+    for (int i = 0; i < A; i++) { s1 += h[2 * i]; s2 += h[2 * i + 1]; m1 = h[2 * i] > m1 ? h[2 * i] : m1; }
+    printf("%-34s best %7.2f us   scan %8.0f (max %8.0f) pop %7.0f memtime ticks/wave\n", name, best * 1000.0f,
+           s1 / A, m1, s2 / A);
+    return 0;
+}
+
+template <int BITS>
+int runq(const char *name, int A, double *x0, double *tab, int n, int *sel, unsigned long long *cyc)
+{
+    hipEvent_t a, b; (void)hipEventCreate(&a); (void)hipEventCreate(&b);
+    for (int i = 0; i < 5; i++) hipLaunchKernelGGL((kq<BITS>), dim3(A), dim3(64), 0, 0, A, x0, tab, n, 8, sel, cyc);
+    CK(hipDeviceSynchronize());
+    float best = 1e9f;
+    for (int r = 0; r < 50; r++) {
+        (void)hipEventRecord(a, 0);
+        hipLaunchKernelGGL((kq<BITS>), dim3(A), dim3(64), 0, 0, A, x0, tab, n, 8, sel, cyc);
         (void)hipEventRecord(b, 0); (void)hipEventSynchronize(b);
         float ms = 0; (void)hipEventElapsedTime(&ms, a, b);
         best = ms < best ? ms : best;
@@ -118,5 +175,7 @@ int main()
     if (run<4, 4>("no pop rounds", A, x0, tab, n, sel, cyc)) return 1;
     if (run<8, 4>("no table loads", A, x0, tab, n, sel, cyc)) return 1;
     if (run<8 | 2, 4>("no loads, no insertion", A, x0, tab, n, sel, cyc)) return 1;
+    if (runq<0>("round 6: knn_thresh + ballot pop", A, x0, tab, n, sel, cyc)) return 1;
+    if (runq<1>("round 6: knn_thresh only", A, x0, tab, n, sel, cyc)) return 1;
     return 0;
 }
