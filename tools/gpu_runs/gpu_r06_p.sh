@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, call p: selection with as many register slots as the table needs -- selection tests, per-table timing,
+# Round 6, call p: single-table selections on one wave -- selection tests, per-table timing,
 # bench A/B against the previous build (libsrbnmpc_base.so), alternating, same box.
 set -o pipefail
 mkdir -p gpurun_out

@@ -1,5 +1,5 @@
 #!/bin/bash
-# Round 6, call p: selection with as many register slots as the table needs -- selection tests, per-table timing,
+# Round 6, call q: the grid ring gathered in registers (not kept) -- selection tests, per-table timing,
 # bench A/B against the previous build (libsrbnmpc_thr.so), alternating, same box.
 set -o pipefail
 mkdir -p gpurun_out
