@@ -2266,7 +2266,8 @@ extern "C" __global__ void __launch_bounds__(64 * SRB_KNN_WAVES) srb_knn_kernel(
     int *sel = sel_out + (size_t)agent * sel_stride;
     if (SRB_KNN_WAVES == 2 && K_obs > 0 && K_nbr > 0) {
         // the two tables on the two waves at once, each selection wave-local (DPP argmins, no barrier):
-        // configs[2] selection 23.5 -> 20.9 us a step (HIP events, round 5); the same rows.  (Selecting
+        // configs[2] selection 23.5 -> 20.9 us a step (HIP events, round 5; round 6's thresholded scan and ballot
+        // argmin in srb_wave.h: 20.5 -> 13.4 us); the same rows.  (Selecting
         // inside the solve kernel's setup instead measured no faster at configs[2] -- the solve kernel
         // grew by what the launch saved -- and 4.6 % slower at N = 20, where four rounds of agents each
         // wait for their selection; round 5)
