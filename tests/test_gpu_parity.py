@@ -422,6 +422,46 @@ def test_knn_matches_bruteforce(Ko, Kn):
     np.testing.assert_allclose(xus(N, out["x"]), xus(N, r["x"]), atol=NLP_TOL, rtol=0)
 
 
+@pytest.mark.parametrize("n_tab", [5, 64, 256, 257, 1024, 1025, 2048, 2049, 5000])
+def test_knn_threshold_pass_table_sizes(n_tab):
+    """Round 6's thresholded scan (srb_wave.h knn_thresh: 4, 16 or 32 register slots a lane by the table's size,
+    the batched scan beyond 2048 rows) at every size boundary, through srb_select_device on one table and on both
+    (one wave each): the reference's order exactly (oracle.select_idx) -- with exact-distance ties (a table
+    snapped to a quarter-metre lattice around lattice-aligned agents), NaN rows, the agent's own row, and K
+    larger than the rows within reach."""
+    rng = np.random.default_rng(n_tab)
+    N, C, A = 10, 2, min(96, n_tab)                   # (the batch's agents are rows of the snapshot)
+    b = workload.make_batch(A, N, C, seed=40 + n_tab % 7)
+    x0 = b["x0"].copy()
+    x0[:, [0, 2]] = np.round(x0[:, [0, 2]] * 4) / 4
+    half = max(4.0, 0.5 * np.sqrt(n_tab))
+    tab = np.zeros((n_tab, 4))
+    tab[:, :2] = np.round(rng.uniform(-half, half, (n_tab, 2)) * 4) / 4 + x0[rng.integers(0, A, n_tab)][:, [0, 2]]
+    tab[:, 2:] = rng.normal(0, 0.2, (n_tab, 2))
+    off = int(rng.integers(0, n_tab - A + 1))
+    tab[off:off + A, 0] = x0[:, 0]; tab[off:off + A, 1] = x0[:, 2]   # the agents' own rows
+    nan_rows = np.setdiff1d(rng.choice(n_tab, max(1, n_tab // 50), replace=False), np.arange(off, off + A))
+    tab[nan_rows, :2] = np.nan                         # (never an agent's own row)
+    obs = tab[:, :2].copy()
+    dev = torch.device("cuda:0")
+    T = lambda v, dt=torch.float64: torch.as_tensor(np.ascontiguousarray(v), dtype=dt, device=dev)
+    for Ko, Kn in ((3, 0), (0, 8), (16, 0), (3, 8), (2, 12), (2, 4)):
+        if Ko > n_tab or Kn > n_tab - 1:
+            continue                                   # (tables shorter than K: test_knn_sentinel_and_missing_rows)
+        s = srbnmpc.BatchSolver(srbnmpc.default_params(N, C, K_obs=Ko, K_nbr=Kn), A)
+        ko, kn = s.n_selected(n_tab, n_tab)
+        sel = torch.full((A, ko + kn), -7, dtype=torch.int32, device=dev)
+        tables = (1 if Ko else 0) | (2 if Kn else 0)
+        s.select_device(T(x0), T(obs), T(tab), sel, tables=tables, agent_offset=off,
+                        stream=torch.cuda.current_stream(dev).cuda_stream)
+        torch.cuda.synchronize()
+        got = sel.cpu().numpy()
+        s.close()
+        op = oracle.params(N, C, K_obs=Ko, K_nbr=Kn)
+        want = np.array([oracle.select_idx(op, x0[a], obs, tab, off + a) for a in range(A)], np.int32).reshape(A, -1)
+        np.testing.assert_array_equal(got, want, err_msg=f"n_tab {n_tab} K {Ko}+{Kn}")
+
+
 @pytest.mark.parametrize("Ko,Kn", [(3, 8), (16, 16)])
 def test_knn_grid_matches_bruteforce(Ko, Kn):
     """Tables of SRB_GRID_MIN_ROWS (8192) rows or more go through the uniform selection grid
